@@ -1,0 +1,115 @@
+"""Build the gravsim native libraries in-tree.
+
+  libgravsim_cpu.so : g++ -O3 -fopenmp, host-only CPU engine + layout/IC helpers.
+  libgravsim_hip.so : hipcc --offload-arch=gfx950, kernels + Stepper runtime, links RCCL.
+  gravsim_bench     : standalone C++ driver (csrc/tools/gravsim_main.cpp), no Python needed.
+
+Outputs land in <package>/_native/ so they travel with the repo snapshot to the GPU box.
+Rebuilds only when a source or header is newer than the target. Usage:
+    python csrc/build.py [--force] [--only cpu|hip|tool]
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import shutil
+import subprocess
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+CSRC = ROOT / "csrc"
+PKG = ROOT / "gravity-simulator-using-mpi-spark-and-cuda_amd"
+OUT = PKG / "_native"
+ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
+ARCH = os.environ.get("GRAVSIM_ARCH", "gfx950")
+
+HEADERS = sorted((CSRC / "include").glob("*.h"))
+CPU_SRC = [CSRC / "common" / "layout.cpp", CSRC / "cpu" / "cpu_engine.cpp"]
+HIP_SRC = [CSRC / "common" / "layout.cpp", CSRC / "hip" / "nbody_kernels.hip",
+           CSRC / "hip" / "stepper.hip"]
+TOOL_SRC = [CSRC / "tools" / "gravsim_main.cpp"]
+
+CPU_LIB = OUT / "libgravsim_cpu.so"
+HIP_LIB = OUT / "libgravsim_hip.so"
+TOOL_BIN = OUT / "gravsim_bench"
+
+
+def _stale(target: Path, deps: list[Path]) -> bool:
+    if not target.exists():
+        return True
+    t = target.stat().st_mtime
+    return any(d.stat().st_mtime > t for d in deps if d.exists())
+
+
+def _run(cmd: list[str]) -> None:
+    print("+", " ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+
+
+def hipcc() -> str:
+    p = ROCM / "bin" / "hipcc"
+    return str(p) if p.exists() else (shutil.which("hipcc") or "hipcc")
+
+
+def build_cpu(force: bool = False) -> Path:
+    OUT.mkdir(parents=True, exist_ok=True)
+    if force or _stale(CPU_LIB, CPU_SRC + HEADERS):
+        cxx = os.environ.get("CXX", "g++")
+        tmp = CPU_LIB.with_suffix(".so.tmp")
+        _run([cxx, "-O3", "-std=c++17", "-fopenmp", "-march=x86-64-v3", "-ffp-contract=off",
+              "-fPIC", "-shared", f"-I{CSRC / 'include'}", *map(str, CPU_SRC), "-o", str(tmp)])
+        os.replace(tmp, CPU_LIB)
+    return CPU_LIB
+
+
+HIP_FLAGS = ["-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fno-slp-vectorize",
+             "-ffp-contract=off", "-fPIC"]
+
+
+def build_hip(force: bool = False) -> Path:
+    OUT.mkdir(parents=True, exist_ok=True)
+    if force or _stale(HIP_LIB, HIP_SRC + HEADERS):
+        tmp = HIP_LIB.with_suffix(".so.tmp")
+        _run([hipcc(), *HIP_FLAGS, "-shared", f"-I{CSRC / 'include'}", *map(str, HIP_SRC),
+              f"-L{ROCM / 'lib'}", "-lrccl", "-o", str(tmp)])
+        os.replace(tmp, HIP_LIB)
+    return HIP_LIB
+
+
+def build_tool(force: bool = False) -> Path:
+    OUT.mkdir(parents=True, exist_ok=True)
+    deps = TOOL_SRC + HIP_SRC + HEADERS
+    if all(p.exists() for p in TOOL_SRC) and (force or _stale(TOOL_BIN, deps)):
+        tmp = TOOL_BIN.with_suffix(".tmp")
+        _run([hipcc(), *HIP_FLAGS, f"-I{CSRC / 'include'}", *map(str, TOOL_SRC),
+              *map(str, HIP_SRC), f"-L{ROCM / 'lib'}", "-lrccl",
+              f"-Wl,-rpath,{ROCM / 'lib'}", "-o", str(tmp)])
+        os.replace(tmp, TOOL_BIN)
+    return TOOL_BIN
+
+
+def build_all(force: bool = False) -> None:
+    build_cpu(force)
+    build_hip(force)
+    build_tool(force)
+
+
+def main(argv: list[str] | None = None) -> int:
+    ap = argparse.ArgumentParser(description=__doc__)
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("--only", choices=["cpu", "hip", "tool"])
+    a = ap.parse_args(argv)
+    if a.only == "cpu":
+        build_cpu(a.force)
+    elif a.only == "hip":
+        build_hip(a.force)
+    elif a.only == "tool":
+        build_tool(a.force)
+    else:
+        build_all(a.force)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

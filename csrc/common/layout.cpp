@@ -1,0 +1,79 @@
+// Canonical decomposition shared by the CPU and GPU engines, plus host IC fill.
+//
+// Reference: mpi.c:184-187,218-225 spreads the N mod P remainder over the first ranks and
+// rebuilds Allgatherv counts every step. Here the body array is padded once with massless
+// ghost bodies (mu = 0, at the origin) to a multiple of P * chunk, so every rank owns an
+// equal contiguous slice (RCCL all-gather needs equal counts) and the j-chunk boundaries,
+// hence the floating-point summation order, do not depend on P.
+#include <stdio.h>
+#include <string.h>
+
+#include "gravsim.h"
+#include "gs_common.h"
+
+namespace {
+thread_local char g_err[512];
+}
+
+extern "C" const char* gs_last_error(void) { return g_err; }
+
+void gs_set_error(const char* msg) {
+  strncpy(g_err, msg, sizeof(g_err) - 1);
+  g_err[sizeof(g_err) - 1] = 0;
+}
+
+extern "C" int32_t gs_auto_chunk(int64_t n) { return gs::auto_chunk(n); }
+
+extern "C" int gs_layout_compute(const gs_config* cfg, gs_layout* out) {
+  if (!cfg || !out) { gs_set_error("layout: null argument"); return -1; }
+  if (cfg->n < 1) { gs_set_error("layout: n must be >= 1"); return -1; }
+  if (cfg->nranks < 1 || cfg->rank < 0 || cfg->rank >= cfg->nranks) {
+    gs_set_error("layout: bad rank/nranks");
+    return -1;
+  }
+  memset(out, 0, sizeof(*out));
+  const int32_t chunk = cfg->chunk > 0 ? cfg->chunk : gs::auto_chunk(cfg->n);
+  if (chunk % 1024 != 0) { gs_set_error("layout: chunk must be a multiple of 1024"); return -1; }
+  out->n = cfg->n;
+  out->chunk = chunk;
+  out->n_pad = gs::round_up(cfg->n, (int64_t)cfg->nranks * chunk);
+  out->n_local = out->n_pad / cfg->nranks;
+  out->local_begin = (int64_t)cfg->rank * out->n_local;
+  out->n_chunks = (int32_t)((cfg->n + chunk - 1) / chunk);
+  int32_t ipl = cfg->ipl;
+  if (ipl <= 0) ipl = (cfg->dtype == GS_FP64) ? 1 : 2;
+  if (ipl != 1 && ipl != 2 && ipl != 4) { gs_set_error("layout: ipl must be 1, 2 or 4"); return -1; }
+  out->ipl = ipl;
+  out->kernel = cfg->kernel == GS_KERNEL_AUTO ? GS_KERNEL_LDS : cfg->kernel;
+  const int64_t i_blocks = out->n_local / (256 * ipl);
+  int32_t mode = cfg->mode;
+  if (mode == GS_MODE_AUTO) {
+    // Fused needs enough i-blocks to fill 256 CUs at >= 8 workgroups of 4 waves each;
+    // otherwise split j over workgroups (deterministic per-chunk partials).
+    mode = (i_blocks >= 2048) ? GS_MODE_FUSED : GS_MODE_SPLIT;
+  }
+  out->mode = mode;
+  int32_t groups = cfg->split_groups;
+  if (groups <= 0) {
+    const int64_t target = 4096;  // workgroups per split launch (16 per CU)
+    int64_t g = (target + i_blocks - 1) / i_blocks;
+    if (g < 1) g = 1;
+    if (g > out->n_chunks) g = out->n_chunks;
+    groups = (int32_t)g;
+  }
+  out->split_groups = groups;
+  return 0;
+}
+
+extern "C" void gs_ic_fill_host(int32_t ic, uint64_t seed, int64_t n, int64_t begin, int64_t end,
+                                double* pos, double* vel, double* mass) {
+  if (end > n) end = n;
+  for (int64_t i = begin; i < end; ++i) {
+    double p[3], v[3], m;
+    gs::ic_body(ic, seed, i, p, v, &m);
+    const int64_t k = i - begin;
+    if (pos) { pos[3 * k] = p[0]; pos[3 * k + 1] = p[1]; pos[3 * k + 2] = p[2]; }
+    if (vel) { vel[3 * k] = v[0]; vel[3 * k + 1] = v[1]; vel[3 * k + 2] = v[2]; }
+    if (mass) mass[k] = m;
+  }
+}

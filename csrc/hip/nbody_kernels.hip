@@ -1,0 +1,460 @@
+// gfx950 (MI355X / CDNA4) direct-sum N-body kernels.
+//
+// Replaces the reference's single CUDA kernel (cuda.cu:32-60, launched at :156) and its host
+// integrator (cuda.cu:63-78). Design:
+//   * SoA state: X = (x, y, z, mu = G*m) as one 16-B (fp32) / 32-B (fp64) vector per body, so
+//     a j-body is one dwordx4 (fp32) load and no G*m_i*m_j product exists to overflow (D1).
+//   * i-owned accumulation in registers: each lane owns IPL i-bodies and sums the full j row.
+//     No Newton-3 scatter, no atomics, no race (D4), no triangular imbalance (D5).
+//   * j-bodies arrive either as LDS tiles filled by LDS-DMA (global_load_lds_dwordx4, one
+//     1-KiB wave-instruction per 64 fp32 bodies) and read as broadcast ds_read_b128, or as
+//     wave-uniform SGPR operands through the scalar cache (s_load_dwordx16). Both variants
+//     stream the same j range in the same order and give bitwise-identical results.
+//   * Canonical chunked summation: the j range is cut into fixed chunks (length chosen from N
+//     only); each chunk is summed from zero in j order and the chunk sums are added in chunk
+//     order. The fused kernel (one workgroup sweeps every chunk, KD integrate in the
+//     epilogue) and the split kernel (per-chunk partials + reduce/integrate kernel) therefore
+//     produce the same bits, for any rank count.
+//   * Kick-drift (symplectic Euler, "KD") integrate fused into the force epilogue:
+//     v += a dt; x += v dt (cuda.cu:73-76, mpi.c:207-215, pyspark.py:97-99).
+//   * Exact reference cutoff: zero force when r^2 < cutoff^2 (cuda.cu:39, mpi.c:64),
+//     implemented as a select, which also removes the self term.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "gs_common.h"
+#include "gravsim.h"
+#include "gs_kernels.h"
+
+namespace gs {
+
+template <typename T> struct VecT;
+template <> struct VecT<float> { using type = float __attribute__((ext_vector_type(4))); };
+template <> struct VecT<double> { using type = double __attribute__((ext_vector_type(4))); };
+template <typename T> using V4 = typename VecT<T>::type;
+
+constexpr int kBlock = 256;  // 4 waves of 64
+
+__device__ __forceinline__ float rsqrt_dev(float x) { return __builtin_amdgcn_rsqf(x); }
+
+// fp64: v_rsq_f64 seed + two Newton-Raphson steps, y <- y + y * (0.5 - 0.5 x y^2).
+__device__ __forceinline__ double rsqrt_dev(double x) {
+  double y = __builtin_amdgcn_rsq(x);
+  const double hx = 0.5 * x;
+  double e = __builtin_fma(-hx * y, y, 0.5);
+  y = __builtin_fma(y, e, y);
+  e = __builtin_fma(-hx * y, y, 0.5);
+  y = __builtin_fma(y, e, y);
+  return y;
+}
+
+__device__ __forceinline__ float fma_(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
+__device__ __forceinline__ double fma_(double a, double b, double c) { return __builtin_fma(a, b, c); }
+
+// One i-j interaction. 3 sub + 3 fma (r^2) + cmp/select + rsq + 3 mul + 3 fma (+1 add for phi).
+template <typename T, bool PHI>
+__device__ __forceinline__ void interact(T xi, T yi, T zi, T xj, T yj, T zj, T muj, T cut2,
+                                         T eps2, T& ax, T& ay, T& az, T& ph) {
+  const T dx = xj - xi, dy = yj - yi, dz = zj - zi;
+  const T r2 = fma_(dz, dz, fma_(dy, dy, fma_(dx, dx, eps2)));
+  const bool ok = r2 >= cut2;
+  T inv;
+  if constexpr (sizeof(T) == 8) {
+    // Branch-free: the Newton sequence would otherwise be predicated behind exec-mask jumps.
+    inv = rsqrt_dev(ok ? r2 : T(1));
+    inv = ok ? inv : T(0);
+  } else {
+    inv = ok ? rsqrt_dev(r2) : T(0);
+  }
+  const T mi = muj * inv;
+  const T s = mi * (inv * inv);
+  ax = fma_(s, dx, ax);
+  ay = fma_(s, dy, ay);
+  az = fma_(s, dz, az);
+  if constexpr (PHI) ph += mi;
+}
+
+template <typename T, int IPL>
+struct IState {
+  T x[IPL], y[IPL], z[IPL], mu[IPL];
+  T ax[IPL], ay[IPL], az[IPL], ph[IPL];  // current chunk
+  T tx[IPL], ty[IPL], tz[IPL], tp[IPL];  // canonical running total over chunks
+};
+
+template <typename T, int IPL>
+__device__ __forceinline__ void zero_chunk(IState<T, IPL>& s) {
+#pragma unroll
+  for (int k = 0; k < IPL; ++k) s.ax[k] = s.ay[k] = s.az[k] = s.ph[k] = T(0);
+}
+
+template <typename T, int IPL, bool PHI>
+__device__ __forceinline__ void interact_all(IState<T, IPL>& s, const V4<T>& q, T cut2, T eps2) {
+#pragma unroll
+  for (int k = 0; k < IPL; ++k)
+    interact<T, PHI>(s.x[k], s.y[k], s.z[k], q.x, q.y, q.z, q.w, cut2, eps2, s.ax[k], s.ay[k],
+                     s.az[k], s.ph[k]);
+}
+
+// LDS tile geometry: 4 KiB per tile buffer (256 fp32 bodies / 128 fp64 bodies).
+template <typename T> struct Tile { static constexpr int kBodies = 4096 / sizeof(V4<T>); };
+
+// Issue the LDS-DMA fill of one 4-KiB tile: each of the 4 waves moves one 1-KiB piece
+// (64 lanes x 16 B); the LDS destination is the wave-uniform base + lane*16.
+template <typename T>
+__device__ __forceinline__ void tile_fill(const V4<T>* __restrict__ src, V4<T>* dst) {
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const char* g = reinterpret_cast<const char*>(src) + wave * 1024 + lane * 16;
+  char* l = reinterpret_cast<char*>(dst) + wave * 1024;
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                   (__attribute__((address_space(3))) void*)l, 16, 0, 0);
+}
+
+// Sweep chunks [c0, c1) through LDS tiles. For every finished chunk call on_chunk(c).
+template <typename T, int IPL, bool PHI, typename OnChunk>
+__device__ __forceinline__ void sweep_lds(const V4<T>* __restrict__ X, int64_t chunk, int c0,
+                                          int c1, T cut2, T eps2, IState<T, IPL>& st,
+                                          V4<T> (*tile)[Tile<T>::kBodies], OnChunk on_chunk) {
+  constexpr int TB = Tile<T>::kBodies;
+  const int tiles_per_chunk = (int)(chunk / TB);
+  const int ntiles = (c1 - c0) * tiles_per_chunk;
+  if (ntiles <= 0) return;
+  const V4<T>* base = X + (int64_t)c0 * chunk;
+  tile_fill<T>(base, tile[0]);
+  zero_chunk<T, IPL>(st);
+  for (int t = 0; t < ntiles; ++t) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // tile t is in LDS for every wave; buffer (t+1)&1 is free
+    if (t + 1 < ntiles) tile_fill<T>(base + (int64_t)(t + 1) * TB, tile[(t + 1) & 1]);
+    const V4<T>* cur = tile[t & 1];
+#pragma unroll 8
+    for (int j = 0; j < TB; ++j) {
+      const V4<T> q = cur[j];  // uniform address: one broadcast ds_read per wave
+      interact_all<T, IPL, PHI>(st, q, cut2, eps2);
+    }
+    if ((t + 1) % tiles_per_chunk == 0) {
+      on_chunk(c0 + t / tiles_per_chunk);
+      zero_chunk<T, IPL>(st);
+    }
+  }
+}
+
+// Sweep chunks [c0, c1) with wave-uniform j loaded into SGPRs via the scalar cache.
+template <typename T, int IPL, bool PHI, typename OnChunk>
+__device__ __forceinline__ void sweep_smem(const V4<T>* __restrict__ X, int64_t chunk, int c0,
+                                           int c1, T cut2, T eps2, IState<T, IPL>& st,
+                                           OnChunk on_chunk) {
+  for (int c = c0; c < c1; ++c) {
+    zero_chunk<T, IPL>(st);
+    const V4<T>* p = X + (int64_t)c * chunk;
+    for (int64_t j = 0; j < chunk; j += 4) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) interact_all<T, IPL, PHI>(st, p[j + u], cut2, eps2);
+    }
+    on_chunk(c);
+  }
+}
+
+template <typename T, int IPL>
+__device__ __forceinline__ void load_i(const KArgs<T>& a, IState<T, IPL>& st, int64_t ib) {
+#pragma unroll
+  for (int k = 0; k < IPL; ++k) {
+    const V4<T> p = reinterpret_cast<const V4<T>*>(a.X)[a.i_begin + ib + threadIdx.x + k * kBlock];
+    st.x[k] = p.x; st.y[k] = p.y; st.z[k] = p.z; st.mu[k] = p.w;
+    st.tx[k] = st.ty[k] = st.tz[k] = st.tp[k] = T(0);
+  }
+}
+
+// Kick-drift epilogue for one lane's IPL bodies; ghost rows are pinned at the origin, massless.
+template <typename T, int IPL>
+__device__ __forceinline__ void integrate_store(const KArgs<T>& a, const IState<T, IPL>& st,
+                                                int64_t ib) {
+  V4<T>* vel = reinterpret_cast<V4<T>*>(a.vel);
+  V4<T>* xn = reinterpret_cast<V4<T>*>(a.X_next);
+#pragma unroll
+  for (int k = 0; k < IPL; ++k) {
+    const int64_t li = ib + threadIdx.x + k * kBlock;
+    const int64_t gi = a.i_begin + li;
+    if (gi < a.n_real) {
+      V4<T> v = vel[li];
+      v.x = v.x + st.tx[k] * a.dt;
+      v.y = v.y + st.ty[k] * a.dt;
+      v.z = v.z + st.tz[k] * a.dt;
+      V4<T> x;
+      x.x = st.x[k] + v.x * a.dt;
+      x.y = st.y[k] + v.y * a.dt;
+      x.z = st.z[k] + v.z * a.dt;
+      x.w = st.mu[k];
+      vel[li] = v;
+      xn[gi] = x;
+    } else {
+      const V4<T> z = {T(0), T(0), T(0), T(0)};
+      vel[li] = z;
+      xn[gi] = z;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// SPLIT: grid (i_blocks, groups). Workgroup (b, g) sweeps chunks of group g and stores one
+// partial (ax, ay, az, sum mu/r) per chunk: partial[c * n_local + i].
+template <typename T, int IPL, int KV, bool PHI>
+__global__ __launch_bounds__(kBlock) void force_split_kernel(KArgs<T> a) {
+  __shared__ __attribute__((aligned(16))) V4<T> tile[2][Tile<T>::kBodies];
+  const int64_t ib = (int64_t)blockIdx.x * (kBlock * IPL);
+  const int span = a.c_end - a.c_begin;
+  const int per = (span + (int)gridDim.y - 1) / (int)gridDim.y;
+  const int c0 = a.c_begin + (int)blockIdx.y * per;
+  const int c1 = min(c0 + per, a.c_end);
+  IState<T, IPL> st;
+  load_i<T, IPL>(a, st, ib);
+  V4<T>* part = reinterpret_cast<V4<T>*>(a.partial);
+  auto store = [&](int c) {
+#pragma unroll
+    for (int k = 0; k < IPL; ++k) {
+      V4<T> o;
+      o.x = st.ax[k]; o.y = st.ay[k]; o.z = st.az[k]; o.w = st.ph[k];
+      part[(int64_t)c * a.n_local + ib + threadIdx.x + k * kBlock] = o;
+    }
+  };
+  const V4<T>* X = reinterpret_cast<const V4<T>*>(a.X);
+  if constexpr (KV == GS_KERNEL_LDS)
+    sweep_lds<T, IPL, PHI>(X, a.chunk, c0, c1, a.cut2, a.eps2, st, tile, store);
+  else
+    sweep_smem<T, IPL, PHI>(X, a.chunk, c0, c1, a.cut2, a.eps2, st, store);
+}
+
+// FUSED: grid (i_blocks). Sweep every chunk in canonical order; chunks in [pre_begin,
+// pre_end) are taken from partial (computed earlier, e.g. the rank-local tile that overlapped
+// the all-gather). Integrate in the epilogue.
+template <typename T, int IPL, int KV, bool PHI>
+__global__ __launch_bounds__(kBlock) void force_fused_kernel(KArgs<T> a) {
+  __shared__ __attribute__((aligned(16))) V4<T> tile[2][Tile<T>::kBodies];
+  const int64_t ib = (int64_t)blockIdx.x * (kBlock * IPL);
+  IState<T, IPL> st;
+  load_i<T, IPL>(a, st, ib);
+  const V4<T>* part = reinterpret_cast<const V4<T>*>(a.partial);
+  auto fold = [&](int) {
+#pragma unroll
+    for (int k = 0; k < IPL; ++k) {
+      st.tx[k] += st.ax[k]; st.ty[k] += st.ay[k]; st.tz[k] += st.az[k]; st.tp[k] += st.ph[k];
+    }
+  };
+  auto fold_pre = [&](int c) {
+#pragma unroll
+    for (int k = 0; k < IPL; ++k) {
+      const V4<T> p = part[(int64_t)c * a.n_local + ib + threadIdx.x + k * kBlock];
+      st.tx[k] += p.x; st.ty[k] += p.y; st.tz[k] += p.z; st.tp[k] += p.w;
+    }
+  };
+  const V4<T>* X = reinterpret_cast<const V4<T>*>(a.X);
+  // Three canonical-order segments: [0, pre_begin) computed, [pre_begin, pre_end) loaded,
+  // [pre_end, n_chunks) computed.
+  const int pb = min(max(a.pre_begin, 0), a.n_chunks);
+  const int pe = min(max(a.pre_end, pb), a.n_chunks);
+  if constexpr (KV == GS_KERNEL_LDS) {
+    sweep_lds<T, IPL, PHI>(X, a.chunk, 0, pb, a.cut2, a.eps2, st, tile, fold);
+    for (int c = pb; c < pe; ++c) fold_pre(c);
+    __syncthreads();  // both LDS buffers are refilled by the next sweep
+    sweep_lds<T, IPL, PHI>(X, a.chunk, pe, a.n_chunks, a.cut2, a.eps2, st, tile, fold);
+  } else {
+    sweep_smem<T, IPL, PHI>(X, a.chunk, 0, pb, a.cut2, a.eps2, st, fold);
+    for (int c = pb; c < pe; ++c) fold_pre(c);
+    sweep_smem<T, IPL, PHI>(X, a.chunk, pe, a.n_chunks, a.cut2, a.eps2, st, fold);
+  }
+  if (a.acc_out) {
+    V4<T>* out = reinterpret_cast<V4<T>*>(a.acc_out);
+#pragma unroll
+    for (int k = 0; k < IPL; ++k) {
+      V4<T> o;
+      o.x = st.tx[k]; o.y = st.ty[k]; o.z = st.tz[k]; o.w = -st.tp[k];
+      out[ib + threadIdx.x + k * kBlock] = o;
+    }
+  } else {
+    integrate_store<T, IPL>(a, st, ib);
+  }
+}
+
+// REDUCE: total = sum over chunks (canonical order) of partial[c][i]; integrate or emit acc.
+template <typename T>
+__global__ __launch_bounds__(kBlock) void reduce_integrate_kernel(KArgs<T> a) {
+  const V4<T>* part = reinterpret_cast<const V4<T>*>(a.partial);
+  const V4<T>* X = reinterpret_cast<const V4<T>*>(a.X);
+  for (int64_t li = (int64_t)blockIdx.x * kBlock + threadIdx.x; li < a.n_local;
+       li += (int64_t)gridDim.x * kBlock) {
+    T tx = 0, ty = 0, tz = 0, tp = 0;
+    for (int c = 0; c < a.n_chunks; ++c) {
+      const V4<T> p = part[(int64_t)c * a.n_local + li];
+      tx += p.x; ty += p.y; tz += p.z; tp += p.w;
+    }
+    if (a.acc_out) {
+      V4<T> o;
+      o.x = tx; o.y = ty; o.z = tz; o.w = -tp;
+      reinterpret_cast<V4<T>*>(a.acc_out)[li] = o;
+      continue;
+    }
+    const int64_t gi = a.i_begin + li;
+    V4<T>* vel = reinterpret_cast<V4<T>*>(a.vel);
+    V4<T>* xn = reinterpret_cast<V4<T>*>(a.X_next);
+    if (gi < a.n_real) {
+      const V4<T> xi = X[gi];
+      V4<T> v = vel[li];
+      v.x = v.x + tx * a.dt;
+      v.y = v.y + ty * a.dt;
+      v.z = v.z + tz * a.dt;
+      V4<T> x;
+      x.x = xi.x + v.x * a.dt;
+      x.y = xi.y + v.y * a.dt;
+      x.z = xi.z + v.z * a.dt;
+      x.w = xi.w;
+      vel[li] = v;
+      xn[gi] = x;
+    } else {
+      const V4<T> z = {T(0), T(0), T(0), T(0)};
+      vel[li] = z;
+      xn[gi] = z;
+    }
+  }
+}
+
+// ICs on device: full positions (every rank) + this rank's velocities; masses to fp64 array.
+template <typename T>
+__global__ __launch_bounds__(kBlock) void init_ics_kernel(int ic, uint64_t seed, int64_t n,
+                                                          int64_t n_pad, int64_t i_begin,
+                                                          int64_t n_local, double G, T* X4,
+                                                          T* vel4, double* mass) {
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n_pad;
+       i += (int64_t)gridDim.x * kBlock) {
+    double p[3] = {0, 0, 0}, v[3] = {0, 0, 0}, m = 0;
+    if (i < n) ic_body(ic, seed, i, p, v, &m);
+    X4[4 * i] = (T)p[0];
+    X4[4 * i + 1] = (T)p[1];
+    X4[4 * i + 2] = (T)p[2];
+    X4[4 * i + 3] = (T)(G * m);
+    if (mass) mass[i] = m;
+    const int64_t li = i - i_begin;
+    if (li >= 0 && li < n_local) {
+      vel4[4 * li] = (T)v[0];
+      vel4[4 * li + 1] = (T)v[1];
+      vel4[4 * li + 2] = (T)v[2];
+      vel4[4 * li + 3] = T(0);
+    }
+  }
+}
+
+// Count non-finite components in X4 rows [i0, i1) and vel4 rows [0, nl) (NaN/Inf guard).
+template <typename T>
+__global__ __launch_bounds__(kBlock) void count_nonfinite_kernel(const T* X4, int64_t i0,
+                                                                 int64_t nl, const T* vel4,
+                                                                 unsigned long long* out) {
+  unsigned long long cnt = 0;
+  for (int64_t li = (int64_t)blockIdx.x * kBlock + threadIdx.x; li < nl;
+       li += (int64_t)gridDim.x * kBlock) {
+    for (int d = 0; d < 3; ++d) {
+      cnt += !isfinite(X4[4 * (i0 + li) + d]);
+      cnt += !isfinite(vel4[4 * li + d]);
+    }
+  }
+  for (int off = 32; off > 0; off >>= 1) cnt += __shfl_down(cnt, off, 64);
+  if ((threadIdx.x & 63) == 0 && cnt) atomicAdd(out, cnt);
+}
+
+// ---------------------------------------------------------------------------------------
+// Host launchers.
+
+template <typename T, int IPL, int KV>
+static hipError_t launch_split_t(const KArgs<T>& a, int groups, hipStream_t s) {
+  const int64_t blocks = a.n_local / (kBlock * IPL);
+  dim3 grid((unsigned)blocks, (unsigned)groups);
+  if (a.phi)
+    hipLaunchKernelGGL((force_split_kernel<T, IPL, KV, true>), grid, dim3(kBlock), 0, s, a);
+  else
+    hipLaunchKernelGGL((force_split_kernel<T, IPL, KV, false>), grid, dim3(kBlock), 0, s, a);
+  return hipGetLastError();
+}
+
+template <typename T, int IPL, int KV>
+static hipError_t launch_fused_t(const KArgs<T>& a, hipStream_t s) {
+  const int64_t blocks = a.n_local / (kBlock * IPL);
+  if (a.phi)
+    hipLaunchKernelGGL((force_fused_kernel<T, IPL, KV, true>), dim3((unsigned)blocks),
+                       dim3(kBlock), 0, s, a);
+  else
+    hipLaunchKernelGGL((force_fused_kernel<T, IPL, KV, false>), dim3((unsigned)blocks),
+                       dim3(kBlock), 0, s, a);
+  return hipGetLastError();
+}
+
+template <typename T, int KV>
+static hipError_t dispatch_ipl(const KArgs<T>& a, int ipl, bool fused, int groups,
+                               hipStream_t s) {
+  switch (ipl) {
+    case 1: return fused ? launch_fused_t<T, 1, KV>(a, s) : launch_split_t<T, 1, KV>(a, groups, s);
+    case 2: return fused ? launch_fused_t<T, 2, KV>(a, s) : launch_split_t<T, 2, KV>(a, groups, s);
+    case 4: return fused ? launch_fused_t<T, 4, KV>(a, s) : launch_split_t<T, 4, KV>(a, groups, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+template <typename T>
+static hipError_t dispatch(const KArgs<T>& a, int kernel, int ipl, bool fused, int groups,
+                           hipStream_t s) {
+  if (kernel == GS_KERNEL_SMEM) return dispatch_ipl<T, GS_KERNEL_SMEM>(a, ipl, fused, groups, s);
+  return dispatch_ipl<T, GS_KERNEL_LDS>(a, ipl, fused, groups, s);
+}
+
+template <typename T>
+hipError_t launch_force_split(const KArgs<T>& a, int kernel, int ipl, int groups, hipStream_t s) {
+  if (a.c_end <= a.c_begin) return hipSuccess;
+  if (groups < 1) groups = 1;
+  if (groups > a.c_end - a.c_begin) groups = a.c_end - a.c_begin;
+  return dispatch<T>(a, kernel, ipl, false, groups, s);
+}
+
+template <typename T>
+hipError_t launch_force_fused(const KArgs<T>& a, int kernel, int ipl, hipStream_t s) {
+  return dispatch<T>(a, kernel, ipl, true, 1, s);
+}
+
+template <typename T>
+hipError_t launch_reduce_integrate(const KArgs<T>& a, hipStream_t s) {
+  int64_t blocks = (a.n_local + kBlock - 1) / kBlock;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL((reduce_integrate_kernel<T>), dim3((unsigned)blocks), dim3(kBlock), 0, s, a);
+  return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_init_ics(int ic, uint64_t seed, int64_t n, int64_t n_pad, int64_t i_begin,
+                           int64_t n_local, double G, T* X4, T* vel4, double* mass,
+                           hipStream_t s) {
+  int64_t blocks = (n_pad + kBlock - 1) / kBlock;
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL((init_ics_kernel<T>), dim3((unsigned)blocks), dim3(kBlock), 0, s, ic, seed,
+                     n, n_pad, i_begin, n_local, G, X4, vel4, mass);
+  return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_count_nonfinite(const T* X4, int64_t i0, int64_t nl, const T* vel4,
+                                  unsigned long long* out, hipStream_t s) {
+  int64_t blocks = (nl + kBlock - 1) / kBlock;
+  if (blocks > 2048) blocks = 2048;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL((count_nonfinite_kernel<T>), dim3((unsigned)blocks), dim3(kBlock), 0, s, X4,
+                     i0, nl, vel4, out);
+  return hipGetLastError();
+}
+
+#define GS_INSTANTIATE(T)                                                                      \
+  template hipError_t launch_force_split<T>(const KArgs<T>&, int, int, int, hipStream_t);      \
+  template hipError_t launch_force_fused<T>(const KArgs<T>&, int, int, hipStream_t);           \
+  template hipError_t launch_reduce_integrate<T>(const KArgs<T>&, hipStream_t);                \
+  template hipError_t launch_init_ics<T>(int, uint64_t, int64_t, int64_t, int64_t, int64_t,    \
+                                         double, T*, T*, double*, hipStream_t);                \
+  template hipError_t launch_count_nonfinite<T>(const T*, int64_t, int64_t, const T*,          \
+                                                unsigned long long*, hipStream_t);
+GS_INSTANTIATE(float)
+GS_INSTANTIATE(double)
+
+}  // namespace gs

@@ -1,0 +1,560 @@
+// GPU Stepper: device-resident N-body state and the per-step schedule.
+//
+// Reference parity:
+//   cuda.cu:145-160  cudaMalloc / H2D once / per-step kernel + cudaDeviceSynchronize + D2H
+//                    of forces + host update   -> everything stays on device; host transfers
+//                    only at init, dump and checkpoint; no sync inside the step loop.
+//   mpi.c:142-182    MPI_Init/Bcast/Type_create_struct -> RCCL communicator bootstrapped from a
+//                    128-byte unique id; ICs are generated per rank (no broadcast needed).
+//   mpi.c:227-236    MPI_Allgatherv (aliased buffers) + MPI_Barrier every step
+//                    -> in-place ncclAllGather of (x, y, z, mu) rows on a high-priority comm
+//                    stream, overlapped with the rank-local j-chunks on the compute stream;
+//                    ordering by events, no barrier.
+// Step k (P ranks, ping-pong buffers X[0], X[1]):
+//   comm:    wait(own slice of X[k&1] written) -> ncclAllGather in place -> record gathered
+//   compute: split kernel over own chunks (reads only the own slice) -> partial
+//            wait(gathered) -> fused kernel over all chunks (own chunks read from partial)
+//            with the KD integrate in its epilogue -> own slice of X[(k+1)&1]
+// With one rank the step is a single fused launch (or split + reduce at small N); the loop
+// can be captured once into a hipGraph (two steps = one ping-pong period) and replayed.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "gravsim.h"
+#include "gs_common.h"
+#include "gs_kernels.h"
+
+void gs_set_error(const char* msg);
+
+#define GS_HIP(call)                                                                \
+  do {                                                                              \
+    hipError_t e_ = (call);                                                         \
+    if (e_ != hipSuccess) {                                                         \
+      char b_[384];                                                                 \
+      snprintf(b_, sizeof(b_), "%s:%d %s: %s", __FILE__, __LINE__, #call,           \
+               hipGetErrorString(e_));                                              \
+      gs_set_error(b_);                                                             \
+      return -1;                                                                    \
+    }                                                                               \
+  } while (0)
+
+#define GS_NCCL(call)                                                               \
+  do {                                                                              \
+    ncclResult_t r_ = (call);                                                       \
+    if (r_ != ncclSuccess) {                                                        \
+      char b_[384];                                                                 \
+      snprintf(b_, sizeof(b_), "%s:%d %s: %s", __FILE__, __LINE__, #call,           \
+               ncclGetErrorString(r_));                                             \
+      gs_set_error(b_);                                                             \
+      return -1;                                                                    \
+    }                                                                               \
+  } while (0)
+
+struct gs_stepper {
+  gs_config cfg;
+  gs_layout L;
+  size_t esz = 4;  // element size
+  hipStream_t s_comp = nullptr, s_comm = nullptr;
+  hipEvent_t ev_ready = nullptr, ev_gathered = nullptr;
+  hipEvent_t ev_t0 = nullptr, ev_local = nullptr, ev_end = nullptr;
+  void* X[2] = {nullptr, nullptr};
+  void* vel = nullptr;
+  void* partial = nullptr;
+  void* acc = nullptr;
+  double* mass_dev = nullptr;
+  unsigned long long* nonfinite = nullptr;
+  std::vector<double> mass_host;
+  int64_t k = 0;  // steps done; current positions live in X[k & 1]
+  bool full[2] = {true, false};
+  ncclComm_t comm = nullptr;
+  bool have_comm = false;
+  bool virt = false;  // member of a virtual-rank group (gather = device copies, gs_group_step)
+  hipGraphExec_t graph = nullptr;
+  bool timed = false;  // eager steps record phase events
+  int own_c0 = 0, own_c1 = 0;  // this rank's chunks clipped to [0, n_chunks)
+};
+
+namespace {
+
+size_t row_bytes(const gs_stepper* s) { return 4 * s->esz; }
+
+template <typename T>
+gs::KArgs<T> base_args(gs_stepper* s, int cur) {
+  gs::KArgs<T> a;
+  memset(&a, 0, sizeof(a));
+  a.X = static_cast<const T*>(s->X[cur]);
+  a.X_next = static_cast<T*>(s->X[cur ^ 1]);
+  a.vel = static_cast<T*>(s->vel);
+  a.partial = static_cast<T*>(s->partial);
+  a.acc_out = nullptr;
+  a.i_begin = s->L.local_begin;
+  a.n_local = s->L.n_local;
+  a.n_real = s->L.n;
+  a.chunk = s->L.chunk;
+  a.n_chunks = s->L.n_chunks;
+  a.c_begin = 0;
+  a.c_end = s->L.n_chunks;
+  a.pre_begin = a.pre_end = 0;
+  a.phi = 0;
+  a.dt = (T)s->cfg.dt;
+  a.cut2 = (T)(s->cfg.cutoff * s->cfg.cutoff);
+  a.eps2 = (T)(s->cfg.softening * s->cfg.softening);
+  return a;
+}
+
+int gather(gs_stepper* s, int cur) {
+  if (!s->have_comm || s->full[cur]) return 0;
+  char* buf = static_cast<char*>(s->X[cur]);
+  const size_t count = (size_t)s->L.n_local * 4;
+  GS_HIP(hipEventRecord(s->ev_ready, s->s_comp));
+  GS_HIP(hipStreamWaitEvent(s->s_comm, s->ev_ready, 0));
+  GS_NCCL(ncclAllGather(buf + (size_t)s->cfg.rank * s->L.n_local * row_bytes(s), buf, count,
+                        s->esz == 4 ? ncclFloat32 : ncclFloat64, s->comm, s->s_comm));
+  GS_HIP(hipEventRecord(s->ev_gathered, s->s_comm));
+  s->full[cur] = true;
+  return 0;
+}
+
+// Enqueue one step. `capturing` disables timing events.
+template <typename T>
+int enqueue_step(gs_stepper* s, bool capturing, bool gathered_externally) {
+  const int cur = (int)(s->k & 1);
+  gs::KArgs<T> a = base_args<T>(s, cur);
+  const int kernel = s->L.kernel, ipl = s->L.ipl;
+  const bool fused = s->L.mode == GS_MODE_FUSED;
+  const bool timed = s->timed && !capturing;
+  if (timed) GS_HIP(hipEventRecord(s->ev_t0, s->s_comp));
+  const bool need_gather = (s->have_comm || s->virt) && !s->full[cur];
+  if (need_gather) {
+    if (gathered_externally) s->full[cur] = true;
+    else if (gather(s, cur)) return -1;
+    // Rank-local chunks overlap the all-gather: they read only the own slice of X[cur].
+    gs::KArgs<T> loc = a;
+    loc.c_begin = s->own_c0;
+    loc.c_end = s->own_c1;
+    GS_HIP(gs::launch_force_split<T>(loc, kernel, ipl, s->L.split_groups, s->s_comp));
+    if (timed) GS_HIP(hipEventRecord(s->ev_local, s->s_comp));
+    GS_HIP(hipStreamWaitEvent(s->s_comp, s->ev_gathered, 0));
+    if (fused) {
+      a.pre_begin = s->own_c0;
+      a.pre_end = s->own_c1;
+      GS_HIP(gs::launch_force_fused<T>(a, kernel, ipl, s->s_comp));
+    } else {
+      gs::KArgs<T> r = a;
+      r.c_begin = 0;
+      r.c_end = s->own_c0;
+      GS_HIP(gs::launch_force_split<T>(r, kernel, ipl, s->L.split_groups, s->s_comp));
+      r.c_begin = s->own_c1;
+      r.c_end = s->L.n_chunks;
+      GS_HIP(gs::launch_force_split<T>(r, kernel, ipl, s->L.split_groups, s->s_comp));
+      GS_HIP(gs::launch_reduce_integrate<T>(a, s->s_comp));
+    }
+  } else {
+    if (timed) GS_HIP(hipEventRecord(s->ev_local, s->s_comp));
+    if (fused) {
+      GS_HIP(gs::launch_force_fused<T>(a, kernel, ipl, s->s_comp));
+    } else {
+      GS_HIP(gs::launch_force_split<T>(a, kernel, ipl, s->L.split_groups, s->s_comp));
+      GS_HIP(gs::launch_reduce_integrate<T>(a, s->s_comp));
+    }
+  }
+  if (timed) GS_HIP(hipEventRecord(s->ev_end, s->s_comp));
+  s->full[cur ^ 1] = !(s->have_comm || s->virt);  // only the own slice of X[next] is fresh
+  s->k += 1;
+  return 0;
+}
+
+int enqueue_step_any(gs_stepper* s, bool capturing, bool gathered_externally = false) {
+  return s->esz == 4 ? enqueue_step<float>(s, capturing, gathered_externally)
+                     : enqueue_step<double>(s, capturing, gathered_externally);
+}
+
+int build_graph(gs_stepper* s) {
+  // One ping-pong period (two steps) starting from an even step with a gathered buffer.
+  const int64_t k0 = s->k;
+  const bool f0 = s->full[0], f1 = s->full[1];
+  hipGraph_t g = nullptr;
+  GS_HIP(hipStreamBeginCapture(s->s_comp, hipStreamCaptureModeThreadLocal));
+  int rc = enqueue_step_any(s, true);
+  if (rc == 0) rc = enqueue_step_any(s, true);
+  hipError_t e = hipStreamEndCapture(s->s_comp, &g);
+  s->k = k0;
+  s->full[0] = f0;
+  s->full[1] = f1;
+  if (rc) return rc;
+  GS_HIP(e);
+  GS_HIP(hipGraphInstantiate(&s->graph, g, nullptr, nullptr, 0));
+  GS_HIP(hipGraphDestroy(g));
+  return 0;
+}
+
+template <typename T>
+int upload_state(gs_stepper* s, const double* pos, const double* vel, const double* mass) {
+  const int64_t n = s->L.n, np = s->L.n_pad, nl = s->L.n_local, b = s->L.local_begin;
+  std::vector<T> X((size_t)np * 4, T(0));
+  std::vector<T> V((size_t)nl * 4, T(0));
+  for (int64_t i = 0; i < n; ++i) {
+    X[4 * i] = (T)pos[3 * i];
+    X[4 * i + 1] = (T)pos[3 * i + 1];
+    X[4 * i + 2] = (T)pos[3 * i + 2];
+    X[4 * i + 3] = (T)(s->cfg.G * mass[i]);
+  }
+  for (int64_t li = 0; li < nl; ++li) {
+    const int64_t gi = b + li;
+    if (gi >= n) break;
+    V[4 * li] = (T)vel[3 * gi];
+    V[4 * li + 1] = (T)vel[3 * gi + 1];
+    V[4 * li + 2] = (T)vel[3 * gi + 2];
+  }
+  s->mass_host.assign(mass, mass + n);
+  GS_HIP(hipMemcpyAsync(s->X[0], X.data(), X.size() * sizeof(T), hipMemcpyHostToDevice,
+                        s->s_comp));
+  GS_HIP(hipMemcpyAsync(s->vel, V.data(), V.size() * sizeof(T), hipMemcpyHostToDevice,
+                        s->s_comp));
+  GS_HIP(hipStreamSynchronize(s->s_comp));
+  s->k = 0;
+  s->full[0] = true;
+  s->full[1] = false;
+  return 0;
+}
+
+template <typename T>
+int download_state(gs_stepper* s, double* pos, double* vel, double* mass) {
+  const int cur = (int)(s->k & 1);
+  if (pos && gather(s, cur)) return -1;
+  if (pos && s->have_comm) GS_HIP(hipStreamWaitEvent(s->s_comp, s->ev_gathered, 0));
+  // A virtual-rank shard between steps holds only its own slice: return just those rows.
+  const bool own_only = s->virt && !s->full[cur];
+  GS_HIP(hipStreamSynchronize(s->s_comp));
+  GS_HIP(hipStreamSynchronize(s->s_comm));
+  const int64_t n = s->L.n, nl = s->L.n_local, b = s->L.local_begin;
+  if (pos) {
+    std::vector<T> X((size_t)s->L.n_pad * 4);
+    GS_HIP(hipMemcpy(X.data(), s->X[cur], X.size() * sizeof(T), hipMemcpyDeviceToHost));
+    const int64_t i0 = own_only ? b : 0;
+    const int64_t i1 = own_only ? (b + nl < n ? b + nl : n) : n;
+    for (int64_t i = i0; i < i1; ++i)
+      for (int d = 0; d < 3; ++d) pos[3 * i + d] = (double)X[4 * i + d];
+  }
+  if (vel) {
+    std::vector<T> V((size_t)nl * 4);
+    GS_HIP(hipMemcpy(V.data(), s->vel, V.size() * sizeof(T), hipMemcpyDeviceToHost));
+    for (int64_t li = 0; li < nl && b + li < n; ++li)
+      for (int d = 0; d < 3; ++d) vel[3 * (b + li) + d] = (double)V[4 * li + d];
+  }
+  if (mass)
+    for (int64_t i = 0; i < n; ++i) mass[i] = s->mass_host[i];
+  return 0;
+}
+
+template <typename T>
+int accel_impl(gs_stepper* s, double* acc4) {
+  const int cur = (int)(s->k & 1);
+  if (s->virt && !s->full[cur]) {
+    gs_set_error("accel: virtual-rank shard is not gathered (use the group API)");
+    return -1;
+  }
+  if (gather(s, cur)) return -1;
+  if (s->have_comm) GS_HIP(hipStreamWaitEvent(s->s_comp, s->ev_gathered, 0));
+  gs::KArgs<T> a = base_args<T>(s, cur);
+  a.phi = 1;
+  a.acc_out = static_cast<T*>(s->acc);
+  GS_HIP(gs::launch_force_split<T>(a, s->L.kernel, s->L.ipl, s->L.split_groups, s->s_comp));
+  GS_HIP(gs::launch_reduce_integrate<T>(a, s->s_comp));
+  GS_HIP(hipStreamSynchronize(s->s_comp));
+  std::vector<T> A((size_t)s->L.n_local * 4);
+  GS_HIP(hipMemcpy(A.data(), s->acc, A.size() * sizeof(T), hipMemcpyDeviceToHost));
+  for (size_t i = 0; i < A.size(); ++i) acc4[i] = (double)A[i];
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int gs_hip_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+const char* gs_hip_kernel_info(void) {
+  return "gfx950 direct-sum: LDS-DMA tiles (global_load_lds_dwordx4) | SGPR scalar-cache j; "
+         "fused KD epilogue; canonical chunk order; RCCL in-place all-gather";
+}
+
+int gs_stepper_create(const gs_config* cfg, gs_stepper** out) {
+  if (!cfg || !out) { gs_set_error("stepper_create: null argument"); return -1; }
+  *out = nullptr;
+  gs_stepper* s = new gs_stepper();
+  s->cfg = *cfg;
+  if (gs_layout_compute(cfg, &s->L)) { delete s; return -1; }
+  s->esz = cfg->dtype == GS_FP64 ? 8 : 4;
+  s->timed = getenv("GRAVSIM_PHASE_TIMING") != nullptr;
+  const int64_t own_first = s->L.local_begin / s->L.chunk;
+  const int64_t own_last = (s->L.local_begin + s->L.n_local) / s->L.chunk;
+  s->own_c0 = (int)(own_first < s->L.n_chunks ? own_first : s->L.n_chunks);
+  s->own_c1 = (int)(own_last < s->L.n_chunks ? own_last : s->L.n_chunks);
+#define FAIL_CLEAN(call)          \
+  do {                            \
+    if ((call) != hipSuccess) {   \
+      char b_[256];               \
+      snprintf(b_, sizeof(b_), "stepper_create: %s failed: %s", #call, hipGetErrorString(hipGetLastError())); \
+      gs_set_error(b_);           \
+      gs_stepper_destroy(s);      \
+      return -1;                  \
+    }                             \
+  } while (0)
+  FAIL_CLEAN(hipSetDevice(cfg->device));
+  int lo = 0, hi = 0;
+  FAIL_CLEAN(hipDeviceGetStreamPriorityRange(&lo, &hi));
+  FAIL_CLEAN(hipStreamCreateWithFlags(&s->s_comp, hipStreamNonBlocking));
+  FAIL_CLEAN(hipStreamCreateWithPriority(&s->s_comm, hipStreamNonBlocking, hi));
+  FAIL_CLEAN(hipEventCreateWithFlags(&s->ev_ready, hipEventDisableTiming));
+  FAIL_CLEAN(hipEventCreateWithFlags(&s->ev_gathered, hipEventDisableTiming));
+  FAIL_CLEAN(hipEventCreate(&s->ev_t0));
+  FAIL_CLEAN(hipEventCreate(&s->ev_local));
+  FAIL_CLEAN(hipEventCreate(&s->ev_end));
+  const size_t rb = row_bytes(s);
+  FAIL_CLEAN(hipMalloc(&s->X[0], (size_t)s->L.n_pad * rb));
+  FAIL_CLEAN(hipMalloc(&s->X[1], (size_t)s->L.n_pad * rb));
+  FAIL_CLEAN(hipMalloc(&s->vel, (size_t)s->L.n_local * rb));
+  FAIL_CLEAN(hipMalloc(&s->acc, (size_t)s->L.n_local * rb));
+  FAIL_CLEAN(hipMalloc(&s->partial, (size_t)s->L.n_chunks * s->L.n_local * rb));
+  FAIL_CLEAN(hipMalloc(&s->mass_dev, (size_t)s->L.n_pad * sizeof(double)));
+  FAIL_CLEAN(hipMalloc(&s->nonfinite, sizeof(unsigned long long)));
+  FAIL_CLEAN(hipMemset(s->X[0], 0, (size_t)s->L.n_pad * rb));
+  FAIL_CLEAN(hipMemset(s->X[1], 0, (size_t)s->L.n_pad * rb));
+  FAIL_CLEAN(hipMemset(s->vel, 0, (size_t)s->L.n_local * rb));
+#undef FAIL_CLEAN
+  *out = s;
+  return 0;
+}
+
+int gs_stepper_destroy(gs_stepper* s) {
+  if (!s) return 0;
+  if (s->s_comp) (void)hipStreamSynchronize(s->s_comp);
+  if (s->s_comm) (void)hipStreamSynchronize(s->s_comm);
+  if (s->graph) (void)hipGraphExecDestroy(s->graph);
+  if (s->have_comm) (void)ncclCommDestroy(s->comm);
+  for (void* p : {s->X[0], s->X[1], s->vel, s->partial, s->acc, (void*)s->mass_dev,
+                  (void*)s->nonfinite})
+    if (p) (void)hipFree(p);
+  for (hipEvent_t e : {s->ev_ready, s->ev_gathered, s->ev_t0, s->ev_local, s->ev_end})
+    if (e) (void)hipEventDestroy(e);
+  if (s->s_comp) (void)hipStreamDestroy(s->s_comp);
+  if (s->s_comm) (void)hipStreamDestroy(s->s_comm);
+  delete s;
+  return 0;
+}
+
+int gs_stepper_layout(gs_stepper* s, gs_layout* out) {
+  if (!s || !out) return -1;
+  *out = s->L;
+  return 0;
+}
+
+int gs_stepper_init_ics(gs_stepper* s, int32_t ic, uint64_t seed) {
+  GS_HIP(hipSetDevice(s->cfg.device));
+  hipError_t e;
+  if (s->esz == 4)
+    e = gs::launch_init_ics<float>(ic, seed, s->L.n, s->L.n_pad, s->L.local_begin, s->L.n_local,
+                                   s->cfg.G, static_cast<float*>(s->X[0]),
+                                   static_cast<float*>(s->vel), s->mass_dev, s->s_comp);
+  else
+    e = gs::launch_init_ics<double>(ic, seed, s->L.n, s->L.n_pad, s->L.local_begin,
+                                    s->L.n_local, s->cfg.G, static_cast<double*>(s->X[0]),
+                                    static_cast<double*>(s->vel), s->mass_dev, s->s_comp);
+  GS_HIP(e);
+  s->mass_host.resize((size_t)s->L.n);
+  GS_HIP(hipMemcpyAsync(s->mass_host.data(), s->mass_dev, (size_t)s->L.n * sizeof(double),
+                        hipMemcpyDeviceToHost, s->s_comp));
+  GS_HIP(hipStreamSynchronize(s->s_comp));
+  s->k = 0;
+  s->full[0] = true;
+  s->full[1] = false;
+  if (s->graph) { (void)hipGraphExecDestroy(s->graph); s->graph = nullptr; }
+  return 0;
+}
+
+int gs_stepper_set_state(gs_stepper* s, const double* pos, const double* vel, const double* mass) {
+  GS_HIP(hipSetDevice(s->cfg.device));
+  if (s->graph) { (void)hipGraphExecDestroy(s->graph); s->graph = nullptr; }
+  return s->esz == 4 ? upload_state<float>(s, pos, vel, mass)
+                     : upload_state<double>(s, pos, vel, mass);
+}
+
+int gs_stepper_get_state(gs_stepper* s, double* pos, double* vel, double* mass) {
+  GS_HIP(hipSetDevice(s->cfg.device));
+  return s->esz == 4 ? download_state<float>(s, pos, vel, mass)
+                     : download_state<double>(s, pos, vel, mass);
+}
+
+int gs_stepper_step(gs_stepper* s, int32_t nsteps) {
+  GS_HIP(hipSetDevice(s->cfg.device));
+  if (s->cfg.nranks > 1 && !s->have_comm) {
+    gs_set_error("step: nranks > 1 but no RCCL communicator (call gs_stepper_comm_init)");
+    return -1;
+  }
+  // hipGraph replay only for the single-rank schedule (nothing to gather); RCCL capture is
+  // opt-in through use_graph >= 2.
+  const bool graph_ok = s->cfg.use_graph >= (s->have_comm ? 2 : 1) && !s->timed;
+  int32_t left = nsteps;
+  while (left > 0) {
+    const bool period_start = (s->k & 1) == 0 && (s->have_comm ? !s->full[0] : true);
+    if (graph_ok && left >= 2 && period_start) {
+      if (!s->graph && build_graph(s)) return -1;
+      GS_HIP(hipGraphLaunch(s->graph, s->s_comp));
+      s->k += 2;
+      // After one period: X[1] was gathered in the second step, X[0] holds only the own slice.
+      s->full[0] = !s->have_comm;
+      s->full[1] = true;
+      left -= 2;
+      continue;
+    }
+    if (enqueue_step_any(s, false)) return -1;
+    left -= 1;
+  }
+  return 0;
+}
+
+int gs_stepper_sync(gs_stepper* s) {
+  GS_HIP(hipStreamSynchronize(s->s_comm));
+  GS_HIP(hipStreamSynchronize(s->s_comp));
+  return 0;
+}
+
+int gs_stepper_accel(gs_stepper* s, double* acc4) {
+  GS_HIP(hipSetDevice(s->cfg.device));
+  return s->esz == 4 ? accel_impl<float>(s, acc4) : accel_impl<double>(s, acc4);
+}
+
+int64_t gs_stepper_count_nonfinite(gs_stepper* s) {
+  if (hipSetDevice(s->cfg.device) != hipSuccess) return -1;
+  const int cur = (int)(s->k & 1);
+  if (hipMemsetAsync(s->nonfinite, 0, sizeof(unsigned long long), s->s_comp) != hipSuccess)
+    return -1;
+  hipError_t e;
+  if (s->esz == 4)
+    e = gs::launch_count_nonfinite<float>(static_cast<const float*>(s->X[cur]),
+                                          s->L.local_begin, s->L.n_local,
+                                          static_cast<const float*>(s->vel), s->nonfinite,
+                                          s->s_comp);
+  else
+    e = gs::launch_count_nonfinite<double>(static_cast<const double*>(s->X[cur]),
+                                           s->L.local_begin, s->L.n_local,
+                                           static_cast<const double*>(s->vel), s->nonfinite,
+                                           s->s_comp);
+  if (e != hipSuccess) return -1;
+  unsigned long long h = 0;
+  if (hipMemcpyAsync(&h, s->nonfinite, sizeof(h), hipMemcpyDeviceToHost, s->s_comp) !=
+          hipSuccess ||
+      hipStreamSynchronize(s->s_comp) != hipSuccess)
+    return -1;
+  return (int64_t)h;
+}
+
+int64_t gs_stepper_steps_done(gs_stepper* s) { return s->k; }
+
+int gs_stepper_phase_ms(gs_stepper* s, float* local_ms, float* comm_ms, float* total_ms) {
+  if (!s->timed) { gs_set_error("phase timing disabled (set GRAVSIM_PHASE_TIMING=1)"); return -1; }
+  GS_HIP(hipEventSynchronize(s->ev_end));
+  float a = 0, b = 0;
+  GS_HIP(hipEventElapsedTime(&a, s->ev_t0, s->ev_local));
+  GS_HIP(hipEventElapsedTime(&b, s->ev_t0, s->ev_end));
+  if (local_ms) *local_ms = a;
+  if (comm_ms) *comm_ms = 0.f;
+  if (total_ms) *total_ms = b;
+  return 0;
+}
+
+void* gs_stepper_compute_stream(gs_stepper* s) { return (void*)s->s_comp; }
+
+// Virtual ranks: P shards (rank r of P) in one process on one device. The all-gather is
+// P*(P-1) device-to-device copies on shard 0's comm stream, fenced against every shard's
+// compute stream by events: the same kernels, arguments and chunk order as the RCCL path, so
+// a P-shard run must match the 1-rank run bit for bit (SURVEY.md §4.2 "virtual-rank mode").
+int gs_group_step(gs_stepper** sh, int32_t P, int32_t nsteps) {
+  if (!sh || P < 1) { gs_set_error("group_step: bad arguments"); return -1; }
+  for (int r = 0; r < P; ++r) {
+    if (sh[r]->cfg.nranks != P || sh[r]->cfg.rank != r || sh[r]->have_comm ||
+        sh[r]->cfg.device != sh[0]->cfg.device || sh[r]->esz != sh[0]->esz ||
+        sh[r]->L.n_pad != sh[0]->L.n_pad || sh[r]->k != sh[0]->k) {
+      gs_set_error("group_step: shards must be ranks 0..P-1 of one layout, in step");
+      return -1;
+    }
+  }
+  GS_HIP(hipSetDevice(sh[0]->cfg.device));
+  for (int r = 0; r < P; ++r) sh[r]->virt = P > 1;
+  hipStream_t gsm = sh[0]->s_comm;
+  const size_t slice = (size_t)sh[0]->L.n_local * row_bytes(sh[0]);
+  for (int32_t it = 0; it < nsteps; ++it) {
+    const int cur = (int)(sh[0]->k & 1);
+    const bool need = P > 1 && !sh[0]->full[cur];
+    if (need) {
+      for (int r = 0; r < P; ++r) GS_HIP(hipEventRecord(sh[r]->ev_ready, sh[r]->s_comp));
+      for (int r = 0; r < P; ++r) GS_HIP(hipStreamWaitEvent(gsm, sh[r]->ev_ready, 0));
+      for (int dst = 0; dst < P; ++dst)
+        for (int src = 0; src < P; ++src) {
+          if (src == dst) continue;
+          GS_HIP(hipMemcpyAsync(static_cast<char*>(sh[dst]->X[cur]) + src * slice,
+                                static_cast<char*>(sh[src]->X[cur]) + src * slice, slice,
+                                hipMemcpyDeviceToDevice, gsm));
+        }
+      for (int r = 0; r < P; ++r) GS_HIP(hipEventRecord(sh[r]->ev_gathered, gsm));
+    }
+    for (int r = 0; r < P; ++r)
+      if (enqueue_step_any(sh[r], false, need)) return -1;
+  }
+  return 0;
+}
+
+int gs_rccl_unique_id(void* out128) {
+  ncclUniqueId id;
+  GS_NCCL(ncclGetUniqueId(&id));
+  static_assert(sizeof(id) == 128, "unexpected ncclUniqueId size");
+  memcpy(out128, &id, sizeof(id));
+  return 0;
+}
+
+int gs_stepper_comm_init(gs_stepper* s, const void* id128, int32_t rank, int32_t nranks) {
+  if (rank != s->cfg.rank || nranks != s->cfg.nranks) {
+    gs_set_error("comm_init: rank/nranks differ from the stepper's layout");
+    return -1;
+  }
+  GS_HIP(hipSetDevice(s->cfg.device));
+  ncclUniqueId id;
+  memcpy(&id, id128, sizeof(id));
+  GS_NCCL(ncclCommInitRank(&s->comm, nranks, id, rank));
+  s->have_comm = nranks > 1;
+  if (!s->have_comm) {
+    (void)ncclCommDestroy(s->comm);
+    s->comm = nullptr;
+  }
+  if (s->graph) { (void)hipGraphExecDestroy(s->graph); s->graph = nullptr; }
+  // The current buffer is full only if every rank holds identical positions (fresh ICs).
+  return 0;
+}
+
+int gs_stepper_comm_check(gs_stepper* s) {
+  if (!s->have_comm) return 0;
+  ncclResult_t async = ncclSuccess;
+  GS_NCCL(ncclCommGetAsyncError(s->comm, &async));
+  if (async != ncclSuccess && async != ncclInProgress) {
+    char b[256];
+    snprintf(b, sizeof(b), "RCCL async error: %s; communicator aborted", ncclGetErrorString(async));
+    (void)ncclCommAbort(s->comm);
+    s->have_comm = false;
+    gs_set_error(b);
+    return -1;
+  }
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,145 @@
+// gravsim native C ABI — MI355X (gfx950) N-body runtime.
+//
+// One header for both native libraries:
+//   libgravsim_hip.so  (hipcc, gfx950): device kernels + the GPU Stepper (streams, events,
+//                      hipGraph replay, RCCL all-gather over xGMI).
+//   libgravsim_cpu.so  (g++ -fopenmp): fp64/fp32 direct-sum CPU engine (mpi.c world_size=1
+//                      analogue and fast native oracle).
+// Python binds these with ctypes (gravsim/ops/_native.py); there is no torch ABI coupling,
+// so the libraries also serve the standalone C++ driver in csrc/tools/.
+//
+// Reference parity (what these replace, /root/reference):
+//   cuda.cu:32-60   calculate_force_between + calculate_forces_kernel  -> gs force kernels
+//   cuda.cu:63-78   host update()                                      -> fused KD epilogue
+//   cuda.cu:145-160 cudaMalloc/Memcpy/DeviceSynchronize per step       -> device-resident Stepper
+//   mpi.c:160-236   MPI_Bcast / MPI_Allgatherv / MPI_Barrier           -> RCCL in-place all-gather
+//   mpi.c:196-216   per-rank O(N^2/P) loop + in-place integrate       -> gs_cpu_step (Jacobi)
+#pragma once
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum gs_dtype { GS_FP32 = 0, GS_FP64 = 1 };
+
+// Force kernel variants (the j-body source).
+enum gs_kernel {
+  GS_KERNEL_AUTO = 0,
+  GS_KERNEL_LDS = 1,   // j-tiles staged into LDS by global_load_lds (LDS-DMA), broadcast ds_read_b128
+  GS_KERNEL_SMEM = 2,  // wave-uniform j read through the scalar cache into SGPRs (s_load_dwordx16)
+};
+
+// Step schedule.
+enum gs_mode {
+  GS_MODE_AUTO = 0,
+  GS_MODE_FUSED = 1,   // one workgroup per i-block sweeps every j-chunk, KD integrate in the epilogue
+  GS_MODE_SPLIT = 2,   // i-block x chunk-group grid writes per-chunk partials; reduce+integrate kernel
+};
+
+// Initial-condition families (models). Same formulas in gravsim/models/initial_conditions.py.
+enum gs_ic {
+  GS_IC_SOLAR_RANDOM = 0,  // Sun/Earth/Mars + uniform cube bodies (cuda.cu:81-96,129-131)
+  GS_IC_RANDOM = 1,        // uniform cube bodies only
+};
+
+typedef struct gs_config {
+  int64_t n;          // real (global) body count
+  int32_t dtype;      // gs_dtype
+  int32_t kernel;     // gs_kernel
+  int32_t mode;       // gs_mode
+  int32_t ipl;        // i-bodies per lane (0 = auto)
+  int32_t chunk;      // canonical j-chunk length (0 = auto, from n only)
+  int32_t rank;       // this process' rank
+  int32_t nranks;     // world size (bodies are block-partitioned over ranks)
+  int32_t device;     // HIP device ordinal
+  int32_t use_graph;  // capture the step loop into a hipGraph and replay it
+  int32_t split_groups;  // SPLIT mode: chunk groups per i-block (0 = auto)
+  double dt;          // time step [s]
+  double G;           // gravitational constant
+  double cutoff;      // hard cutoff radius [m]: zero force below it (mpi.c:64)
+  double softening;   // Plummer softening length [m] (0 = reference semantics)
+} gs_config;
+
+typedef struct gs_layout {
+  int64_t n;            // real bodies
+  int64_t n_pad;        // padded global length (multiple of nranks*chunk)
+  int64_t n_local;      // bodies per rank (padded)
+  int64_t local_begin;  // global index of this rank's slice
+  int32_t chunk;        // canonical j-chunk length
+  int32_t n_chunks;     // chunks that contain at least one real body
+  int32_t ipl;          // resolved i-bodies per lane
+  int32_t kernel;       // resolved kernel variant
+  int32_t mode;         // resolved schedule
+  int32_t split_groups; // resolved chunk groups (SPLIT)
+} gs_layout;
+
+// ---------------------------------------------------------------- layout (host-only math)
+// Canonical, world-size-independent decomposition (shared by CPU and GPU engines).
+int gs_layout_compute(const gs_config* cfg, gs_layout* out);
+int32_t gs_auto_chunk(int64_t n);
+
+// ---------------------------------------------------------------- counter-based RNG / ICs (host)
+// Fill bodies [begin, end) of the IC family into fp64 arrays (pos/vel: 3 per body, mass: 1).
+void gs_ic_fill_host(int32_t ic, uint64_t seed, int64_t n, int64_t begin, int64_t end,
+                     double* pos, double* vel, double* mass);
+
+// ---------------------------------------------------------------- CPU engine (libgravsim_cpu)
+// Accelerations for global bodies [i0, i1) against all j (positions X4 = x,y,z,mu; n_pad rows),
+// summed in the canonical chunk order. acc4 gets (ax, ay, az, phi) per body. fp64 or fp32 (X4 type).
+int gs_cpu_accel_f64(const double* X4, int64_t n_real, int64_t i0, int64_t i1, int32_t chunk,
+                     double cut2, double eps2, double* acc4);
+int gs_cpu_accel_f32(const float* X4, int64_t n_real, int64_t i0, int64_t i1, int32_t chunk,
+                     float cut2, float eps2, float* acc4);
+// One KD step for global bodies [i0, i1): reads X4 (full), vel4 (local, i0-based), writes
+// Xnext4 rows [i0, i1) and vel4. Ghost rows (>= n_real) are zeroed.
+int gs_cpu_step_f64(const double* X4, double* Xnext4, double* vel4, int64_t n_real, int64_t i0,
+                    int64_t i1, int32_t chunk, double dt, double cut2, double eps2);
+int gs_cpu_step_f32(const float* X4, float* Xnext4, float* vel4, int64_t n_real, int64_t i0,
+                    int64_t i1, int32_t chunk, float dt, float cut2, float eps2);
+int gs_cpu_num_threads(void);
+
+// ---------------------------------------------------------------- GPU Stepper (libgravsim_hip)
+typedef struct gs_stepper gs_stepper;
+
+int gs_stepper_create(const gs_config* cfg, gs_stepper** out);
+int gs_stepper_destroy(gs_stepper* s);
+int gs_stepper_layout(gs_stepper* s, gs_layout* out);
+// Generate ICs on device (every rank generates the full position set and its own velocities).
+int gs_stepper_init_ics(gs_stepper* s, int32_t ic, uint64_t seed);
+// Upload a global fp64 state (pos n*3, vel n*3, mass n). Every rank passes the full arrays.
+int gs_stepper_set_state(gs_stepper* s, const double* pos, const double* vel, const double* mass);
+// Download: full gathered positions (n*3), this rank's velocities (global layout n*3: only the
+// rank's own rows are written), masses (n). Any pointer may be NULL.
+int gs_stepper_get_state(gs_stepper* s, double* pos, double* vel, double* mass);
+// Enqueue n steps (asynchronous w.r.t. the host).
+int gs_stepper_step(gs_stepper* s, int32_t nsteps);
+int gs_stepper_sync(gs_stepper* s);
+// Accelerations (+potential) of this rank's bodies for the current positions: acc4 = n_local*4.
+int gs_stepper_accel(gs_stepper* s, double* acc4);
+// Non-finite guard: returns number of non-finite position/velocity components on this rank.
+int64_t gs_stepper_count_nonfinite(gs_stepper* s);
+int64_t gs_stepper_steps_done(gs_stepper* s);
+// Per-step phase timing of the last step (ms): local tile, gather wait, remote+integrate.
+int gs_stepper_phase_ms(gs_stepper* s, float* local_ms, float* comm_ms, float* total_ms);
+void* gs_stepper_compute_stream(gs_stepper* s);
+
+// Virtual ranks on one device: shards[r] created with rank r of P; steps all of them in
+// lockstep with the all-gather done by device copies (the RCCL schedule without RCCL).
+int gs_group_step(gs_stepper** shards, int32_t P, int32_t nsteps);
+
+// RCCL: 128-byte unique id (rank 0 creates it; the launcher broadcasts it), then init.
+int gs_rccl_unique_id(void* out128);
+int gs_stepper_comm_init(gs_stepper* s, const void* id128, int32_t rank, int32_t nranks);
+// Poll RCCL async errors; aborts the communicator on error. Returns 0 if healthy.
+int gs_stepper_comm_check(gs_stepper* s);
+
+int gs_hip_device_count(void);
+const char* gs_hip_kernel_info(void);
+
+// ---------------------------------------------------------------- errors
+const char* gs_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif

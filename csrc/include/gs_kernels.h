@@ -1,0 +1,43 @@
+// Internal kernel-launch interface between nbody_kernels.hip and the Stepper runtime.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace gs {
+
+// Kernel arguments (passed by value). Arrays hold 4 components per body: X/X_next/partial
+// are (x, y, z, mu) / (ax, ay, az, sum mu/r); vel is (vx, vy, vz, 0); acc_out is
+// (ax, ay, az, phi). i-indexed arrays other than X/X_next are rank-local (li = gi - i_begin).
+template <typename T>
+struct KArgs {
+  const T* X;        // [n_pad * 4] gathered positions for this step
+  T* X_next;         // [n_pad * 4] next-step positions (own slice written)
+  T* vel;            // [n_local * 4]
+  T* partial;        // [n_chunks * n_local * 4] per-chunk partial sums
+  T* acc_out;        // optional [n_local * 4]: emit accelerations instead of integrating
+  int64_t i_begin;   // global index of this rank's first body
+  int64_t n_local;   // padded bodies per rank
+  int64_t n_real;    // real global body count
+  int64_t chunk;     // canonical j-chunk length
+  int32_t n_chunks;  // chunks holding real bodies
+  int32_t c_begin, c_end;      // split kernel: chunk range
+  int32_t pre_begin, pre_end;  // fused kernel: chunk range read from partial
+  int32_t phi;       // accumulate the potential sum too
+  T dt, cut2, eps2;
+};
+
+template <typename T>
+hipError_t launch_force_split(const KArgs<T>& a, int kernel, int ipl, int groups, hipStream_t s);
+template <typename T>
+hipError_t launch_force_fused(const KArgs<T>& a, int kernel, int ipl, hipStream_t s);
+template <typename T>
+hipError_t launch_reduce_integrate(const KArgs<T>& a, hipStream_t s);
+template <typename T>
+hipError_t launch_init_ics(int ic, uint64_t seed, int64_t n, int64_t n_pad, int64_t i_begin,
+                           int64_t n_local, double G, T* X4, T* vel4, double* mass,
+                           hipStream_t s);
+template <typename T>
+hipError_t launch_count_nonfinite(const T* X4, int64_t i0, int64_t nl, const T* vel4,
+                                  unsigned long long* out, hipStream_t s);
+
+}  // namespace gs

@@ -1,0 +1,140 @@
+"""Command-line entry: `python -m gravsim --n N --dt DT --steps STEPS [...]`.
+
+Replaces the three reference `main`s, none of which parses arguments (cuda.cu:120,
+mpi.c:140, pyspark.py:152), and the Spark configuration sweep (pyspark.py:166-200, `--sweep`).
+Multi-process runs: `python -m torch.distributed.run --nproc-per-node P --master-addr
+127.0.0.1 -m gravsim ...` (one rank per GPU; gloo control plane, RCCL data plane).
+"""
+from __future__ import annotations
+
+import argparse
+import sys
+from typing import Optional
+
+from .config import SimConfig
+
+
+def build_parser() -> argparse.ArgumentParser:
+    d = SimConfig()
+    p = argparse.ArgumentParser(prog="gravsim", description="MI355X-native direct-sum N-body "
+                                "gravity simulator (Sun/Earth/Mars + random bodies by default)")
+    p.add_argument("--n", type=int, default=d.n, help="number of bodies")
+    p.add_argument("--dt", type=float, default=d.dt, help="time step [s]")
+    p.add_argument("--steps", type=int, default=d.steps, help="number of steps")
+    p.add_argument("--dtype", choices=["fp32", "fp64"], default=d.dtype)
+    p.add_argument("--device", choices=["auto", "cpu", "gpu"], default=d.device)
+    p.add_argument("--init", default=d.init,
+                   help="IC family: solar+random | random | plummer | kepler | cold")
+    p.add_argument("--seed", type=int, default=d.seed)
+    p.add_argument("--G", type=float, default=d.G)
+    p.add_argument("--cutoff", type=float, default=d.cutoff)
+    p.add_argument("--softening", type=float, default=d.softening)
+    p.add_argument("--kernel", choices=["auto", "lds", "smem"], default=d.kernel)
+    p.add_argument("--mode", choices=["auto", "fused", "split"], default=d.mode)
+    p.add_argument("--ipl", type=int, default=d.ipl, choices=[0, 1, 2, 4])
+    p.add_argument("--chunk", type=int, default=d.chunk)
+    p.add_argument("--no-graph", dest="graph", action="store_false")
+    p.add_argument("--threads", type=int, default=0)
+    p.add_argument("--log-dir", default=None, help="write the text log under this directory")
+    p.add_argument("--log-format", choices=["mpi", "spark", "cuda", "none"], default=d.log_format)
+    p.add_argument("--progress-every", type=int, default=d.progress_every)
+    p.add_argument("--print-positions", type=int, default=d.print_positions)
+    p.add_argument("--dump", dest="dump_path", default=None,
+                   help="final state: .txt (mpi.c 'Particle i: (x, y, z)' lines) or .gsck")
+    p.add_argument("--checkpoint-dir", default=None)
+    p.add_argument("--checkpoint-every", type=int, default=0)
+    p.add_argument("--resume", default=None, help="checkpoint file (or directory: latest)")
+    p.add_argument("--record-every", type=int, default=0)
+    p.add_argument("--record-path", default=None, help="trajectory .npy (frames x n x 3)")
+    p.add_argument("--nan-check-every", type=int, default=0)
+    p.add_argument("--metrics-json", default=None, help="append the run's JSON metrics line here")
+    p.add_argument("--sweep", default=None,
+                   help="comma-separated N values: run each config in turn (pyspark.py sweep)")
+    p.add_argument("--quiet", action="store_true")
+    return p
+
+
+def config_from_args(a: argparse.Namespace) -> SimConfig:
+    from .utils import checkpoint as ckpt
+
+    resume = a.resume
+    if resume:
+        import os
+
+        if os.path.isdir(resume):
+            resume = ckpt.latest(resume)
+    return SimConfig(n=a.n, dt=a.dt, steps=a.steps, dtype=a.dtype, device=a.device, init=a.init,
+                     seed=a.seed, G=a.G, cutoff=a.cutoff, softening=a.softening, kernel=a.kernel,
+                     mode=a.mode, ipl=a.ipl, chunk=a.chunk, graph=a.graph, threads=a.threads,
+                     log_dir=a.log_dir, log_format=a.log_format, progress_every=a.progress_every,
+                     print_positions=a.print_positions, dump_path=a.dump_path,
+                     checkpoint_dir=a.checkpoint_dir, checkpoint_every=a.checkpoint_every,
+                     resume=resume, record_every=a.record_every, record_path=a.record_path,
+                     nan_check_every=a.nan_check_every, metrics_json=a.metrics_json).validate()
+
+
+def run_one(cfg: SimConfig, dist, log, quiet: bool = False, final: bool = True) -> dict:
+    from .runtime.simulation import Simulation
+    from .utils import checkpoint as ckpt
+    from .utils.logs import format_positions_mpi
+
+    sim = Simulation(cfg, dist)
+    try:
+        if log and dist.is_root:
+            log.header(dist.world, cfg.n, cfg.steps, cfg.dt)
+        m = sim.run(cfg.steps, log if dist.is_root else None)
+        state = sim.global_state()
+        if dist.is_root:
+            if log:
+                log.stats(m.wall_s, m.steps)
+                log.positions(state.pos, cfg.print_positions)
+                if final:
+                    log.completed()
+            if cfg.dump_path:
+                if cfg.dump_path.endswith(".gsck"):
+                    meta = dict(dt=cfg.dt, dtype=cfg.dtype, G=cfg.G, cutoff=cfg.cutoff,
+                                softening=cfg.softening, init=cfg.init, seed=cfg.seed)
+                    ckpt.save(cfg.dump_path, state, sim.step, meta)
+                else:
+                    with open(cfg.dump_path, "w") as f:
+                        f.write(format_positions_mpi(state.pos))
+            if cfg.record_path:
+                sim.save_trajectory(cfg.record_path)
+            line = m.to_json()
+            if not quiet:
+                print(line, flush=True)
+            if cfg.metrics_json:
+                with open(cfg.metrics_json, "a") as f:
+                    f.write(line + "\n")
+        return {"metrics": m, "state": state}
+    finally:
+        sim.close()
+
+
+def main(argv: Optional[list[str]] = None) -> int:
+    from .parallel import comm
+    from .utils.logs import RunLog
+
+    a = build_parser().parse_args(argv)
+    cfg = config_from_args(a)
+    dist = comm.init()
+    try:
+        if a.sweep:
+            sizes = [int(x) for x in a.sweep.split(",") if x]
+            fmt = cfg.log_format if a.log_format != "mpi" else "spark"
+            log = RunLog(fmt, cfg.log_dir if dist.is_root else None, echo=dist.is_root)
+            for n in sizes:
+                run_one(cfg.replace(n=n, log_format=fmt), dist, log, a.quiet, final=False)
+            if dist.is_root:
+                log.completed()
+        else:
+            log = RunLog(cfg.log_format, cfg.log_dir if dist.is_root else None,
+                         echo=dist.is_root and not a.quiet)
+            run_one(cfg, dist, log, a.quiet)
+    finally:
+        comm.shutdown(dist)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,87 @@
+"""Simulation configuration.
+
+The reference has no configuration system: N, dt, steps and cores are source literals
+(cuda.cu:121-123,155; mpi.c:107,146-148; pyspark.py:48,168-173,183-188). Here every knob is
+a field of SimConfig and a CLI flag (gravsim/cli.py). Defaults reproduce the reference run:
+dt = 3600 s, 500 steps, Sun/Earth/Mars + uniform random bodies, cutoff 1e-10 m, G = 6.67430e-11.
+"""
+from __future__ import annotations
+
+import dataclasses
+from dataclasses import dataclass, field
+from typing import Optional
+
+G_SI = 6.67430e-11  # cuda.cu:11, mpi.c:9, pyspark.py:46
+
+DTYPES = ("fp32", "fp64")
+DEVICES = ("auto", "cpu", "gpu")
+KERNELS = ("auto", "lds", "smem")
+MODES = ("auto", "fused", "split")
+COMMS = ("auto", "rccl", "gloo", "none")
+LOG_FORMATS = ("mpi", "spark", "cuda", "none")
+
+
+@dataclass
+class SimConfig:
+    n: int = 1024                 # bodies (cuda.cu:121 uses 50,000; mpi.c:107 uses 8)
+    dt: float = 3600.0            # seconds (cuda.cu:123, mpi.c:148, pyspark.py:186)
+    steps: int = 500              # (cuda.cu:155, mpi.c:147, pyspark.py:188)
+    dtype: str = "fp64"           # fp32 (cuda.cu) | fp64 (mpi.c, pyspark.py)
+    device: str = "auto"          # auto -> gpu when a HIP device is visible
+    init: str = "solar+random"    # IC family, see gravsim.models.initial_conditions
+    seed: int = 20250307
+    G: float = G_SI
+    cutoff: float = 1e-10         # hard cutoff radius (cuda.cu:39, mpi.c:64, pyspark.py:38)
+    softening: float = 0.0        # Plummer softening length (0 = reference semantics)
+    kernel: str = "auto"          # GPU j-source variant: lds | smem
+    mode: str = "auto"            # GPU schedule: fused | split
+    ipl: int = 0                  # i-bodies per lane (0 = auto)
+    chunk: int = 0                # canonical j-chunk (0 = auto from n)
+    split_groups: int = 0
+    graph: bool = True            # hipGraph replay of the step loop (single rank)
+    comm: str = "auto"            # rccl (GPU) | gloo (CPU) | none
+    threads: int = 0              # CPU engine OpenMP threads (0 = default)
+    # observability / IO
+    log_dir: Optional[str] = None     # directory for the text log (None = no file)
+    log_format: str = "mpi"           # mpi | spark | cuda | none
+    progress_every: int = 100         # "Step s/steps" progress lines (mpi.c:192, cuda.cu:164)
+    print_positions: int = 10         # final-position lines on stdout (cuda.cu:101)
+    dump_path: Optional[str] = None   # final state dump (text, mpi.c format) or .npz
+    checkpoint_dir: Optional[str] = None
+    checkpoint_every: int = 0
+    resume: Optional[str] = None
+    record_every: int = 0             # trajectory recorder (pyspark.py:105,114-115)
+    record_path: Optional[str] = None
+    nan_check_every: int = 0          # NaN/Inf guard period (0 = only at the end)
+    metrics_json: Optional[str] = None
+
+    def validate(self) -> "SimConfig":
+        if self.n < 1:
+            raise ValueError("n must be >= 1")
+        if self.steps < 0:
+            raise ValueError("steps must be >= 0")
+        if self.dtype not in DTYPES:
+            raise ValueError(f"dtype must be one of {DTYPES}")
+        if self.device not in DEVICES:
+            raise ValueError(f"device must be one of {DEVICES}")
+        if self.kernel not in KERNELS:
+            raise ValueError(f"kernel must be one of {KERNELS}")
+        if self.mode not in MODES:
+            raise ValueError(f"mode must be one of {MODES}")
+        if self.comm not in COMMS:
+            raise ValueError(f"comm must be one of {COMMS}")
+        if self.log_format not in LOG_FORMATS:
+            raise ValueError(f"log_format must be one of {LOG_FORMATS}")
+        if self.ipl not in (0, 1, 2, 4):
+            raise ValueError("ipl must be 0, 1, 2 or 4")
+        if self.chunk and self.chunk % 1024:
+            raise ValueError("chunk must be a multiple of 1024")
+        if self.cutoff < 0 or self.softening < 0:
+            raise ValueError("cutoff and softening must be >= 0")
+        return self
+
+    def replace(self, **kw) -> "SimConfig":
+        return dataclasses.replace(self, **kw)
+
+    def to_dict(self) -> dict:
+        return dataclasses.asdict(self)

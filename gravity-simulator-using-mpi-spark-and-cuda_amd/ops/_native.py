@@ -1,0 +1,170 @@
+"""ctypes bindings to the in-tree native libraries (built by csrc/build.py).
+
+libgravsim_cpu.so is host-only. libgravsim_hip.so holds the gfx950 kernels and the GPU
+Stepper; torch is imported before it is loaded so that both share one HIP runtime (the
+library's libamdhip64.so.7 / librccl.so.1 dependencies bind to the copies torch already
+loaded, by soname). Missing libraries are built on demand when a compiler is available, and
+otherwise raise NativeUnavailable — there is no silent Python fallback for the GPU path.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+from ctypes import POINTER, c_double, c_float, c_int32, c_int64, c_uint64, c_void_p
+from pathlib import Path
+
+_HERE = Path(__file__).resolve().parent.parent
+NATIVE_DIR = _HERE / "_native"
+_REPO = _HERE.parent
+_lock = threading.Lock()
+_cpu = None
+_hip = None
+
+
+class NativeUnavailable(RuntimeError):
+    pass
+
+
+class GsConfig(ctypes.Structure):
+    _fields_ = [
+        ("n", c_int64), ("dtype", c_int32), ("kernel", c_int32), ("mode", c_int32),
+        ("ipl", c_int32), ("chunk", c_int32), ("rank", c_int32), ("nranks", c_int32),
+        ("device", c_int32), ("use_graph", c_int32), ("split_groups", c_int32),
+        ("dt", c_double), ("G", c_double), ("cutoff", c_double), ("softening", c_double),
+    ]
+
+
+class GsLayout(ctypes.Structure):
+    _fields_ = [
+        ("n", c_int64), ("n_pad", c_int64), ("n_local", c_int64), ("local_begin", c_int64),
+        ("chunk", c_int32), ("n_chunks", c_int32), ("ipl", c_int32), ("kernel", c_int32),
+        ("mode", c_int32), ("split_groups", c_int32),
+    ]
+
+    def as_dict(self) -> dict:
+        return {f: getattr(self, f) for f, _ in self._fields_}
+
+
+GS_FP32, GS_FP64 = 0, 1
+KERNEL_IDS = {"auto": 0, "lds": 1, "smem": 2}
+MODE_IDS = {"auto": 0, "fused": 1, "split": 2}
+KERNEL_NAMES = {v: k for k, v in KERNEL_IDS.items()}
+MODE_NAMES = {v: k for k, v in MODE_IDS.items()}
+
+_P = c_void_p
+_PD = POINTER(c_double)
+_PF = POINTER(c_float)
+
+
+def _build(which: str) -> None:
+    import subprocess
+    import sys
+
+    script = _REPO / "csrc" / "build.py"
+    if not script.exists():
+        raise NativeUnavailable(f"{which} library missing and no build script at {script}")
+    r = subprocess.run([sys.executable, str(script), "--only", which], capture_output=True,
+                       text=True)
+    if r.returncode != 0:
+        raise NativeUnavailable(f"building libgravsim_{which}.so failed:\n{r.stdout}\n{r.stderr}")
+
+
+def _sig(lib, name, res, args):
+    f = getattr(lib, name)
+    f.restype = res
+    f.argtypes = args
+    return f
+
+
+def _declare_common(lib) -> None:
+    _sig(lib, "gs_last_error", ctypes.c_char_p, [])
+    _sig(lib, "gs_layout_compute", c_int32, [POINTER(GsConfig), POINTER(GsLayout)])
+    _sig(lib, "gs_auto_chunk", c_int32, [c_int64])
+    _sig(lib, "gs_ic_fill_host", None, [c_int32, c_uint64, c_int64, c_int64, c_int64, _PD, _PD,
+                                        _PD])
+
+
+def cpu_lib():
+    """Load (building if needed) libgravsim_cpu.so."""
+    global _cpu
+    with _lock:
+        if _cpu is not None:
+            return _cpu
+        path = NATIVE_DIR / "libgravsim_cpu.so"
+        if not path.exists() or os.environ.get("GRAVSIM_REBUILD"):
+            _build("cpu")
+        lib = ctypes.CDLL(str(path))
+        _declare_common(lib)
+        for t, P in (("f64", _PD), ("f32", _PF)):
+            T = c_double if t == "f64" else c_float
+            _sig(lib, f"gs_cpu_accel_{t}", c_int32, [P, c_int64, c_int64, c_int64, c_int32, T, T, P])
+            _sig(lib, f"gs_cpu_step_{t}", c_int32,
+                 [P, P, P, c_int64, c_int64, c_int64, c_int32, T, T, T])
+        _sig(lib, "gs_cpu_num_threads", c_int32, [])
+        _cpu = lib
+        return lib
+
+
+def hip_lib():
+    """Load libgravsim_hip.so (after torch, so the HIP runtime is shared)."""
+    global _hip
+    with _lock:
+        if _hip is not None:
+            return _hip
+        import torch  # noqa: F401  (binds libamdhip64 / librccl first)
+
+        path = NATIVE_DIR / "libgravsim_hip.so"
+        if not path.exists() or os.environ.get("GRAVSIM_REBUILD"):
+            _build("hip")
+        try:
+            lib = ctypes.CDLL(str(path))
+        except OSError as e:  # pragma: no cover - depends on the box
+            raise NativeUnavailable(f"cannot load {path}: {e}") from e
+        _declare_common(lib)
+        S = c_void_p
+        _sig(lib, "gs_stepper_create", c_int32, [POINTER(GsConfig), POINTER(S)])
+        _sig(lib, "gs_stepper_destroy", c_int32, [S])
+        _sig(lib, "gs_stepper_layout", c_int32, [S, POINTER(GsLayout)])
+        _sig(lib, "gs_stepper_init_ics", c_int32, [S, c_int32, c_uint64])
+        _sig(lib, "gs_stepper_set_state", c_int32, [S, _PD, _PD, _PD])
+        _sig(lib, "gs_stepper_get_state", c_int32, [S, _PD, _PD, _PD])
+        _sig(lib, "gs_stepper_step", c_int32, [S, c_int32])
+        _sig(lib, "gs_stepper_sync", c_int32, [S])
+        _sig(lib, "gs_stepper_accel", c_int32, [S, _PD])
+        _sig(lib, "gs_stepper_count_nonfinite", c_int64, [S])
+        _sig(lib, "gs_stepper_steps_done", c_int64, [S])
+        _sig(lib, "gs_stepper_phase_ms", c_int32, [S, _PF, _PF, _PF])
+        _sig(lib, "gs_stepper_compute_stream", c_void_p, [S])
+        _sig(lib, "gs_group_step", c_int32, [POINTER(S), c_int32, c_int32])
+        _sig(lib, "gs_rccl_unique_id", c_int32, [c_void_p])
+        _sig(lib, "gs_stepper_comm_init", c_int32, [S, c_void_p, c_int32, c_int32])
+        _sig(lib, "gs_stepper_comm_check", c_int32, [S])
+        _sig(lib, "gs_hip_device_count", c_int32, [])
+        _sig(lib, "gs_hip_kernel_info", ctypes.c_char_p, [])
+        _hip = lib
+        return lib
+
+
+def check(lib, rc: int, what: str) -> None:
+    if rc != 0:
+        msg = lib.gs_last_error().decode(errors="replace")
+        raise RuntimeError(f"{what} failed: {msg}")
+
+
+def loaded_libraries() -> list[str]:
+    out = []
+    if _cpu is not None:
+        out.append(str(NATIVE_DIR / "libgravsim_cpu.so"))
+    if _hip is not None:
+        out.append(str(NATIVE_DIR / "libgravsim_hip.so"))
+    return out
+
+
+def dptr(a):
+    """ctypes double* of a contiguous float64 NumPy array."""
+    return a.ctypes.data_as(_PD)
+
+
+def fptr(a):
+    return a.ctypes.data_as(_PF)

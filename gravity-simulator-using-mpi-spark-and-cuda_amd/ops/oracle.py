@@ -1,0 +1,90 @@
+"""NumPy fp64 oracle: the intended physics of the reference, as one vectorised function.
+
+    a_i = sum_{j : |x_j - x_i| >= r_cut} G m_j (x_j - x_i) / |x_j - x_i|^3      (mpi.c:59-73)
+    v <- v + a dt ;  x <- x + v dt                                             (mpi.c:206-215)
+
+with every acceleration of a step evaluated from the positions at the start of that step
+(synchronous / Jacobi). This is NOT the reference output — cuda.cu overflows in fp32 and
+never refreshes its device positions, and mpi.c updates in place — but the physics all three
+programs intend. Optional Plummer softening eps: r^2 -> r^2 + eps^2.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from ..config import G_SI
+
+
+def accelerations(pos: np.ndarray, mass: np.ndarray, G: float = G_SI, cutoff: float = 1e-10,
+                  softening: float = 0.0, block: int = 256, with_potential: bool = False):
+    """Direct-sum accelerations (n, 3) in fp64; optionally the potential phi (n,) too."""
+    pos = np.asarray(pos, dtype=np.float64)
+    mu = G * np.asarray(mass, dtype=np.float64)
+    n = pos.shape[0]
+    acc = np.zeros((n, 3))
+    phi = np.zeros(n)
+    cut2 = cutoff * cutoff
+    eps2 = softening * softening
+    for i0 in range(0, n, block):
+        i1 = min(n, i0 + block)
+        d = pos[None, :, :] - pos[i0:i1, None, :]            # (b, n, 3)  x_j - x_i
+        r2 = (d * d).sum(-1) + eps2
+        ok = r2 >= cut2
+        inv = np.zeros_like(r2)
+        inv[ok] = 1.0 / np.sqrt(r2[ok])
+        mi = mu[None, :] * inv
+        s = mi * inv * inv
+        acc[i0:i1] = (s[:, :, None] * d).sum(1)
+        phi[i0:i1] = -mi.sum(1)
+    if with_potential:
+        return acc, phi
+    return acc
+
+
+def step(pos, vel, mass, dt, G=G_SI, cutoff=1e-10, softening=0.0):
+    """One synchronous kick-drift step; returns new (pos, vel)."""
+    a = accelerations(pos, mass, G, cutoff, softening)
+    v = vel + a * dt
+    x = pos + v * dt
+    return x, v
+
+
+def simulate(pos, vel, mass, dt, steps, G=G_SI, cutoff=1e-10, softening=0.0, record_every=0):
+    """Run `steps` steps. Returns (pos, vel, trajectory list of positions if record_every)."""
+    x = np.array(pos, dtype=np.float64, copy=True)
+    v = np.array(vel, dtype=np.float64, copy=True)
+    traj = []
+    for s in range(steps):
+        x, v = step(x, v, mass, dt, G, cutoff, softening)
+        if record_every and (s + 1) % record_every == 0:
+            traj.append(x.copy())
+    return x, v, traj
+
+
+def gauss_seidel_step(pos, vel, mass, dt, nranks, G=G_SI, cutoff=1e-10):
+    """Emulation of mpi.c's in-place update inside each rank's block (mpi.c:196-216, D6).
+
+    Kept only to document the defect in tests: results depend on `nranks`.
+    """
+    x = np.array(pos, dtype=np.float64, copy=True)
+    v = np.array(vel, dtype=np.float64, copy=True)
+    n = x.shape[0]
+    base, rem = divmod(n, nranks)
+    snapshot = x.copy()  # what other ranks hold until the Allgatherv
+    new_x = x.copy()
+    for r in range(nranks):
+        start = r * base + min(r, rem)
+        cnt = base + (1 if r < rem else 0)
+        local = snapshot.copy()
+        for i in range(start, start + cnt):
+            d = local - local[i]
+            r2 = (d * d).sum(1)
+            ok = r2 >= cutoff * cutoff
+            ok[i] = False
+            inv = np.zeros(n)
+            inv[ok] = 1.0 / np.sqrt(r2[ok])
+            a = ((G * mass * inv ** 3)[:, None] * d).sum(0)
+            v[i] = v[i] + a * dt
+            local[i] = local[i] + v[i] * dt
+            new_x[i] = local[i]
+    return new_x, v

@@ -1,0 +1,74 @@
+"""Canonical body decomposition (pure-Python mirror of csrc/common/layout.cpp).
+
+Reference: mpi.c:184-187 gives rank r the block [r*floor(N/P) + min(r, N mod P), ...) and
+rebuilds Allgatherv counts/displacements every step (mpi.c:218-225). Equal-count collectives
+(RCCL all-gather) need equal slices, and bitwise world-size independence needs the j-sum
+order fixed, so instead:
+
+* chunk  = C(N): canonical j-chunk length, a function of N only;
+* n_pad  = N rounded up to a multiple of P*C; rows [N, n_pad) are massless ghosts at the origin;
+* rank r owns rows [r*n_pad/P, (r+1)*n_pad/P);
+* every body's acceleration is sum over chunks c (in order) of a chunk sum that starts at 0,
+  so partials computed on any rank, in any launch shape, add up to the same bits.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+
+def auto_chunk(n: int) -> int:
+    p = 1
+    while p < n:
+        p <<= 1
+    return int(min(65536, max(2048, p // 64)))
+
+
+def round_up(a: int, b: int) -> int:
+    return (a + b - 1) // b * b
+
+
+@dataclass(frozen=True)
+class Layout:
+    n: int
+    n_pad: int
+    n_local: int
+    local_begin: int
+    chunk: int
+    n_chunks: int
+    rank: int
+    nranks: int
+
+    @property
+    def local_end(self) -> int:
+        return self.local_begin + self.n_local
+
+    @property
+    def real_local(self) -> range:
+        """Global indices of the real (non-ghost) bodies this rank owns."""
+        return range(self.local_begin, min(self.local_end, self.n))
+
+    @property
+    def own_chunks(self) -> range:
+        c0 = min(self.local_begin // self.chunk, self.n_chunks)
+        c1 = min(self.local_end // self.chunk, self.n_chunks)
+        return range(c0, c1)
+
+
+def layout(n: int, rank: int = 0, nranks: int = 1, chunk: int = 0) -> Layout:
+    if n < 1:
+        raise ValueError("n must be >= 1")
+    if not (0 <= rank < nranks):
+        raise ValueError("bad rank/nranks")
+    c = chunk or auto_chunk(n)
+    if c % 1024:
+        raise ValueError("chunk must be a multiple of 1024")
+    n_pad = round_up(n, nranks * c)
+    n_local = n_pad // nranks
+    return Layout(n=n, n_pad=n_pad, n_local=n_local, local_begin=rank * n_local, chunk=c,
+                  n_chunks=(n + c - 1) // c, rank=rank, nranks=nranks)
+
+
+def mpi_block(n: int, rank: int, nranks: int) -> tuple[int, int]:
+    """The reference's remainder-spread block (start, count) of mpi.c:184-187 (for parity docs)."""
+    base, rem = divmod(n, nranks)
+    return rank * base + min(rank, rem), base + (1 if rank < rem else 0)

@@ -1,0 +1,288 @@
+"""Execution engines behind the Simulation driver.
+
+Both engines expose the same small interface (load / init_ics / step / sync / state / accel /
+nonfinite / close) and the same canonical layout, so the driver, the tests and the CLI do not
+care where the bodies live.
+
+* HipEngine — the native GPU Stepper (csrc/hip/stepper.hip): device-resident state, gfx950
+  force kernels with the KD integrate fused in, hipGraph replay, RCCL all-gather for P > 1.
+  Replaces cuda.cu:145-167 (per-step kernel + sync + D2H + host update).
+* CpuEngine — the native C++/OpenMP engine (csrc/cpu/cpu_engine.cpp) with a gloo all-gather
+  for P > 1. Replaces mpi.c:189-237's step loop (with Jacobi semantics) and pyspark.py's
+  driver-side reduce/update (pyspark.py:59-102).
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional
+
+import numpy as np
+
+from ..config import SimConfig
+from ..models.initial_conditions import DEVICE_IC_IDS, BodySet, make, solar_random, random_cube
+from ..ops import _native
+from ..parallel import comm
+from ..parallel.partition import Layout, layout as make_layout
+
+
+def _gs_config(cfg: SimConfig, rank: int, nranks: int, device: int) -> _native.GsConfig:
+    return _native.GsConfig(
+        n=cfg.n, dtype=_native.GS_FP64 if cfg.dtype == "fp64" else _native.GS_FP32,
+        kernel=_native.KERNEL_IDS[cfg.kernel], mode=_native.MODE_IDS[cfg.mode], ipl=cfg.ipl,
+        chunk=cfg.chunk, rank=rank, nranks=nranks, device=device, use_graph=int(cfg.graph),
+        split_groups=cfg.split_groups, dt=cfg.dt, G=cfg.G, cutoff=cfg.cutoff,
+        softening=cfg.softening)
+
+
+def gpu_available() -> bool:
+    try:
+        import torch
+
+        if not torch.cuda.is_available():
+            return False
+        return _native.hip_lib().gs_hip_device_count() > 0
+    except Exception:
+        return False
+
+
+class HipEngine:
+    """GPU engine: one native gs_stepper per process (or per virtual rank)."""
+
+    kind = "gpu"
+
+    def __init__(self, cfg: SimConfig, rank: int = 0, nranks: int = 1, device: int = 0,
+                 dist: Optional[comm.DistInfo] = None):
+        self.cfg = cfg
+        self.rank, self.nranks, self.device = rank, nranks, device
+        self.dist = dist
+        self.lib = _native.hip_lib()
+        c = _gs_config(cfg, rank, nranks, device)
+        self._s = ctypes.c_void_p()
+        _native.check(self.lib, self.lib.gs_stepper_create(ctypes.byref(c), ctypes.byref(self._s)),
+                      "gs_stepper_create")
+        L = _native.GsLayout()
+        _native.check(self.lib, self.lib.gs_stepper_layout(self._s, ctypes.byref(L)), "layout")
+        self.native_layout = L.as_dict()
+        self.layout: Layout = make_layout(cfg.n, rank, nranks, L.chunk)
+        self.mass: Optional[np.ndarray] = None
+
+    # -- communicator ---------------------------------------------------------------------
+    def comm_init(self, uid: bytes) -> None:
+        buf = ctypes.create_string_buffer(uid, 128)
+        _native.check(self.lib, self.lib.gs_stepper_comm_init(self._s, buf, self.rank,
+                                                              self.nranks), "comm_init")
+
+    @staticmethod
+    def unique_id() -> bytes:
+        lib = _native.hip_lib()
+        buf = ctypes.create_string_buffer(128)
+        _native.check(lib, lib.gs_rccl_unique_id(buf), "rccl unique id")
+        return buf.raw
+
+    def comm_check(self) -> None:
+        _native.check(self.lib, self.lib.gs_stepper_comm_check(self._s), "rccl health")
+
+    # -- state ----------------------------------------------------------------------------
+    def init_ics(self, family: str, seed: int) -> None:
+        if family in DEVICE_IC_IDS:
+            _native.check(self.lib, self.lib.gs_stepper_init_ics(self._s, DEVICE_IC_IDS[family],
+                                                                 seed), "init_ics")
+            self.mass = None
+        else:
+            self.load(make(family, self.cfg.n, seed, self.cfg.G))
+
+    def load(self, b: BodySet) -> None:
+        pos = np.ascontiguousarray(b.pos, dtype=np.float64)
+        vel = np.ascontiguousarray(b.vel, dtype=np.float64)
+        mass = np.ascontiguousarray(b.mass, dtype=np.float64)
+        _native.check(self.lib, self.lib.gs_stepper_set_state(
+            self._s, _native.dptr(pos), _native.dptr(vel), _native.dptr(mass)), "set_state")
+        self.mass = mass
+
+    def step(self, n: int) -> None:
+        if n > 0:
+            _native.check(self.lib, self.lib.gs_stepper_step(self._s, int(n)), "step")
+
+    def sync(self) -> None:
+        _native.check(self.lib, self.lib.gs_stepper_sync(self._s), "sync")
+
+    def state(self) -> BodySet:
+        """Full positions (collective for P > 1), own velocity rows, masses."""
+        n = self.cfg.n
+        pos = np.zeros((n, 3))
+        vel = np.zeros((n, 3))
+        mass = np.zeros(n)
+        _native.check(self.lib, self.lib.gs_stepper_get_state(
+            self._s, _native.dptr(pos), _native.dptr(vel), _native.dptr(mass)), "get_state")
+        return BodySet(pos, vel, mass)
+
+    def accel(self) -> np.ndarray:
+        """(n_local, 4) = (ax, ay, az, phi) of this rank's rows (ghost rows included)."""
+        out = np.zeros((self.layout.n_local, 4))
+        _native.check(self.lib, self.lib.gs_stepper_accel(self._s, _native.dptr(out)), "accel")
+        return out
+
+    def nonfinite(self) -> int:
+        r = int(self.lib.gs_stepper_count_nonfinite(self._s))
+        if r < 0:
+            raise RuntimeError("nonfinite check failed: " + self.lib.gs_last_error().decode())
+        return r
+
+    @property
+    def steps_done(self) -> int:
+        return int(self.lib.gs_stepper_steps_done(self._s))
+
+    def close(self) -> None:
+        if self._s:
+            self.lib.gs_stepper_destroy(self._s)
+            self._s = ctypes.c_void_p()
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class CpuEngine:
+    """Native CPU engine; P > 1 exchanges position slices with a gloo all-gather."""
+
+    kind = "cpu"
+
+    def __init__(self, cfg: SimConfig, rank: int = 0, nranks: int = 1,
+                 dist: Optional[comm.DistInfo] = None):
+        self.cfg = cfg
+        self.rank, self.nranks = rank, nranks
+        self.dist = dist or comm.DistInfo(rank=rank, world=nranks)
+        self.lib = _native.cpu_lib()
+        self.layout: Layout = make_layout(cfg.n, rank, nranks, cfg.chunk)
+        self.np_dtype = np.float64 if cfg.dtype == "fp64" else np.float32
+        L = self.layout
+        self.X = [np.zeros((L.n_pad, 4), self.np_dtype), np.zeros((L.n_pad, 4), self.np_dtype)]
+        self.V = np.zeros((L.n_local, 4), self.np_dtype)
+        self.k = 0
+        self.mass = np.zeros(cfg.n)
+        suf = "f64" if cfg.dtype == "fp64" else "f32"
+        self._step = getattr(self.lib, f"gs_cpu_step_{suf}")
+        self._accel = getattr(self.lib, f"gs_cpu_accel_{suf}")
+        self._ptr = _native.dptr if cfg.dtype == "fp64" else _native.fptr
+        if cfg.threads:
+            import os
+
+            os.environ["OMP_NUM_THREADS"] = str(cfg.threads)
+
+    def init_ics(self, family: str, seed: int) -> None:
+        n, L = self.cfg.n, self.layout
+        if family == "solar+random":
+            b = solar_random(n, seed)
+        elif family == "random":
+            b = random_cube(n, seed)
+        else:
+            b = make(family, n, seed, self.cfg.G)
+        self.load(b)
+
+    def load(self, b: BodySet) -> None:
+        L, n = self.layout, self.cfg.n
+        X = self.X[0]
+        X[:] = 0
+        X[:n, :3] = b.pos
+        X[:n, 3] = self.cfg.G * b.mass
+        self.V[:] = 0
+        rows = L.real_local
+        if len(rows):
+            self.V[: len(rows), :3] = b.vel[rows.start:rows.stop]
+        self.mass = np.array(b.mass, dtype=np.float64)
+        self.k = 0
+
+    def step(self, n: int) -> None:
+        L = self.layout
+        T = self.np_dtype
+        cut2 = T(self.cfg.cutoff ** 2)
+        eps2 = T(self.cfg.softening ** 2)
+        for _ in range(int(n)):
+            cur, nxt = self.X[self.k & 1], self.X[(self.k + 1) & 1]
+            rc = self._step(self._ptr(cur), self._ptr(nxt), self._ptr(self.V), L.n,
+                            L.local_begin, L.local_end, L.chunk, T(self.cfg.dt), cut2, eps2)
+            _native.check(self.lib, rc, "cpu step")
+            comm.allgather_rows(self.dist, nxt, L.local_begin, L.n_local)
+            self.k += 1
+
+    def sync(self) -> None:
+        pass
+
+    def state(self) -> BodySet:
+        n, L = self.cfg.n, self.layout
+        X = self.X[self.k & 1]
+        pos = X[:n, :3].astype(np.float64)
+        vel = np.zeros((n, 3))
+        rows = L.real_local
+        if len(rows):
+            vel[rows.start:rows.stop] = self.V[: len(rows), :3]
+        return BodySet(pos, vel, self.mass.copy())
+
+    def accel(self) -> np.ndarray:
+        L = self.layout
+        T = self.np_dtype
+        out = np.zeros((L.n_local, 4), T)
+        rc = self._accel(self._ptr(self.X[self.k & 1]), L.n, L.local_begin, L.local_end, L.chunk,
+                         T(self.cfg.cutoff ** 2), T(self.cfg.softening ** 2), self._ptr(out))
+        _native.check(self.lib, rc, "cpu accel")
+        return out.astype(np.float64)
+
+    def nonfinite(self) -> int:
+        L = self.layout
+        X = self.X[self.k & 1][L.local_begin:L.local_end, :3]
+        return int((~np.isfinite(X)).sum() + (~np.isfinite(self.V[:, :3])).sum())
+
+    @property
+    def steps_done(self) -> int:
+        return self.k
+
+    def close(self) -> None:
+        pass
+
+
+class VirtualGroup:
+    """P virtual ranks (one HipEngine each, rank r of P) on one device, stepped in lockstep by
+    the native gs_group_step: the RCCL schedule with the all-gather done by device copies."""
+
+    def __init__(self, cfg: SimConfig, nranks: int, device: int = 0):
+        self.cfg = cfg
+        self.shards = [HipEngine(cfg, r, nranks, device) for r in range(nranks)]
+        self.lib = self.shards[0].lib
+
+    def init_ics(self, family: str, seed: int) -> None:
+        for s in self.shards:
+            s.init_ics(family, seed)
+
+    def load(self, b: BodySet) -> None:
+        for s in self.shards:
+            s.load(b)
+
+    def step(self, n: int) -> None:
+        arr = (ctypes.c_void_p * len(self.shards))(*[s._s.value for s in self.shards])
+        _native.check(self.lib, self.lib.gs_group_step(arr, len(self.shards), int(n)),
+                      "group_step")
+
+    def sync(self) -> None:
+        for s in self.shards:
+            s.sync()
+
+    def state(self) -> BodySet:
+        """Assemble the global state from each shard's own rows."""
+        n = self.cfg.n
+        pos = np.zeros((n, 3))
+        vel = np.zeros((n, 3))
+        mass = None
+        for s in self.shards:
+            b = s.state()
+            rows = s.layout.real_local
+            if len(rows):
+                pos[rows.start:rows.stop] = b.pos[rows.start:rows.stop]
+                vel[rows.start:rows.stop] = b.vel[rows.start:rows.stop]
+            mass = b.mass
+        return BodySet(pos, vel, mass)
+
+    def close(self) -> None:
+        for s in self.shards:
+            s.close()

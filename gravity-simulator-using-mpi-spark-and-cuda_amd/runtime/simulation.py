@@ -1,0 +1,136 @@
+"""Simulation driver: ICs or resume -> step loop -> stats, dumps, checkpoints.
+
+Reference step loops: cuda.cu:154-167, mpi.c:189-237, pyspark.py:104-121. Differences by
+design:
+* the whole loop is enqueued on the device; the host only wakes up at "events" (progress
+  lines, checkpoints, trajectory frames, NaN guard) instead of crossing the host/device
+  boundary twice per step (cuda.cu:157,160);
+* timing brackets the step loop like the reference ("Total execution time", mpi.c:239-247)
+  but ends with a device sync so the number is real;
+* NaN/Inf guard (the reference silently produced non-finite output, D1-D3) and RCCL health
+  checks run at a configurable period;
+* checkpoints are rank-agnostic and a resumed run continues bit-exactly.
+"""
+from __future__ import annotations
+
+import time
+from typing import Optional
+
+import numpy as np
+
+from ..config import SimConfig
+from ..models.initial_conditions import BodySet
+from ..parallel import comm
+from ..utils import checkpoint as ckpt
+from ..utils.logs import RunLog
+from ..utils.metrics import RunMetrics
+from .engines import CpuEngine, HipEngine, gpu_available
+
+
+class NonFiniteError(RuntimeError):
+    pass
+
+
+class Simulation:
+    def __init__(self, cfg: SimConfig, dist: Optional[comm.DistInfo] = None):
+        self.cfg = cfg.validate()
+        self.dist = dist or comm.env_info()
+        use_gpu = cfg.device == "gpu" or (cfg.device == "auto" and gpu_available())
+        if cfg.device == "gpu" and not gpu_available():
+            raise RuntimeError("device=gpu requested but no HIP device / native library")
+        d = self.dist
+        if use_gpu:
+            import torch
+
+            dev = d.local_rank % max(1, torch.cuda.device_count())
+            self.engine = HipEngine(cfg, d.rank, d.world, device=dev, dist=d)
+            if d.world > 1:
+                uid = HipEngine.unique_id() if d.is_root else None
+                uid = comm.broadcast_bytes(d, uid)
+                self.engine.comm_init(uid)
+        else:
+            self.engine = CpuEngine(cfg, d.rank, d.world, dist=d)
+        self.step0 = 0
+        self.trajectory: list[np.ndarray] = []
+        if cfg.resume:
+            c = ckpt.load(cfg.resume)
+            if c.bodies.n != cfg.n:
+                raise ValueError(f"checkpoint has n={c.bodies.n}, config n={cfg.n}")
+            self.engine.load(c.bodies)
+            self.step0 = c.step
+        else:
+            self.engine.init_ics(cfg.init, cfg.seed)
+
+    @property
+    def device(self) -> str:
+        return self.engine.kind
+
+    @property
+    def step(self) -> int:
+        return self.step0 + self.engine.steps_done
+
+    def global_state(self) -> BodySet:
+        """Full (pos, vel, mass) on every rank (collective when P > 1)."""
+        b = self.engine.state()
+        if self.dist.world > 1:
+            rows = self.engine.layout.real_local
+            comm.gather_rows_to_root(self.dist, b.vel, slice(rows.start, rows.stop))
+        return b
+
+    def check_finite(self) -> None:
+        bad = comm.allreduce_sum(self.dist, self.engine.nonfinite())
+        if bad:
+            raise NonFiniteError(f"{int(bad)} non-finite position/velocity components at step "
+                                 f"{self.step}")
+        if isinstance(self.engine, HipEngine) and self.dist.world > 1:
+            self.engine.comm_check()
+
+    def save_checkpoint(self, path: Optional[str] = None) -> Optional[str]:
+        b = self.global_state()
+        if not self.dist.is_root:
+            return None
+        cfg = self.cfg
+        path = path or ckpt.path_for(cfg.checkpoint_dir or ".", self.step)
+        meta = dict(dt=cfg.dt, dtype=cfg.dtype, G=cfg.G, cutoff=cfg.cutoff,
+                    softening=cfg.softening, init=cfg.init, seed=cfg.seed,
+                    time=self.step * cfg.dt)
+        return ckpt.save(path, b, self.step, meta)
+
+    def run(self, steps: Optional[int] = None, log: Optional[RunLog] = None) -> RunMetrics:
+        cfg = self.cfg
+        steps = cfg.steps if steps is None else int(steps)
+        periods = [p for p in (cfg.progress_every if log else 0, cfg.checkpoint_every,
+                               cfg.record_every, cfg.nan_check_every) if p and p > 0]
+        comm.barrier(self.dist)
+        t0 = time.perf_counter()
+        s = 0
+        while s < steps:
+            if log and cfg.progress_every and s % cfg.progress_every == 0 and self.dist.is_root:
+                log.progress(s, steps)
+            nxt = min([steps] + [(s // p + 1) * p for p in periods])
+            self.engine.step(nxt - s)
+            s = nxt
+            if cfg.nan_check_every and s % cfg.nan_check_every == 0:
+                self.check_finite()
+            if cfg.record_every and s % cfg.record_every == 0:
+                self.trajectory.append(self.global_state().pos.copy())
+            if cfg.checkpoint_every and s % cfg.checkpoint_every == 0 and cfg.checkpoint_dir:
+                self.save_checkpoint()
+        self.engine.sync()
+        wall = time.perf_counter() - t0
+        wall = comm.allreduce_max(self.dist, wall)
+        self.check_finite()
+        lay = getattr(self.engine, "native_layout", {})
+        from ..ops._native import KERNEL_NAMES, MODE_NAMES
+
+        return RunMetrics(n=cfg.n, steps=steps, dt=cfg.dt, dtype=cfg.dtype, device=self.device,
+                          nranks=self.dist.world, wall_s=wall,
+                          kernel=KERNEL_NAMES.get(lay.get("kernel", 0), "cpu"),
+                          mode=MODE_NAMES.get(lay.get("mode", 0), "cpu"))
+
+    def save_trajectory(self, path: str) -> None:
+        if self.dist.is_root and self.trajectory:
+            np.save(path, np.stack(self.trajectory))
+
+    def close(self) -> None:
+        self.engine.close()

@@ -1,0 +1,164 @@
+"""GPU numerics of the gfx950 force/step kernels against the fp64 oracle.
+
+Tile-edge sizes, both j-source variants (LDS-DMA tiles / SGPR scalar cache), both schedules
+(fused / split), fp32 and fp64, random data. Determinism and schedule-independence are
+bitwise; accuracy is relative to max |a| (fp32 ~1e-6, fp64 ~1e-13).
+"""
+import numpy as np
+import pytest
+
+from gravsim.config import SimConfig
+from gravsim.models import initial_conditions as ic
+from gravsim.models.initial_conditions import BodySet
+from gravsim.ops import oracle
+from gravsim.ops.force import cpu_accelerations
+
+pytestmark = pytest.mark.gpu
+
+SIZES = [1, 2, 3, 63, 64, 65, 1000, 4097]
+
+
+def _engine(n, dtype="fp32", **kw):
+    from gravsim.runtime.engines import HipEngine
+
+    return HipEngine(SimConfig(n=n, dtype=dtype, device="gpu", **kw))
+
+
+def _accel(bodies, dtype, **kw):
+    eng = _engine(bodies.n, dtype, **kw)
+    try:
+        eng.load(bodies)
+        return eng.accel()[: bodies.n]
+    finally:
+        eng.close()
+
+
+@pytest.mark.parametrize("n", SIZES)
+@pytest.mark.parametrize("dtype", ["fp32", "fp64"])
+@pytest.mark.parametrize("kernel", ["lds", "smem"])
+def test_accel_matches_oracle(hip, n, dtype, kernel):
+    b = ic.solar_random(n, seed=7 + n)
+    ref, phi = oracle.accelerations(b.pos, b.mass, with_potential=True)
+    got = _accel(b, dtype, kernel=kernel)
+    scale = np.abs(ref).max() if n > 1 else 1.0
+    tol = 2e-6 if dtype == "fp32" else 1e-13
+    assert np.abs(got[:, :3] - ref).max() <= tol * max(scale, 1e-300) + 1e-300
+    if n > 1:
+        assert np.abs(got[:, 3] - phi).max() <= tol * np.abs(phi).max()
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "fp64"])
+def test_variants_and_schedules_bitwise(hip, dtype):
+    """LDS vs SMEM and fused vs split, every ipl: identical bits (canonical chunk order)."""
+    b = ic.random_cube(5000, seed=3)
+    outs = []
+    for kernel in ("lds", "smem"):
+        for mode in ("fused", "split"):
+            for ipl in (1, 2, 4):
+                eng = _engine(b.n, dtype, kernel=kernel, mode=mode, ipl=ipl)
+                eng.load(b)
+                eng.step(3)
+                outs.append(eng.state().pos)
+                eng.close()
+    for o in outs[1:]:
+        assert np.array_equal(o, outs[0])
+
+
+def test_determinism_two_runs(hip):
+    res = []
+    for _ in range(2):
+        eng = _engine(9000, "fp32")
+        eng.init_ics("solar+random", 11)
+        eng.step(5)
+        res.append(eng.state().pos)
+        eng.close()
+    assert np.array_equal(res[0], res[1])
+
+
+def test_device_ics_match_host(hip):
+    for fam in ("solar+random", "random"):
+        eng = _engine(3000, "fp64")
+        eng.init_ics(fam, 1234)
+        got = eng.state()
+        eng.close()
+        ref = ic.make(fam, 3000, 1234)
+        assert np.array_equal(got.pos, ref.pos)
+        assert np.array_equal(got.mass, ref.mass)
+        assert np.array_equal(got.vel, ref.vel)
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "fp64"])
+def test_steps_match_oracle(hip, dtype):
+    b = ic.solar_random(700, seed=5)
+    eng = _engine(b.n, dtype, dt=3600.0)
+    eng.load(b)
+    eng.step(20)
+    got = eng.state()
+    eng.close()
+    x, v, _ = oracle.simulate(b.pos, b.vel, b.mass, 3600.0, 20)
+    tol = 1e-5 if dtype == "fp32" else 1e-12
+    assert np.abs(got.pos - x).max() / np.abs(x).max() < tol
+    assert np.abs(got.vel - v).max() / np.abs(v).max() < tol * 10
+
+
+def test_graph_replay_equals_eager(hip):
+    outs = []
+    for graph in (True, False):
+        eng = _engine(6000, "fp32", graph=graph)
+        eng.init_ics("solar+random", 2)
+        eng.step(7)
+        outs.append(eng.state().pos)
+        eng.close()
+    assert np.array_equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("P", [2, 3, 4])
+@pytest.mark.parametrize("mode", ["fused", "split"])
+def test_virtual_ranks_bitwise(hip, P, mode):
+    """P shards with the RCCL schedule (overlapped own-chunk partials) == 1 rank, bitwise."""
+    from gravsim.runtime.engines import VirtualGroup
+
+    n = 5000
+    cfg = SimConfig(n=n, dtype="fp32", device="gpu", mode=mode, chunk=1024)
+    g = VirtualGroup(cfg, P)
+    g.init_ics("solar+random", 9)
+    g.step(6)
+    got = g.state()
+    g.close()
+    one = VirtualGroup(cfg, 1)
+    one.init_ics("solar+random", 9)
+    one.step(6)
+    ref = one.state()
+    one.close()
+    assert np.array_equal(got.pos, ref.pos)
+    assert np.array_equal(got.vel, ref.vel)
+
+
+def test_fp32_no_overflow_heavy_masses(hip):
+    """D1: G*m_i*m_j overflows fp32 in the reference; mu = G*m per body does not."""
+    rng = np.random.default_rng(0)
+    n = 512
+    pos = rng.uniform(-3e11, 3e11, (n, 3))
+    mass = rng.uniform(1e24, 1e25, n)
+    mass[0] = 1.989e30
+    b = BodySet(pos, np.zeros((n, 3)), mass)
+    got = _accel(b, "fp32")
+    assert np.isfinite(got).all()
+    ref = oracle.accelerations(pos, mass)
+    assert np.abs(got[:, :3] - ref).max() / np.abs(ref).max() < 2e-6
+
+
+def test_gpu_matches_cpu_engine_fp64(hip):
+    b = ic.solar_random(3000, seed=21)
+    got = _accel(b, "fp64")
+    a, phi = cpu_accelerations(b.pos, b.mass, dtype="fp64")
+    assert np.abs(got[:, :3] - a).max() / np.abs(a).max() < 1e-13
+
+
+def test_nonfinite_guard(hip):
+    b = ic.solar_random(100, seed=1)
+    b.pos[5] = np.nan
+    eng = _engine(b.n, "fp32")
+    eng.load(b)
+    assert eng.nonfinite() > 0
+    eng.close()
