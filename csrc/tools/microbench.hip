@@ -1,0 +1,167 @@
+// gfx950 microbenchmarks that size the N-body kernel design:
+//   1. issue throughput of v_fma_f32 / v_rsq_f32 / v_pk_fma_f32 and of an rsq+fma mix
+//      (does the transcendental overlap with plain VALU under multi-wave load?)
+//   2. throughput of v_mfma_f32_16x16x4_f32 and v_mfma_f32_4x4x1_16b_f32, alone and beside
+//      VALU work (separate pipes?)
+//   3. the operand/result lane layout of v_mfma_f32_4x4x1_16b_f32 (exact integer data)
+// Build: hipcc -O3 --offload-arch=gfx950 csrc/tools/microbench.hip -o microbench
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+#define CK(x)                                                                            \
+  do {                                                                                   \
+    hipError_t e = (x);                                                                  \
+    if (e != hipSuccess) {                                                               \
+      fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e));           \
+      exit(1);                                                                           \
+    }                                                                                    \
+  } while (0)
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+// OPS: 0 fma, 1 rsq, 2 mix(1 rsq + 7 fma), 3 pk_fma, 4 mix(1 rsq + 14 fma)
+template <int OPS>
+__global__ __launch_bounds__(256) void valu_kernel(float* out, int iters, float a, float b) {
+  float x[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) x[u] = 1.0f + 0.001f * (threadIdx.x + u);
+  for (int it = 0; it < iters; ++it) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      if constexpr (OPS == 0) {
+        x[u] = __builtin_fmaf(x[u], a, b);
+      } else if constexpr (OPS == 1) {
+        x[u] = __builtin_amdgcn_rsqf(x[u]);
+      } else if constexpr (OPS == 2) {
+        float y = __builtin_amdgcn_rsqf(x[u]);
+#pragma unroll
+        for (int k = 0; k < 7; ++k) y = __builtin_fmaf(y, a, b);
+        x[u] = y;
+      } else if constexpr (OPS == 4) {
+        float y = __builtin_amdgcn_rsqf(x[u]);
+#pragma unroll
+        for (int k = 0; k < 14; ++k) y = __builtin_fmaf(y, a, b);
+        x[u] = y;
+      }
+    }
+    if constexpr (OPS == 3) {
+      typedef float f2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+      for (int u = 0; u < 8; u += 2) {
+        f2 v = {x[u], x[u + 1]};
+        f2 aa = {a, a}, bb = {b, b};
+        v = __builtin_elementwise_fma(v, aa, bb);
+        x[u] = v.x;
+        x[u + 1] = v.y;
+      }
+    }
+  }
+  float s = 0;
+#pragma unroll
+  for (int u = 0; u < 8; ++u) s += x[u];
+  out[blockIdx.x * 256 + threadIdx.x] = s;
+}
+
+// MFMA throughput; VALU_TOO adds 8 independent fma chains per MFMA.
+template <int SHAPE, bool VALU_TOO>
+__global__ __launch_bounds__(256) void mfma_kernel(float* out, int iters, float a, float b) {
+  f4 acc[4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
+  float av = 0.001f * threadIdx.x, bv = 0.002f * threadIdx.x;
+  float x[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) x[u] = 1.0f + u;
+  for (int it = 0; it < iters; ++it) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if constexpr (SHAPE == 16)
+        acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc[q], 0, 0, 0);
+      else
+        acc[q] = __builtin_amdgcn_mfma_f32_4x4x1f32(av, bv, acc[q], 0, 0, 0);
+      if constexpr (VALU_TOO) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) x[u] = __builtin_fmaf(x[u], a, b);
+      }
+    }
+  }
+  float s = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) s += acc[q].x + acc[q].y + acc[q].z + acc[q].w;
+#pragma unroll
+  for (int u = 0; u < 8; ++u) s += x[u];
+  out[blockIdx.x * 256 + threadIdx.x] = s;
+}
+
+__global__ void layout_kernel(float* out, int mode) {
+  const int l = threadIdx.x;
+  float a = 1.f, b = 1.f;
+  if (mode == 0) a = (float)(l + 1);
+  if (mode == 1) b = (float)(l + 1);
+  f4 c = {0, 0, 0, 0};
+  c = __builtin_amdgcn_mfma_f32_4x4x1f32(a, b, c, 0, 0, 0);
+  for (int r = 0; r < 4; ++r) out[l * 4 + r] = c[r];
+}
+
+template <typename K>
+static float time_kernel(K kern, float* out, int iters, int blocks, int reps) {
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), 0, 0, out, iters, 1.0001f, 0.0001f);
+  CK(hipDeviceSynchronize());
+  CK(hipEventRecord(e0));
+  for (int r = 0; r < reps; ++r)
+    hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), 0, 0, out, iters, 1.0001f, 0.0001f);
+  CK(hipEventRecord(e1));
+  CK(hipEventSynchronize(e1));
+  float ms = 0;
+  CK(hipEventElapsedTime(&ms, e0, e1));
+  return ms / reps;
+}
+
+int main() {
+  int cus = 0;
+  CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+  int clk_khz = 0;
+  CK(hipDeviceGetAttribute(&clk_khz, hipDeviceAttributeClockRate, 0));
+  const int blocks = cus * 8;  // 8 workgroups of 4 waves per CU -> 8 waves per SIMD
+  float* out;
+  CK(hipMalloc(&out, (size_t)blocks * 256 * sizeof(float)));
+  const int iters = 2048;
+  const double waves_per_simd = (double)blocks * 4 / (cus * 4);
+  printf("{\"cus\": %d, \"clock_mhz\": %.0f}\n", cus, clk_khz / 1e3);
+  struct { const char* name; float ms; double instr_per_iter; } r[5];
+  r[0] = {"v_fma_f32 x8", time_kernel(valu_kernel<0>, out, iters, blocks, 5), 8};
+  r[1] = {"v_rsq_f32 x8", time_kernel(valu_kernel<1>, out, iters, blocks, 5), 8};
+  r[2] = {"(rsq + 7 fma) x8", time_kernel(valu_kernel<2>, out, iters, blocks, 5), 64};
+  r[3] = {"v_pk_fma_f32 x4", time_kernel(valu_kernel<3>, out, iters, blocks, 5), 4};
+  r[4] = {"(rsq + 14 fma) x8", time_kernel(valu_kernel<4>, out, iters, blocks, 5), 120};
+  for (auto& x : r) {
+    // wave-instructions per SIMD = waves_per_simd * iters * instr_per_iter
+    const double wi = waves_per_simd * iters * x.instr_per_iter;
+    const double ns_per_wi = x.ms * 1e6 / wi;
+    printf("{\"test\": \"%s\", \"ms\": %.4f, \"ns_per_wave_instr_per_simd\": %.4f, "
+           "\"cycles_at_2.4GHz\": %.3f}\n", x.name, x.ms, ns_per_wi, ns_per_wi * 2.4);
+  }
+  struct { const char* name; float ms; } m[4];
+  m[0] = {"mfma 16x16x4 f32", time_kernel(mfma_kernel<16, false>, out, iters, blocks, 5)};
+  m[1] = {"mfma 4x4x1_16b f32", time_kernel(mfma_kernel<4, false>, out, iters, blocks, 5)};
+  m[2] = {"mfma 16x16x4 + 8 fma", time_kernel(mfma_kernel<16, true>, out, iters, blocks, 5)};
+  m[3] = {"mfma 4x4x1 + 8 fma", time_kernel(mfma_kernel<4, true>, out, iters, blocks, 5)};
+  for (auto& x : m) {
+    const double mi = waves_per_simd * iters * 4;
+    const double ns = x.ms * 1e6 / mi;
+    printf("{\"test\": \"%s\", \"ms\": %.4f, \"ns_per_mfma_per_simd\": %.4f, "
+           "\"cycles_at_2.4GHz\": %.3f}\n", x.name, x.ms, ns, ns * 2.4);
+  }
+  float h[256];
+  for (int mode = 0; mode < 2; ++mode) {
+    hipLaunchKernelGGL(layout_kernel, dim3(1), dim3(64), 0, 0, out, mode);
+    CK(hipMemcpy(h, out, sizeof(h), hipMemcpyDeviceToHost));
+    printf("{\"layout_4x4x1\": \"%s\", \"D\": [", mode == 0 ? "A=lane+1,B=1" : "A=1,B=lane+1");
+    for (int i = 0; i < 256; ++i) printf("%s%.0f", i ? "," : "", h[i]);
+    printf("]}\n");
+  }
+  CK(hipFree(out));
+  return 0;
+}

@@ -43,8 +43,9 @@ def test_accel_matches_oracle(hip, n, dtype, kernel):
     scale = np.abs(ref).max() if n > 1 else 1.0
     tol = 2e-6 if dtype == "fp32" else 1e-13
     assert np.abs(got[:, :3] - ref).max() <= tol * max(scale, 1e-300) + 1e-300
-    if n > 1:
-        assert np.abs(got[:, 3] - phi).max() <= tol * np.abs(phi).max()
+    if n > 1:  # the potential is a sum of positive terms: fp32 summation noise ~ sqrt(n) eps
+        ptol = 2e-5 if dtype == "fp32" else 1e-13
+        assert np.abs(got[:, 3] - phi).max() <= ptol * np.abs(phi).max()
 
 
 @pytest.mark.parametrize("dtype", ["fp32", "fp64"])
