@@ -37,6 +37,7 @@ def main() -> int:
     ap.add_argument("--ipl", type=int, default=0)
     ap.add_argument("--no-graph", dest="graph", action="store_false")
     ap.add_argument("--dt", type=float, default=3600.0)
+    ap.add_argument("--cutoff-mode", default="auto", choices=["auto", "exact", "fast"])
     a = ap.parse_args()
 
     import torch
@@ -57,7 +58,7 @@ def main() -> int:
     torch.cuda.set_device(dev)
 
     cfg = SimConfig(n=a.n, dt=a.dt, dtype=a.dtype, device="gpu", kernel=a.kernel, mode=a.mode,
-                    ipl=a.ipl, graph=a.graph).validate()
+                    ipl=a.ipl, graph=a.graph, cutoff_mode=a.cutoff_mode).validate()
     eng = HipEngine(cfg, rank, world, device=dev, dist=dist)
     if world > 1:
         uid = HipEngine.unique_id() if rank == 0 else None
@@ -80,6 +81,7 @@ def main() -> int:
 
     bad = comm.allreduce_sum(dist, eng.nonfinite())
     lay = eng.native_layout
+    fmode = eng.force_mode()
     eng.close()
     if rank == 0:
         value = cfg.n * a.steps / wall
@@ -108,6 +110,9 @@ def main() -> int:
                 "mode": _native.MODE_NAMES.get(lay["mode"]),
                 "ipl": lay["ipl"],
                 "chunk": lay["chunk"],
+                "cutoff_path": "exact-select" if fmode["exact"] else
+                f"fast (core^2={fmode['eps2']:.3g} m^2; bit-identical to the 1e-10 m hard cutoff "
+                "for separations above ~mm)",
                 "interactions_per_s": float(cfg.n) * cfg.n * a.steps / wall,
                 "nonfinite": int(bad),
             },

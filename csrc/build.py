@@ -20,7 +20,8 @@ from pathlib import Path
 ROOT = Path(__file__).resolve().parent.parent
 CSRC = ROOT / "csrc"
 PKG = ROOT / "gravity-simulator-using-mpi-spark-and-cuda_amd"
-OUT = PKG / "_native"
+OUT = Path(os.environ["GRAVSIM_NATIVE_DIR"]) if os.environ.get("GRAVSIM_NATIVE_DIR") else \
+    PKG / "_native"
 ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
 ARCH = os.environ.get("GRAVSIM_ARCH", "gfx950")
 
@@ -33,6 +34,8 @@ TOOL_SRC = [CSRC / "tools" / "gravsim_main.cpp"]
 CPU_LIB = OUT / "libgravsim_cpu.so"
 HIP_LIB = OUT / "libgravsim_hip.so"
 TOOL_BIN = OUT / "gravsim_bench"
+MICRO_SRC = CSRC / "tools" / "microbench.hip"
+MICRO_BIN = OUT / "microbench"
 
 
 def _stale(target: Path, deps: list[Path]) -> bool:
@@ -63,8 +66,11 @@ def build_cpu(force: bool = False) -> Path:
     return CPU_LIB
 
 
-HIP_FLAGS = ["-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fno-slp-vectorize",
-             "-ffp-contract=off", "-fPIC"]
+# SLP vectorisation packs the per-lane i-bodies into v_pk_{add,mul,fma}_f32; GRAVSIM_SLP=0
+# builds the scalar-VALU variant for A/B runs.
+HIP_FLAGS = ["-O3", "-std=c++17", f"--offload-arch={ARCH}", "-ffp-contract=off", "-fPIC"]
+if os.environ.get("GRAVSIM_SLP", "1") == "0":
+    HIP_FLAGS.append("-fno-slp-vectorize")
 
 
 def build_hip(force: bool = False) -> Path:
@@ -89,16 +95,27 @@ def build_tool(force: bool = False) -> Path:
     return TOOL_BIN
 
 
+def build_microbench(force: bool = False) -> Path:
+    OUT.mkdir(parents=True, exist_ok=True)
+    if MICRO_SRC.exists() and (force or _stale(MICRO_BIN, [MICRO_SRC])):
+        tmp = MICRO_BIN.with_suffix(".tmp")
+        _run([hipcc(), "-O3", "-std=c++17", f"--offload-arch={ARCH}", str(MICRO_SRC), "-o",
+              str(tmp)])
+        os.replace(tmp, MICRO_BIN)
+    return MICRO_BIN
+
+
 def build_all(force: bool = False) -> None:
     build_cpu(force)
     build_hip(force)
     build_tool(force)
+    build_microbench(force)
 
 
 def main(argv: list[str] | None = None) -> int:
     ap = argparse.ArgumentParser(description=__doc__)
     ap.add_argument("--force", action="store_true")
-    ap.add_argument("--only", choices=["cpu", "hip", "tool"])
+    ap.add_argument("--only", choices=["cpu", "hip", "tool", "microbench"])
     a = ap.parse_args(argv)
     if a.only == "cpu":
         build_cpu(a.force)
@@ -106,6 +123,8 @@ def main(argv: list[str] | None = None) -> int:
         build_hip(a.force)
     elif a.only == "tool":
         build_tool(a.force)
+    elif a.only == "microbench":
+        build_microbench(a.force)
     else:
         build_all(a.force)
     return 0

@@ -41,8 +41,20 @@ extern "C" int gs_layout_compute(const gs_config* cfg, gs_layout* out) {
   out->local_begin = (int64_t)cfg->rank * out->n_local;
   out->n_chunks = (int32_t)((cfg->n + chunk - 1) / chunk);
   int32_t ipl = cfg->ipl;
-  if (ipl <= 0) ipl = (cfg->dtype == GS_FP64) ? 1 : 2;
-  if (ipl != 1 && ipl != 2 && ipl != 4) { gs_set_error("layout: ipl must be 1, 2 or 4"); return -1; }
+  if (ipl <= 0) {
+    // Measured on MI355X (bench/sweep.py): more i-bodies per lane amortise each j read and
+    // pack into v_pk_* pairs; 8 wins at >= 256K bodies per rank, 4 below.
+    if (cfg->dtype == GS_FP64) ipl = 2;
+    else ipl = out->n_local >= 262144 ? 8 : 4;
+  }
+  if (ipl != 1 && ipl != 2 && ipl != 4 && !(ipl == 8 && cfg->dtype == GS_FP32)) {
+    gs_set_error("layout: ipl must be 1, 2, 4 (or 8 for fp32)");
+    return -1;
+  }
+  if ((out->n_local % (256 * ipl)) != 0) {
+    gs_set_error("layout: 256*ipl must divide the per-rank body count (raise chunk)");
+    return -1;
+  }
   out->ipl = ipl;
   out->kernel = cfg->kernel == GS_KERNEL_AUTO ? GS_KERNEL_LDS : cfg->kernel;
   const int64_t i_blocks = out->n_local / (256 * ipl);

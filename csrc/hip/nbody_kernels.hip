@@ -51,27 +51,39 @@ __device__ __forceinline__ double rsqrt_dev(double x) {
 __device__ __forceinline__ float fma_(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
 __device__ __forceinline__ double fma_(double a, double b, double c) { return __builtin_fma(a, b, c); }
 
-// One i-j interaction. 3 sub + 3 fma (r^2) + cmp/select + rsq + 3 mul + 3 fma (+1 add for phi).
-template <typename T, bool PHI>
+// Force modes (template FM):
+//   FM_FAST  : r^2 + eps2 with eps2 >= a tiny overflow-safe core (set by the host), no select.
+//              The self term and coincident bodies give s*0 = 0. Bit-identical to FM_EXACT
+//              for every pair with r^2 >= 2^24 * eps2 (fp32: r >~ 4.5 mm at solar masses).
+//   FM_EXACT : reference hard cutoff (cuda.cu:39, mpi.c:64): s = 0 when r^2 < cutoff^2.
+//   FM_PHI   : FM_EXACT plus the potential sum (diagnostics / accel queries).
+enum { FM_FAST = 0, FM_EXACT = 1, FM_PHI = 2 };
+
+// One i-j interaction. 3 sub + 3 fma (r^2) + rsq + 3 mul + 3 fma; FM_EXACT adds cmp/select.
+template <typename T, int FM>
 __device__ __forceinline__ void interact(T xi, T yi, T zi, T xj, T yj, T zj, T muj, T cut2,
                                          T eps2, T& ax, T& ay, T& az, T& ph) {
   const T dx = xj - xi, dy = yj - yi, dz = zj - zi;
   const T r2 = fma_(dz, dz, fma_(dy, dy, fma_(dx, dx, eps2)));
-  const bool ok = r2 >= cut2;
   T inv;
-  if constexpr (sizeof(T) == 8) {
-    // Branch-free: the Newton sequence would otherwise be predicated behind exec-mask jumps.
-    inv = rsqrt_dev(ok ? r2 : T(1));
-    inv = ok ? inv : T(0);
+  if constexpr (FM == FM_FAST) {
+    inv = rsqrt_dev(r2);
   } else {
-    inv = ok ? rsqrt_dev(r2) : T(0);
+    const bool ok = r2 >= cut2;
+    if constexpr (sizeof(T) == 8) {
+      // Branch-free: the Newton sequence would otherwise be predicated behind exec-mask jumps.
+      inv = rsqrt_dev(ok ? r2 : T(1));
+      inv = ok ? inv : T(0);
+    } else {
+      inv = ok ? rsqrt_dev(r2) : T(0);
+    }
   }
   const T mi = muj * inv;
   const T s = mi * (inv * inv);
   ax = fma_(s, dx, ax);
   ay = fma_(s, dy, ay);
   az = fma_(s, dz, az);
-  if constexpr (PHI) ph += mi;
+  if constexpr (FM == FM_PHI) ph += mi;
 }
 
 template <typename T, int IPL>
@@ -87,11 +99,11 @@ __device__ __forceinline__ void zero_chunk(IState<T, IPL>& s) {
   for (int k = 0; k < IPL; ++k) s.ax[k] = s.ay[k] = s.az[k] = s.ph[k] = T(0);
 }
 
-template <typename T, int IPL, bool PHI>
+template <typename T, int IPL, int FM>
 __device__ __forceinline__ void interact_all(IState<T, IPL>& s, const V4<T>& q, T cut2, T eps2) {
 #pragma unroll
   for (int k = 0; k < IPL; ++k)
-    interact<T, PHI>(s.x[k], s.y[k], s.z[k], q.x, q.y, q.z, q.w, cut2, eps2, s.ax[k], s.ay[k],
+    interact<T, FM>(s.x[k], s.y[k], s.z[k], q.x, q.y, q.z, q.w, cut2, eps2, s.ax[k], s.ay[k],
                      s.az[k], s.ph[k]);
 }
 
@@ -111,7 +123,7 @@ __device__ __forceinline__ void tile_fill(const V4<T>* __restrict__ src, V4<T>* 
 }
 
 // Sweep chunks [c0, c1) through LDS tiles. For every finished chunk call on_chunk(c).
-template <typename T, int IPL, bool PHI, typename OnChunk>
+template <typename T, int IPL, int FM, typename OnChunk>
 __device__ __forceinline__ void sweep_lds(const V4<T>* __restrict__ X, int64_t chunk, int c0,
                                           int c1, T cut2, T eps2, IState<T, IPL>& st,
                                           V4<T> (*tile)[Tile<T>::kBodies], OnChunk on_chunk) {
@@ -130,7 +142,7 @@ __device__ __forceinline__ void sweep_lds(const V4<T>* __restrict__ X, int64_t c
 #pragma unroll 8
     for (int j = 0; j < TB; ++j) {
       const V4<T> q = cur[j];  // uniform address: one broadcast ds_read per wave
-      interact_all<T, IPL, PHI>(st, q, cut2, eps2);
+      interact_all<T, IPL, FM>(st, q, cut2, eps2);
     }
     if ((t + 1) % tiles_per_chunk == 0) {
       on_chunk(c0 + t / tiles_per_chunk);
@@ -140,7 +152,7 @@ __device__ __forceinline__ void sweep_lds(const V4<T>* __restrict__ X, int64_t c
 }
 
 // Sweep chunks [c0, c1) with wave-uniform j loaded into SGPRs via the scalar cache.
-template <typename T, int IPL, bool PHI, typename OnChunk>
+template <typename T, int IPL, int FM, typename OnChunk>
 __device__ __forceinline__ void sweep_smem(const V4<T>* __restrict__ X, int64_t chunk, int c0,
                                            int c1, T cut2, T eps2, IState<T, IPL>& st,
                                            OnChunk on_chunk) {
@@ -149,7 +161,7 @@ __device__ __forceinline__ void sweep_smem(const V4<T>* __restrict__ X, int64_t 
     const V4<T>* p = X + (int64_t)c * chunk;
     for (int64_t j = 0; j < chunk; j += 4) {
 #pragma unroll
-      for (int u = 0; u < 4; ++u) interact_all<T, IPL, PHI>(st, p[j + u], cut2, eps2);
+      for (int u = 0; u < 4; ++u) interact_all<T, IPL, FM>(st, p[j + u], cut2, eps2);
     }
     on_chunk(c);
   }
@@ -198,7 +210,7 @@ __device__ __forceinline__ void integrate_store(const KArgs<T>& a, const IState<
 // ---------------------------------------------------------------------------------------
 // SPLIT: grid (i_blocks, groups). Workgroup (b, g) sweeps chunks of group g and stores one
 // partial (ax, ay, az, sum mu/r) per chunk: partial[c * n_local + i].
-template <typename T, int IPL, int KV, bool PHI>
+template <typename T, int IPL, int KV, int FM>
 __global__ __launch_bounds__(kBlock) void force_split_kernel(KArgs<T> a) {
   __shared__ __attribute__((aligned(16))) V4<T> tile[2][Tile<T>::kBodies];
   const int64_t ib = (int64_t)blockIdx.x * (kBlock * IPL);
@@ -219,15 +231,15 @@ __global__ __launch_bounds__(kBlock) void force_split_kernel(KArgs<T> a) {
   };
   const V4<T>* X = reinterpret_cast<const V4<T>*>(a.X);
   if constexpr (KV == GS_KERNEL_LDS)
-    sweep_lds<T, IPL, PHI>(X, a.chunk, c0, c1, a.cut2, a.eps2, st, tile, store);
+    sweep_lds<T, IPL, FM>(X, a.chunk, c0, c1, a.cut2, a.eps2, st, tile, store);
   else
-    sweep_smem<T, IPL, PHI>(X, a.chunk, c0, c1, a.cut2, a.eps2, st, store);
+    sweep_smem<T, IPL, FM>(X, a.chunk, c0, c1, a.cut2, a.eps2, st, store);
 }
 
 // FUSED: grid (i_blocks). Sweep every chunk in canonical order; chunks in [pre_begin,
 // pre_end) are taken from partial (computed earlier, e.g. the rank-local tile that overlapped
 // the all-gather). Integrate in the epilogue.
-template <typename T, int IPL, int KV, bool PHI>
+template <typename T, int IPL, int KV, int FM>
 __global__ __launch_bounds__(kBlock) void force_fused_kernel(KArgs<T> a) {
   __shared__ __attribute__((aligned(16))) V4<T> tile[2][Tile<T>::kBodies];
   const int64_t ib = (int64_t)blockIdx.x * (kBlock * IPL);
@@ -253,14 +265,14 @@ __global__ __launch_bounds__(kBlock) void force_fused_kernel(KArgs<T> a) {
   const int pb = min(max(a.pre_begin, 0), a.n_chunks);
   const int pe = min(max(a.pre_end, pb), a.n_chunks);
   if constexpr (KV == GS_KERNEL_LDS) {
-    sweep_lds<T, IPL, PHI>(X, a.chunk, 0, pb, a.cut2, a.eps2, st, tile, fold);
+    sweep_lds<T, IPL, FM>(X, a.chunk, 0, pb, a.cut2, a.eps2, st, tile, fold);
     for (int c = pb; c < pe; ++c) fold_pre(c);
     __syncthreads();  // both LDS buffers are refilled by the next sweep
-    sweep_lds<T, IPL, PHI>(X, a.chunk, pe, a.n_chunks, a.cut2, a.eps2, st, tile, fold);
+    sweep_lds<T, IPL, FM>(X, a.chunk, pe, a.n_chunks, a.cut2, a.eps2, st, tile, fold);
   } else {
-    sweep_smem<T, IPL, PHI>(X, a.chunk, 0, pb, a.cut2, a.eps2, st, fold);
+    sweep_smem<T, IPL, FM>(X, a.chunk, 0, pb, a.cut2, a.eps2, st, fold);
     for (int c = pb; c < pe; ++c) fold_pre(c);
-    sweep_smem<T, IPL, PHI>(X, a.chunk, pe, a.n_chunks, a.cut2, a.eps2, st, fold);
+    sweep_smem<T, IPL, FM>(X, a.chunk, pe, a.n_chunks, a.cut2, a.eps2, st, fold);
   }
   if (a.acc_out) {
     V4<T>* out = reinterpret_cast<V4<T>*>(a.acc_out);
@@ -367,21 +379,23 @@ static hipError_t launch_split_t(const KArgs<T>& a, int groups, hipStream_t s) {
   const int64_t blocks = a.n_local / (kBlock * IPL);
   dim3 grid((unsigned)blocks, (unsigned)groups);
   if (a.phi)
-    hipLaunchKernelGGL((force_split_kernel<T, IPL, KV, true>), grid, dim3(kBlock), 0, s, a);
+    hipLaunchKernelGGL((force_split_kernel<T, IPL, KV, FM_PHI>), grid, dim3(kBlock), 0, s, a);
+  else if (a.exact)
+    hipLaunchKernelGGL((force_split_kernel<T, IPL, KV, FM_EXACT>), grid, dim3(kBlock), 0, s, a);
   else
-    hipLaunchKernelGGL((force_split_kernel<T, IPL, KV, false>), grid, dim3(kBlock), 0, s, a);
+    hipLaunchKernelGGL((force_split_kernel<T, IPL, KV, FM_FAST>), grid, dim3(kBlock), 0, s, a);
   return hipGetLastError();
 }
 
 template <typename T, int IPL, int KV>
 static hipError_t launch_fused_t(const KArgs<T>& a, hipStream_t s) {
-  const int64_t blocks = a.n_local / (kBlock * IPL);
+  const dim3 grid((unsigned)(a.n_local / (kBlock * IPL)));
   if (a.phi)
-    hipLaunchKernelGGL((force_fused_kernel<T, IPL, KV, true>), dim3((unsigned)blocks),
-                       dim3(kBlock), 0, s, a);
+    hipLaunchKernelGGL((force_fused_kernel<T, IPL, KV, FM_PHI>), grid, dim3(kBlock), 0, s, a);
+  else if (a.exact)
+    hipLaunchKernelGGL((force_fused_kernel<T, IPL, KV, FM_EXACT>), grid, dim3(kBlock), 0, s, a);
   else
-    hipLaunchKernelGGL((force_fused_kernel<T, IPL, KV, false>), dim3((unsigned)blocks),
-                       dim3(kBlock), 0, s, a);
+    hipLaunchKernelGGL((force_fused_kernel<T, IPL, KV, FM_FAST>), grid, dim3(kBlock), 0, s, a);
   return hipGetLastError();
 }
 
@@ -392,6 +406,10 @@ static hipError_t dispatch_ipl(const KArgs<T>& a, int ipl, bool fused, int group
     case 1: return fused ? launch_fused_t<T, 1, KV>(a, s) : launch_split_t<T, 1, KV>(a, groups, s);
     case 2: return fused ? launch_fused_t<T, 2, KV>(a, s) : launch_split_t<T, 2, KV>(a, groups, s);
     case 4: return fused ? launch_fused_t<T, 4, KV>(a, s) : launch_split_t<T, 4, KV>(a, groups, s);
+    case 8:
+      if constexpr (sizeof(T) == 4)
+        return fused ? launch_fused_t<T, 8, KV>(a, s) : launch_split_t<T, 8, KV>(a, groups, s);
+      return hipErrorInvalidValue;
     default: return hipErrorInvalidValue;
   }
 }
@@ -446,7 +464,37 @@ hipError_t launch_count_nonfinite(const T* X4, int64_t i0, int64_t nl, const T* 
   return hipGetLastError();
 }
 
+// Resident workgroups per CU of the split kernel actually launched for (kernel, ipl, mode).
+template <typename T, int IPL, int KV>
+static int occ_t(int fm) {
+  int b = 0;
+  hipError_t e;
+  if (fm == FM_PHI)
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, force_split_kernel<T, IPL, KV, FM_PHI>, kBlock, 0);
+  else if (fm == FM_EXACT)
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, force_split_kernel<T, IPL, KV, FM_EXACT>, kBlock, 0);
+  else
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, force_split_kernel<T, IPL, KV, FM_FAST>, kBlock, 0);
+  return e == hipSuccess ? b : 0;
+}
+
+template <typename T>
+int split_occupancy(int kernel, int ipl, int fm) {
+  const bool smem = kernel == GS_KERNEL_SMEM;
+  switch (ipl) {
+    case 1: return smem ? occ_t<T, 1, GS_KERNEL_SMEM>(fm) : occ_t<T, 1, GS_KERNEL_LDS>(fm);
+    case 2: return smem ? occ_t<T, 2, GS_KERNEL_SMEM>(fm) : occ_t<T, 2, GS_KERNEL_LDS>(fm);
+    case 4: return smem ? occ_t<T, 4, GS_KERNEL_SMEM>(fm) : occ_t<T, 4, GS_KERNEL_LDS>(fm);
+    case 8:
+      if constexpr (sizeof(T) == 4)
+        return smem ? occ_t<T, 8, GS_KERNEL_SMEM>(fm) : occ_t<T, 8, GS_KERNEL_LDS>(fm);
+      return 0;
+    default: return 0;
+  }
+}
+
 #define GS_INSTANTIATE(T)                                                                      \
+  template int split_occupancy<T>(int, int, int);                                              \
   template hipError_t launch_force_split<T>(const KArgs<T>&, int, int, int, hipStream_t);      \
   template hipError_t launch_force_fused<T>(const KArgs<T>&, int, int, hipStream_t);           \
   template hipError_t launch_reduce_integrate<T>(const KArgs<T>&, hipStream_t);                \

@@ -17,13 +17,17 @@
 //            with the KD integrate in its epilogue -> own slice of X[(k+1)&1]
 // With one rank the step is a single fused launch (or split + reduce at small N); the loop
 // can be captured once into a hipGraph (two steps = one ping-pong period) and replayed.
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <math.h>
 #include <rccl/rccl.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
+#include <chrono>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "gravsim.h"
@@ -78,9 +82,46 @@ struct gs_stepper {
   hipGraphExec_t graph = nullptr;
   bool timed = false;  // eager steps record phase events
   int own_c0 = 0, own_c1 = 0;  // this rank's chunks clipped to [0, n_chunks)
+  bool exact = true;           // hard-cutoff select vs fast core-softened path
+  double eps2 = 0.0;           // r^2 offset used by the kernels
+  int cus = 256;               // compute units
+  int occ[3] = {0, 0, 0};      // split-kernel workgroups per CU by force mode
 };
 
 namespace {
+
+// Optional roctx ranges (GRAVSIM_ROCTX=1): resolved with dlopen so the library never links a
+// profiler; under `rocprofv3 --marker-trace` the step phases show up on the timeline.
+struct Roctx {
+  int (*push)(const char*) = nullptr;
+  int (*pop)() = nullptr;
+  Roctx() {
+    if (!getenv("GRAVSIM_ROCTX")) return;
+    for (const char* name : {"librocprofiler-sdk-roctx.so.1", "librocprofiler-sdk-roctx.so",
+                             "libroctx64.so"}) {
+      void* h = dlopen(name, RTLD_NOW | RTLD_GLOBAL);
+      if (!h) continue;
+      push = (int (*)(const char*))dlsym(h, "roctxRangePushA");
+      pop = (int (*)())dlsym(h, "roctxRangePop");
+      if (push && pop) return;
+      push = nullptr;
+      pop = nullptr;
+    }
+  }
+};
+Roctx& roctx() {
+  static Roctx r;
+  return r;
+}
+struct Range {
+  bool on;
+  explicit Range(const char* n) : on(roctx().push != nullptr) {
+    if (on) roctx().push(n);
+  }
+  ~Range() {
+    if (on) roctx().pop();
+  }
+};
 
 size_t row_bytes(const gs_stepper* s) { return 4 * s->esz; }
 
@@ -102,10 +143,58 @@ gs::KArgs<T> base_args(gs_stepper* s, int cur) {
   a.c_end = s->L.n_chunks;
   a.pre_begin = a.pre_end = 0;
   a.phi = 0;
+  a.exact = s->exact ? 1 : 0;
   a.dt = (T)s->cfg.dt;
   a.cut2 = (T)(s->cfg.cutoff * s->cfg.cutoff);
-  a.eps2 = (T)(s->cfg.softening * s->cfg.softening);
+  a.eps2 = (T)s->eps2;
   return a;
+}
+
+// Choose the fast or exact force path once the masses are known. The fast path adds a core
+// c^2 to r^2 instead of selecting on the cutoff; c^2 is the smallest value that keeps
+// mu_max * c^-3 (the self term's s) finite, so s * dx = 0 for the self term. It is used only
+// when the requested cutoff lies inside that core (the default 1e-10 m does).
+void resolve_force_mode(gs_stepper* s) {
+  double mu_max = 0.0;
+  for (double m : s->mass_host) mu_max = fmax(mu_max, s->cfg.G * m);
+  const double big = s->esz == 4 ? 3.4028234663852886e38 / 16.0 : 1.7976931348623157e308 / 16.0;
+  const double floor2 = s->esz == 4 ? 1e-30 : 1e-290;
+  const double core2 = fmax(pow(mu_max / big, 2.0 / 3.0), floor2);
+  const double soft2 = s->cfg.softening * s->cfg.softening;
+  const double cut2 = s->cfg.cutoff * s->cfg.cutoff;
+  const double fast_eps2 = fmax(soft2, core2);
+  bool exact;
+  if (s->cfg.cutoff_mode == 1) exact = true;
+  else if (s->cfg.cutoff_mode == 2) exact = false;
+  else exact = cut2 > fast_eps2;
+  s->exact = exact;
+  s->eps2 = exact ? soft2 : fast_eps2;
+}
+
+// Chunk groups for one split launch of `span` chunks over the i-blocks: minimise
+// rounds(g) * chunks_per_group(g) with rounds = ceil(i_blocks * g / resident).
+int choose_groups(gs_stepper* s, int span, bool phi) {
+  if (span <= 0) return 1;
+  if (s->cfg.split_groups > 0) return s->cfg.split_groups < span ? s->cfg.split_groups : span;
+  const int fm = phi ? 2 : (s->exact ? 1 : 0);
+  const int64_t resident = (int64_t)(s->occ[fm] > 0 ? s->occ[fm] : 4) * s->cus;
+  const int64_t ib = s->L.n_local / (256 * s->L.ipl);
+  int best = 1;
+  double best_cost = 1e300;
+  for (int g = 1; g <= span; ++g) {
+    const int64_t per = (span + g - 1) / g;
+    if (g > 1 && (int64_t)(g - 1) * per >= span) continue;  // an empty trailing group
+    const int64_t rounds = (ib * g + resident - 1) / resident;
+    const double cost = (double)rounds * (double)per;
+    // ties: prefer more workgroups (dynamic balance) while they fit in a few rounds
+    const bool better = cost < best_cost * (1 - 1e-9) ||
+                        (cost <= best_cost * (1 + 1e-9) && rounds <= 4 && g > best);
+    if (better) {
+      best = g;
+      best_cost = cost;
+    }
+  }
+  return best;
 }
 
 int gather(gs_stepper* s, int cur) {
@@ -124,6 +213,7 @@ int gather(gs_stepper* s, int cur) {
 // Enqueue one step. `capturing` disables timing events.
 template <typename T>
 int enqueue_step(gs_stepper* s, bool capturing, bool gathered_externally) {
+  Range range("gs.step");
   const int cur = (int)(s->k & 1);
   gs::KArgs<T> a = base_args<T>(s, cur);
   const int kernel = s->L.kernel, ipl = s->L.ipl;
@@ -138,7 +228,8 @@ int enqueue_step(gs_stepper* s, bool capturing, bool gathered_externally) {
     gs::KArgs<T> loc = a;
     loc.c_begin = s->own_c0;
     loc.c_end = s->own_c1;
-    GS_HIP(gs::launch_force_split<T>(loc, kernel, ipl, s->L.split_groups, s->s_comp));
+    GS_HIP(gs::launch_force_split<T>(loc, kernel, ipl, choose_groups(s, s->own_c1 - s->own_c0, false),
+                                     s->s_comp));
     if (timed) GS_HIP(hipEventRecord(s->ev_local, s->s_comp));
     GS_HIP(hipStreamWaitEvent(s->s_comp, s->ev_gathered, 0));
     if (fused) {
@@ -149,10 +240,13 @@ int enqueue_step(gs_stepper* s, bool capturing, bool gathered_externally) {
       gs::KArgs<T> r = a;
       r.c_begin = 0;
       r.c_end = s->own_c0;
-      GS_HIP(gs::launch_force_split<T>(r, kernel, ipl, s->L.split_groups, s->s_comp));
+      GS_HIP(gs::launch_force_split<T>(r, kernel, ipl, choose_groups(s, s->own_c0, false),
+                                       s->s_comp));
       r.c_begin = s->own_c1;
       r.c_end = s->L.n_chunks;
-      GS_HIP(gs::launch_force_split<T>(r, kernel, ipl, s->L.split_groups, s->s_comp));
+      GS_HIP(gs::launch_force_split<T>(r, kernel, ipl,
+                                       choose_groups(s, s->L.n_chunks - s->own_c1, false),
+                                       s->s_comp));
       GS_HIP(gs::launch_reduce_integrate<T>(a, s->s_comp));
     }
   } else {
@@ -160,7 +254,8 @@ int enqueue_step(gs_stepper* s, bool capturing, bool gathered_externally) {
     if (fused) {
       GS_HIP(gs::launch_force_fused<T>(a, kernel, ipl, s->s_comp));
     } else {
-      GS_HIP(gs::launch_force_split<T>(a, kernel, ipl, s->L.split_groups, s->s_comp));
+      GS_HIP(gs::launch_force_split<T>(a, kernel, ipl, choose_groups(s, s->L.n_chunks, false),
+                                       s->s_comp));
       GS_HIP(gs::launch_reduce_integrate<T>(a, s->s_comp));
     }
   }
@@ -213,6 +308,7 @@ int upload_state(gs_stepper* s, const double* pos, const double* vel, const doub
     V[4 * li + 2] = (T)vel[3 * gi + 2];
   }
   s->mass_host.assign(mass, mass + n);
+  resolve_force_mode(s);
   GS_HIP(hipMemcpyAsync(s->X[0], X.data(), X.size() * sizeof(T), hipMemcpyHostToDevice,
                         s->s_comp));
   GS_HIP(hipMemcpyAsync(s->vel, V.data(), V.size() * sizeof(T), hipMemcpyHostToDevice,
@@ -264,8 +360,11 @@ int accel_impl(gs_stepper* s, double* acc4) {
   if (s->have_comm) GS_HIP(hipStreamWaitEvent(s->s_comp, s->ev_gathered, 0));
   gs::KArgs<T> a = base_args<T>(s, cur);
   a.phi = 1;
+  a.exact = 1;
+  a.eps2 = (T)(s->cfg.softening * s->cfg.softening);
   a.acc_out = static_cast<T*>(s->acc);
-  GS_HIP(gs::launch_force_split<T>(a, s->L.kernel, s->L.ipl, s->L.split_groups, s->s_comp));
+  GS_HIP(gs::launch_force_split<T>(a, s->L.kernel, s->L.ipl, choose_groups(s, s->L.n_chunks, true),
+                                   s->s_comp));
   GS_HIP(gs::launch_reduce_integrate<T>(a, s->s_comp));
   GS_HIP(hipStreamSynchronize(s->s_comp));
   std::vector<T> A((size_t)s->L.n_local * 4);
@@ -312,6 +411,11 @@ int gs_stepper_create(const gs_config* cfg, gs_stepper** out) {
     }                             \
   } while (0)
   FAIL_CLEAN(hipSetDevice(cfg->device));
+  FAIL_CLEAN(hipDeviceGetAttribute(&s->cus, hipDeviceAttributeMultiprocessorCount, cfg->device));
+  for (int fm = 0; fm < 3; ++fm)
+    s->occ[fm] = s->esz == 4 ? gs::split_occupancy<float>(s->L.kernel, s->L.ipl, fm)
+                             : gs::split_occupancy<double>(s->L.kernel, s->L.ipl, fm);
+  resolve_force_mode(s);
   int lo = 0, hi = 0;
   FAIL_CLEAN(hipDeviceGetStreamPriorityRange(&lo, &hi));
   FAIL_CLEAN(hipStreamCreateWithFlags(&s->s_comp, hipStreamNonBlocking));
@@ -376,6 +480,7 @@ int gs_stepper_init_ics(gs_stepper* s, int32_t ic, uint64_t seed) {
   GS_HIP(hipMemcpyAsync(s->mass_host.data(), s->mass_dev, (size_t)s->L.n * sizeof(double),
                         hipMemcpyDeviceToHost, s->s_comp));
   GS_HIP(hipStreamSynchronize(s->s_comp));
+  resolve_force_mode(s);
   s->k = 0;
   s->full[0] = true;
   s->full[1] = false;
@@ -430,6 +535,38 @@ int gs_stepper_sync(gs_stepper* s) {
   return 0;
 }
 
+// Bounded wait for both streams, polling RCCL async errors. A hang (a dead peer, a stuck
+// collective) or an RCCL error aborts the communicator and returns -1 instead of blocking
+// forever (the reference's MPI_ERRORS_ARE_FATAL / silent CUDA errors: SURVEY.md §5).
+int gs_stepper_wait(gs_stepper* s, double timeout_s) {
+  const auto t0 = std::chrono::steady_clock::now();
+  for (;;) {
+    const hipError_t a = hipStreamQuery(s->s_comp);
+    const hipError_t b = hipStreamQuery(s->s_comm);
+    if (a == hipSuccess && b == hipSuccess) return 0;
+    if ((a != hipSuccess && a != hipErrorNotReady) || (b != hipSuccess && b != hipErrorNotReady)) {
+      char m[256];
+      snprintf(m, sizeof(m), "stream error: %s / %s", hipGetErrorString(a), hipGetErrorString(b));
+      gs_set_error(m);
+      return -1;
+    }
+    if (s->have_comm && gs_stepper_comm_check(s)) return -1;
+    const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (timeout_s > 0 && el > timeout_s) {
+      char m[256];
+      snprintf(m, sizeof(m), "step timeout after %.1f s (rank %d); communicator aborted", el,
+               s->cfg.rank);
+      if (s->have_comm) {
+        (void)ncclCommAbort(s->comm);
+        s->have_comm = false;
+      }
+      gs_set_error(m);
+      return -1;
+    }
+    std::this_thread::sleep_for(std::chrono::microseconds(200));
+  }
+}
+
 int gs_stepper_accel(gs_stepper* s, double* acc4) {
   GS_HIP(hipSetDevice(s->cfg.device));
   return s->esz == 4 ? accel_impl<float>(s, acc4) : accel_impl<double>(s, acc4);
@@ -475,6 +612,12 @@ int gs_stepper_phase_ms(gs_stepper* s, float* local_ms, float* comm_ms, float* t
 }
 
 void* gs_stepper_compute_stream(gs_stepper* s) { return (void*)s->s_comp; }
+
+int gs_stepper_force_mode(gs_stepper* s, int32_t* exact, double* eps2) {
+  if (exact) *exact = s->exact ? 1 : 0;
+  if (eps2) *eps2 = s->eps2;
+  return 0;
+}
 
 // Virtual ranks: P shards (rank r of P) in one process on one device. The all-gather is
 // P*(P-1) device-to-device copies on shard 0's comm stream, fenced against every shard's

@@ -55,6 +55,7 @@ typedef struct gs_config {
   int32_t device;     // HIP device ordinal
   int32_t use_graph;  // capture the step loop into a hipGraph and replay it
   int32_t split_groups;  // SPLIT mode: chunk groups per i-block (0 = auto)
+  int32_t cutoff_mode;   // 0 auto, 1 exact hard cutoff (select), 2 fast (overflow-safe core)
   double dt;          // time step [s]
   double G;           // gravitational constant
   double cutoff;      // hard cutoff radius [m]: zero force below it (mpi.c:64)
@@ -115,6 +116,8 @@ int gs_stepper_get_state(gs_stepper* s, double* pos, double* vel, double* mass);
 // Enqueue n steps (asynchronous w.r.t. the host).
 int gs_stepper_step(gs_stepper* s, int32_t nsteps);
 int gs_stepper_sync(gs_stepper* s);
+// Bounded wait (timeout_s <= 0: unbounded) polling RCCL async errors; aborts on timeout.
+int gs_stepper_wait(gs_stepper* s, double timeout_s);
 // Accelerations (+potential) of this rank's bodies for the current positions: acc4 = n_local*4.
 int gs_stepper_accel(gs_stepper* s, double* acc4);
 // Non-finite guard: returns number of non-finite position/velocity components on this rank.
@@ -122,6 +125,8 @@ int64_t gs_stepper_count_nonfinite(gs_stepper* s);
 int64_t gs_stepper_steps_done(gs_stepper* s);
 // Per-step phase timing of the last step (ms): local tile, gather wait, remote+integrate.
 int gs_stepper_phase_ms(gs_stepper* s, float* local_ms, float* comm_ms, float* total_ms);
+// Resolved force path: *exact = 1 for the hard-cutoff select, *eps2 = r^2 offset in use.
+int gs_stepper_force_mode(gs_stepper* s, int32_t* exact, double* eps2);
 void* gs_stepper_compute_stream(gs_stepper* s);
 
 // Virtual ranks on one device: shards[r] created with rank r of P; steps all of them in

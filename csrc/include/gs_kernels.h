@@ -22,14 +22,18 @@ struct KArgs {
   int32_t n_chunks;  // chunks holding real bodies
   int32_t c_begin, c_end;      // split kernel: chunk range
   int32_t pre_begin, pre_end;  // fused kernel: chunk range read from partial
-  int32_t phi;       // accumulate the potential sum too
-  T dt, cut2, eps2;
+  int32_t phi;       // accumulate the potential sum too (implies the exact cutoff)
+  int32_t exact;     // hard cutoff select (else the fast core-softened path)
+  T dt, cut2, eps2;  // eps2: softening^2, or the fast path's core^2 when larger
 };
 
 template <typename T>
 hipError_t launch_force_split(const KArgs<T>& a, int kernel, int ipl, int groups, hipStream_t s);
 template <typename T>
 hipError_t launch_force_fused(const KArgs<T>& a, int kernel, int ipl, hipStream_t s);
+// Resident workgroups per CU of the split kernel (fm: 0 fast, 1 exact, 2 exact+phi).
+template <typename T>
+int split_occupancy(int kernel, int ipl, int fm);
 template <typename T>
 hipError_t launch_reduce_integrate(const KArgs<T>& a, hipStream_t s);
 template <typename T>

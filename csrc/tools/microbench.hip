@@ -92,6 +92,64 @@ __global__ __launch_bounds__(256) void mfma_kernel(float* out, int iters, float 
   out[blockIdx.x * 256 + threadIdx.x] = s;
 }
 
+// 16 independent chains, x4 unrolled: VALU peak without dependency or loop-overhead limits.
+template <bool PK>
+__global__ __launch_bounds__(256) void valu16_kernel(float* out, int iters, float a, float b) {
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  f2 x[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) x[u] = f2{1.0f + 0.001f * threadIdx.x, 1.0f + u};
+  const f2 aa = {a, a}, bb = {b, b};
+  for (int it = 0; it < iters; ++it) {
+#pragma unroll
+    for (int rep = 0; rep < 4; ++rep)
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        if constexpr (PK) {
+          x[u] = __builtin_elementwise_fma(x[u], aa, bb);
+        } else {
+          x[u].x = __builtin_fmaf(x[u].x, a, b);
+          x[u].y = __builtin_fmaf(x[u].y, a, b);
+        }
+      }
+  }
+  float s = 0;
+#pragma unroll
+  for (int u = 0; u < 8; ++u) s += x[u].x + x[u].y;
+  out[blockIdx.x * 256 + threadIdx.x] = s;
+}
+
+// Role split: waves 0,2 of each workgroup run an MFMA loop, waves 1,3 run a VALU loop.
+// MODE 0: both roles, 1: MFMA role only (VALU waves exit), 2: VALU role only.
+template <int MODE>
+__global__ __launch_bounds__(256) void split_kernel(float* out, int iters, float a, float b) {
+  const int w = threadIdx.x >> 6;
+  float s = 0;
+  if ((w & 1) == 0) {
+    if (MODE == 2) return;
+    f4 acc[4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
+    float av = 0.001f * threadIdx.x, bv = 0.002f * threadIdx.x;
+    for (int it = 0; it < iters; ++it)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc[q], 0, 0, 0);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) s += acc[q].x + acc[q].y + acc[q].z + acc[q].w;
+  } else {
+    if (MODE == 1) return;
+    float x[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) x[u] = 1.0f + u;
+    for (int it = 0; it < iters; ++it)
+#pragma unroll
+      for (int rep = 0; rep < 2; ++rep)
+#pragma unroll
+        for (int u = 0; u < 16; ++u) x[u] = __builtin_fmaf(x[u], a, b);
+#pragma unroll
+    for (int u = 0; u < 16; ++u) s += x[u];
+  }
+  out[blockIdx.x * 256 + threadIdx.x] = s;
+}
+
 __global__ void layout_kernel(float* out, int mode) {
   const int l = threadIdx.x;
   float a = 1.f, b = 1.f;
@@ -153,6 +211,21 @@ int main() {
     const double ns = x.ms * 1e6 / mi;
     printf("{\"test\": \"%s\", \"ms\": %.4f, \"ns_per_mfma_per_simd\": %.4f, "
            "\"cycles_at_2.4GHz\": %.3f}\n", x.name, x.ms, ns, ns * 2.4);
+  }
+  {
+    // 64 fma (or 32 pk_fma) per iteration per lane
+    const float t0 = time_kernel(valu16_kernel<false>, out, iters, blocks, 5);
+    const float t1 = time_kernel(valu16_kernel<true>, out, iters, blocks, 5);
+    const double wi0 = waves_per_simd * iters * 64, wi1 = waves_per_simd * iters * 32;
+    printf("{\"test\": \"v_fma_f32 16 chains\", \"ms\": %.4f, \"ns_per_wave_instr_per_simd\": %.4f, \"lane_flops_per_clk_per_simd_at_2.4\": %.2f}\n",
+           t0, t0 * 1e6 / wi0, 128.0 / (t0 * 1e6 / wi0 * 2.4));
+    printf("{\"test\": \"v_pk_fma_f32 16 chains\", \"ms\": %.4f, \"ns_per_wave_instr_per_simd\": %.4f, \"lane_flops_per_clk_per_simd_at_2.4\": %.2f}\n",
+           t1, t1 * 1e6 / wi1, 256.0 / (t1 * 1e6 / wi1 * 2.4));
+    const float s0 = time_kernel(split_kernel<0>, out, iters, blocks, 5);
+    const float s1 = time_kernel(split_kernel<1>, out, iters, blocks, 5);
+    const float s2 = time_kernel(split_kernel<2>, out, iters, blocks, 5);
+    printf("{\"test\": \"role split mfma-waves + valu-waves\", \"both_ms\": %.4f, \"mfma_only_ms\": %.4f, \"valu_only_ms\": %.4f, \"overlap\": %.3f}\n",
+           s0, s1, s2, (s1 + s2 - s0) / (s1 < s2 ? s1 : s2));
   }
   float h[256];
   for (int mode = 0; mode < 2; ++mode) {

@@ -29,9 +29,12 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--G", type=float, default=d.G)
     p.add_argument("--cutoff", type=float, default=d.cutoff)
     p.add_argument("--softening", type=float, default=d.softening)
+    p.add_argument("--cutoff-mode", choices=["auto", "exact", "fast"], default=d.cutoff_mode,
+                   help="GPU force path: exact hard-cutoff select, or fast (cutoff inside an "
+                        "overflow-safe core; bit-identical for separations above ~mm)")
     p.add_argument("--kernel", choices=["auto", "lds", "smem"], default=d.kernel)
     p.add_argument("--mode", choices=["auto", "fused", "split"], default=d.mode)
-    p.add_argument("--ipl", type=int, default=d.ipl, choices=[0, 1, 2, 4])
+    p.add_argument("--ipl", type=int, default=d.ipl, choices=[0, 1, 2, 4, 8])
     p.add_argument("--chunk", type=int, default=d.chunk)
     p.add_argument("--no-graph", dest="graph", action="store_false")
     p.add_argument("--threads", type=int, default=0)
@@ -64,7 +67,8 @@ def config_from_args(a: argparse.Namespace) -> SimConfig:
         if os.path.isdir(resume):
             resume = ckpt.latest(resume)
     return SimConfig(n=a.n, dt=a.dt, steps=a.steps, dtype=a.dtype, device=a.device, init=a.init,
-                     seed=a.seed, G=a.G, cutoff=a.cutoff, softening=a.softening, kernel=a.kernel,
+                     seed=a.seed, G=a.G, cutoff=a.cutoff, softening=a.softening,
+                     cutoff_mode=a.cutoff_mode, kernel=a.kernel,
                      mode=a.mode, ipl=a.ipl, chunk=a.chunk, graph=a.graph, threads=a.threads,
                      log_dir=a.log_dir, log_format=a.log_format, progress_every=a.progress_every,
                      print_positions=a.print_positions, dump_path=a.dump_path,

@@ -33,6 +33,7 @@ class SimConfig:
     G: float = G_SI
     cutoff: float = 1e-10         # hard cutoff radius (cuda.cu:39, mpi.c:64, pyspark.py:38)
     softening: float = 0.0        # Plummer softening length (0 = reference semantics)
+    cutoff_mode: str = "auto"     # GPU: exact (select) | fast (overflow-safe core) | auto
     kernel: str = "auto"          # GPU j-source variant: lds | smem
     mode: str = "auto"            # GPU schedule: fused | split
     ipl: int = 0                  # i-bodies per lane (0 = auto)
@@ -41,6 +42,7 @@ class SimConfig:
     graph: bool = True            # hipGraph replay of the step loop (single rank)
     comm: str = "auto"            # rccl (GPU) | gloo (CPU) | none
     threads: int = 0              # CPU engine OpenMP threads (0 = default)
+    step_timeout_s: float = 600.0 # multi-rank hang detection: abort RCCL after this wait
     # observability / IO
     log_dir: Optional[str] = None     # directory for the text log (None = no file)
     log_format: str = "mpi"           # mpi | spark | cuda | none
@@ -72,10 +74,12 @@ class SimConfig:
             raise ValueError(f"comm must be one of {COMMS}")
         if self.log_format not in LOG_FORMATS:
             raise ValueError(f"log_format must be one of {LOG_FORMATS}")
-        if self.ipl not in (0, 1, 2, 4):
-            raise ValueError("ipl must be 0, 1, 2 or 4")
+        if self.ipl not in (0, 1, 2, 4, 8) or (self.ipl == 8 and self.dtype != "fp32"):
+            raise ValueError("ipl must be 0, 1, 2, 4 (or 8 for fp32)")
         if self.chunk and self.chunk % 1024:
             raise ValueError("chunk must be a multiple of 1024")
+        if self.cutoff_mode not in ("auto", "exact", "fast"):
+            raise ValueError("cutoff_mode must be auto, exact or fast")
         if self.cutoff < 0 or self.softening < 0:
             raise ValueError("cutoff and softening must be >= 0")
         return self

@@ -15,7 +15,8 @@ from ctypes import POINTER, c_double, c_float, c_int32, c_int64, c_uint64, c_voi
 from pathlib import Path
 
 _HERE = Path(__file__).resolve().parent.parent
-NATIVE_DIR = _HERE / "_native"
+NATIVE_DIR = Path(os.environ["GRAVSIM_NATIVE_DIR"]) if os.environ.get("GRAVSIM_NATIVE_DIR") \
+    else _HERE / "_native"
 _REPO = _HERE.parent
 _lock = threading.Lock()
 _cpu = None
@@ -31,7 +32,7 @@ class GsConfig(ctypes.Structure):
         ("n", c_int64), ("dtype", c_int32), ("kernel", c_int32), ("mode", c_int32),
         ("ipl", c_int32), ("chunk", c_int32), ("rank", c_int32), ("nranks", c_int32),
         ("device", c_int32), ("use_graph", c_int32), ("split_groups", c_int32),
-        ("dt", c_double), ("G", c_double), ("cutoff", c_double), ("softening", c_double),
+        ("cutoff_mode", c_int32), ("dt", c_double), ("G", c_double), ("cutoff", c_double), ("softening", c_double),
     ]
 
 
@@ -49,6 +50,7 @@ class GsLayout(ctypes.Structure):
 GS_FP32, GS_FP64 = 0, 1
 KERNEL_IDS = {"auto": 0, "lds": 1, "smem": 2}
 MODE_IDS = {"auto": 0, "fused": 1, "split": 2}
+CUTOFF_IDS = {"auto": 0, "exact": 1, "fast": 2}
 KERNEL_NAMES = {v: k for k, v in KERNEL_IDS.items()}
 MODE_NAMES = {v: k for k, v in MODE_IDS.items()}
 
@@ -64,8 +66,9 @@ def _build(which: str) -> None:
     script = _REPO / "csrc" / "build.py"
     if not script.exists():
         raise NativeUnavailable(f"{which} library missing and no build script at {script}")
+    env = dict(os.environ, GRAVSIM_NATIVE_DIR=str(NATIVE_DIR))
     r = subprocess.run([sys.executable, str(script), "--only", which], capture_output=True,
-                       text=True)
+                       text=True, env=env)
     if r.returncode != 0:
         raise NativeUnavailable(f"building libgravsim_{which}.so failed:\n{r.stdout}\n{r.stderr}")
 
@@ -131,11 +134,13 @@ def hip_lib():
         _sig(lib, "gs_stepper_get_state", c_int32, [S, _PD, _PD, _PD])
         _sig(lib, "gs_stepper_step", c_int32, [S, c_int32])
         _sig(lib, "gs_stepper_sync", c_int32, [S])
+        _sig(lib, "gs_stepper_wait", c_int32, [S, c_double])
         _sig(lib, "gs_stepper_accel", c_int32, [S, _PD])
         _sig(lib, "gs_stepper_count_nonfinite", c_int64, [S])
         _sig(lib, "gs_stepper_steps_done", c_int64, [S])
         _sig(lib, "gs_stepper_phase_ms", c_int32, [S, _PF, _PF, _PF])
         _sig(lib, "gs_stepper_compute_stream", c_void_p, [S])
+        _sig(lib, "gs_stepper_force_mode", c_int32, [S, POINTER(c_int32), POINTER(c_double)])
         _sig(lib, "gs_group_step", c_int32, [POINTER(S), c_int32, c_int32])
         _sig(lib, "gs_rccl_unique_id", c_int32, [c_void_p])
         _sig(lib, "gs_stepper_comm_init", c_int32, [S, c_void_p, c_int32, c_int32])

@@ -16,12 +16,17 @@ from ..config import G_SI
 
 
 def accelerations(pos: np.ndarray, mass: np.ndarray, G: float = G_SI, cutoff: float = 1e-10,
-                  softening: float = 0.0, block: int = 256, with_potential: bool = False):
-    """Direct-sum accelerations (n, 3) in fp64; optionally the potential phi (n,) too."""
+                  softening: float = 0.0, block: int = 256, with_potential: bool = False,
+                  with_abs: bool = False):
+    """Direct-sum accelerations (n, 3) in fp64; optionally the potential phi (n,) too.
+
+    with_abs also returns sum_j |term_ij| per component (n, 3): the scale against which a
+    floating-point sum of the terms should be judged (error <= c * eps * sum |terms|)."""
     pos = np.asarray(pos, dtype=np.float64)
     mu = G * np.asarray(mass, dtype=np.float64)
     n = pos.shape[0]
     acc = np.zeros((n, 3))
+    absacc = np.zeros((n, 3))
     phi = np.zeros(n)
     cut2 = cutoff * cutoff
     eps2 = softening * softening
@@ -35,10 +40,15 @@ def accelerations(pos: np.ndarray, mass: np.ndarray, G: float = G_SI, cutoff: fl
         mi = mu[None, :] * inv
         s = mi * inv * inv
         acc[i0:i1] = (s[:, :, None] * d).sum(1)
+        if with_abs:
+            absacc[i0:i1] = (s[:, :, None] * np.abs(d)).sum(1)
         phi[i0:i1] = -mi.sum(1)
+    out = (acc,)
     if with_potential:
-        return acc, phi
-    return acc
+        out += (phi,)
+    if with_abs:
+        out += (absacc,)
+    return out if len(out) > 1 else acc
 
 
 def step(pos, vel, mass, dt, G=G_SI, cutoff=1e-10, softening=0.0):

@@ -30,8 +30,8 @@ def _gs_config(cfg: SimConfig, rank: int, nranks: int, device: int) -> _native.G
         n=cfg.n, dtype=_native.GS_FP64 if cfg.dtype == "fp64" else _native.GS_FP32,
         kernel=_native.KERNEL_IDS[cfg.kernel], mode=_native.MODE_IDS[cfg.mode], ipl=cfg.ipl,
         chunk=cfg.chunk, rank=rank, nranks=nranks, device=device, use_graph=int(cfg.graph),
-        split_groups=cfg.split_groups, dt=cfg.dt, G=cfg.G, cutoff=cfg.cutoff,
-        softening=cfg.softening)
+        split_groups=cfg.split_groups, cutoff_mode=_native.CUTOFF_IDS[cfg.cutoff_mode], dt=cfg.dt,
+        G=cfg.G, cutoff=cfg.cutoff, softening=cfg.softening)
 
 
 def gpu_available() -> bool:
@@ -103,8 +103,15 @@ class HipEngine:
         if n > 0:
             _native.check(self.lib, self.lib.gs_stepper_step(self._s, int(n)), "step")
 
-    def sync(self) -> None:
-        _native.check(self.lib, self.lib.gs_stepper_sync(self._s), "sync")
+    def sync(self, timeout_s: float = 0.0) -> None:
+        """Wait for the enqueued steps. With a timeout (or P > 1, default 600 s) the wait
+        polls RCCL async errors and aborts the communicator on a hang."""
+        if timeout_s <= 0 and self.nranks > 1:
+            timeout_s = float(self.cfg.step_timeout_s or 0)
+        if timeout_s > 0:
+            _native.check(self.lib, self.lib.gs_stepper_wait(self._s, timeout_s), "wait")
+        else:
+            _native.check(self.lib, self.lib.gs_stepper_sync(self._s), "sync")
 
     def state(self) -> BodySet:
         """Full positions (collective for P > 1), own velocity rows, masses."""
@@ -131,6 +138,12 @@ class HipEngine:
     @property
     def steps_done(self) -> int:
         return int(self.lib.gs_stepper_steps_done(self._s))
+
+    def force_mode(self) -> dict:
+        """Resolved force path: exact hard-cutoff select, or the fast core-softened path."""
+        ex, e2 = ctypes.c_int32(), ctypes.c_double()
+        self.lib.gs_stepper_force_mode(self._s, ctypes.byref(ex), ctypes.byref(e2))
+        return {"exact": bool(ex.value), "eps2": e2.value}
 
     def close(self) -> None:
         if self._s:
