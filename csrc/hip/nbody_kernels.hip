@@ -122,41 +122,57 @@ __device__ __forceinline__ void tile_fill(const V4<T>* __restrict__ src, V4<T>* 
                                    (__attribute__((address_space(3))) void*)l, 16, 0, 0);
 }
 
-// Sweep chunks [c0, c1) through LDS tiles. For every finished chunk call on_chunk(c).
+// A contiguous run of virtual chunk indices [v0, v1) over the chunk sequence
+// [c_begin, c_end) minus the skipped range [skip_begin, skip_end): chunk(v) maps back to the
+// canonical chunk index, so per-chunk partial sums are the same bits whichever launch
+// (rank-local overlap phase, remote phase, single-rank sweep) computes them.
+struct ChunkSeq {
+  int c_begin, skip_begin, skip_len;
+  __device__ __forceinline__ int chunk(int v) const {
+    const int c = c_begin + v;
+    return c < skip_begin ? c : c + skip_len;
+  }
+};
+
+// Sweep virtual chunks [v0, v1) through LDS tiles; on_chunk(c) after every finished chunk.
 template <typename T, int IPL, int FM, typename OnChunk>
-__device__ __forceinline__ void sweep_lds(const V4<T>* __restrict__ X, int64_t chunk, int c0,
-                                          int c1, T cut2, T eps2, IState<T, IPL>& st,
-                                          V4<T> (*tile)[Tile<T>::kBodies], OnChunk on_chunk) {
+__device__ __forceinline__ void sweep_lds(const V4<T>* __restrict__ X, int64_t chunk,
+                                          const ChunkSeq& seq, int v0, int v1, T cut2, T eps2,
+                                          IState<T, IPL>& st, V4<T> (*tile)[Tile<T>::kBodies],
+                                          OnChunk on_chunk) {
   constexpr int TB = Tile<T>::kBodies;
-  const int tiles_per_chunk = (int)(chunk / TB);
-  const int ntiles = (c1 - c0) * tiles_per_chunk;
+  const int tpc = (int)(chunk / TB);  // tiles per chunk
+  const int ntiles = (v1 - v0) * tpc;
   if (ntiles <= 0) return;
-  const V4<T>* base = X + (int64_t)c0 * chunk;
-  tile_fill<T>(base, tile[0]);
+  auto tile_src = [&](int t) {
+    return X + (int64_t)seq.chunk(v0 + t / tpc) * chunk + (int64_t)(t % tpc) * TB;
+  };
+  tile_fill<T>(tile_src(0), tile[0]);
   zero_chunk<T, IPL>(st);
   for (int t = 0; t < ntiles; ++t) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();  // tile t is in LDS for every wave; buffer (t+1)&1 is free
-    if (t + 1 < ntiles) tile_fill<T>(base + (int64_t)(t + 1) * TB, tile[(t + 1) & 1]);
+    if (t + 1 < ntiles) tile_fill<T>(tile_src(t + 1), tile[(t + 1) & 1]);
     const V4<T>* cur = tile[t & 1];
 #pragma unroll 8
     for (int j = 0; j < TB; ++j) {
       const V4<T> q = cur[j];  // uniform address: one broadcast ds_read per wave
       interact_all<T, IPL, FM>(st, q, cut2, eps2);
     }
-    if ((t + 1) % tiles_per_chunk == 0) {
-      on_chunk(c0 + t / tiles_per_chunk);
+    if ((t + 1) % tpc == 0) {
+      on_chunk(seq.chunk(v0 + t / tpc));
       zero_chunk<T, IPL>(st);
     }
   }
 }
 
-// Sweep chunks [c0, c1) with wave-uniform j loaded into SGPRs via the scalar cache.
+// Sweep virtual chunks [v0, v1) with wave-uniform j loaded into SGPRs via the scalar cache.
 template <typename T, int IPL, int FM, typename OnChunk>
-__device__ __forceinline__ void sweep_smem(const V4<T>* __restrict__ X, int64_t chunk, int c0,
-                                           int c1, T cut2, T eps2, IState<T, IPL>& st,
-                                           OnChunk on_chunk) {
-  for (int c = c0; c < c1; ++c) {
+__device__ __forceinline__ void sweep_smem(const V4<T>* __restrict__ X, int64_t chunk,
+                                           const ChunkSeq& seq, int v0, int v1, T cut2, T eps2,
+                                           IState<T, IPL>& st, OnChunk on_chunk) {
+  for (int v = v0; v < v1; ++v) {
+    const int c = seq.chunk(v);
     zero_chunk<T, IPL>(st);
     const V4<T>* p = X + (int64_t)c * chunk;
     for (int64_t j = 0; j < chunk; j += 4) {
@@ -214,10 +230,13 @@ template <typename T, int IPL, int KV, int FM>
 __global__ __launch_bounds__(kBlock) void force_split_kernel(KArgs<T> a) {
   __shared__ __attribute__((aligned(16))) V4<T> tile[2][Tile<T>::kBodies];
   const int64_t ib = (int64_t)blockIdx.x * (kBlock * IPL);
-  const int span = a.c_end - a.c_begin;
+  const int sb = min(max(a.skip_begin, a.c_begin), a.c_end);
+  const int se = min(max(a.skip_end, sb), a.c_end);
+  const ChunkSeq seq{a.c_begin, sb, se - sb};
+  const int span = (a.c_end - a.c_begin) - (se - sb);
   const int per = (span + (int)gridDim.y - 1) / (int)gridDim.y;
-  const int c0 = a.c_begin + (int)blockIdx.y * per;
-  const int c1 = min(c0 + per, a.c_end);
+  const int v0 = (int)blockIdx.y * per;
+  const int v1 = min(v0 + per, span);
   IState<T, IPL> st;
   load_i<T, IPL>(a, st, ib);
   V4<T>* part = reinterpret_cast<V4<T>*>(a.partial);
@@ -231,9 +250,9 @@ __global__ __launch_bounds__(kBlock) void force_split_kernel(KArgs<T> a) {
   };
   const V4<T>* X = reinterpret_cast<const V4<T>*>(a.X);
   if constexpr (KV == GS_KERNEL_LDS)
-    sweep_lds<T, IPL, FM>(X, a.chunk, c0, c1, a.cut2, a.eps2, st, tile, store);
+    sweep_lds<T, IPL, FM>(X, a.chunk, seq, v0, v1, a.cut2, a.eps2, st, tile, store);
   else
-    sweep_smem<T, IPL, FM>(X, a.chunk, c0, c1, a.cut2, a.eps2, st, store);
+    sweep_smem<T, IPL, FM>(X, a.chunk, seq, v0, v1, a.cut2, a.eps2, st, store);
 }
 
 // FUSED: grid (i_blocks). Sweep every chunk in canonical order; chunks in [pre_begin,
@@ -264,15 +283,16 @@ __global__ __launch_bounds__(kBlock) void force_fused_kernel(KArgs<T> a) {
   // [pre_end, n_chunks) computed.
   const int pb = min(max(a.pre_begin, 0), a.n_chunks);
   const int pe = min(max(a.pre_end, pb), a.n_chunks);
+  const ChunkSeq seq{0, a.n_chunks, 0};
   if constexpr (KV == GS_KERNEL_LDS) {
-    sweep_lds<T, IPL, FM>(X, a.chunk, 0, pb, a.cut2, a.eps2, st, tile, fold);
+    sweep_lds<T, IPL, FM>(X, a.chunk, seq, 0, pb, a.cut2, a.eps2, st, tile, fold);
     for (int c = pb; c < pe; ++c) fold_pre(c);
     __syncthreads();  // both LDS buffers are refilled by the next sweep
-    sweep_lds<T, IPL, FM>(X, a.chunk, pe, a.n_chunks, a.cut2, a.eps2, st, tile, fold);
+    sweep_lds<T, IPL, FM>(X, a.chunk, seq, pe, a.n_chunks, a.cut2, a.eps2, st, tile, fold);
   } else {
-    sweep_smem<T, IPL, FM>(X, a.chunk, 0, pb, a.cut2, a.eps2, st, fold);
+    sweep_smem<T, IPL, FM>(X, a.chunk, seq, 0, pb, a.cut2, a.eps2, st, fold);
     for (int c = pb; c < pe; ++c) fold_pre(c);
-    sweep_smem<T, IPL, FM>(X, a.chunk, pe, a.n_chunks, a.cut2, a.eps2, st, fold);
+    sweep_smem<T, IPL, FM>(X, a.chunk, seq, pe, a.n_chunks, a.cut2, a.eps2, st, fold);
   }
   if (a.acc_out) {
     V4<T>* out = reinterpret_cast<V4<T>*>(a.acc_out);
@@ -423,9 +443,10 @@ static hipError_t dispatch(const KArgs<T>& a, int kernel, int ipl, bool fused, i
 
 template <typename T>
 hipError_t launch_force_split(const KArgs<T>& a, int kernel, int ipl, int groups, hipStream_t s) {
-  if (a.c_end <= a.c_begin) return hipSuccess;
+  const int span = split_span(a);
+  if (span <= 0) return hipSuccess;
   if (groups < 1) groups = 1;
-  if (groups > a.c_end - a.c_begin) groups = a.c_end - a.c_begin;
+  if (groups > span) groups = span;
   return dispatch<T>(a, kernel, ipl, false, groups, s);
 }
 

@@ -237,16 +237,13 @@ int enqueue_step(gs_stepper* s, bool capturing, bool gathered_externally) {
       a.pre_end = s->own_c1;
       GS_HIP(gs::launch_force_fused<T>(a, kernel, ipl, s->s_comp));
     } else {
+      // One launch for every remote chunk: [0, n_chunks) minus the own range.
       gs::KArgs<T> r = a;
-      r.c_begin = 0;
-      r.c_end = s->own_c0;
-      GS_HIP(gs::launch_force_split<T>(r, kernel, ipl, choose_groups(s, s->own_c0, false),
-                                       s->s_comp));
-      r.c_begin = s->own_c1;
-      r.c_end = s->L.n_chunks;
-      GS_HIP(gs::launch_force_split<T>(r, kernel, ipl,
-                                       choose_groups(s, s->L.n_chunks - s->own_c1, false),
-                                       s->s_comp));
+      r.skip_begin = s->own_c0;
+      r.skip_end = s->own_c1;
+      GS_HIP(gs::launch_force_split<T>(
+          r, kernel, ipl, choose_groups(s, s->L.n_chunks - (s->own_c1 - s->own_c0), false),
+          s->s_comp));
       GS_HIP(gs::launch_reduce_integrate<T>(a, s->s_comp));
     }
   } else {

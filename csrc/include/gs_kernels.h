@@ -20,12 +20,21 @@ struct KArgs {
   int64_t n_real;    // real global body count
   int64_t chunk;     // canonical j-chunk length
   int32_t n_chunks;  // chunks holding real bodies
-  int32_t c_begin, c_end;      // split kernel: chunk range
+  int32_t c_begin, c_end;      // split kernel: chunk range ...
+  int32_t skip_begin, skip_end;  // ... minus this sub-range (the rank's own chunks)
   int32_t pre_begin, pre_end;  // fused kernel: chunk range read from partial
   int32_t phi;       // accumulate the potential sum too (implies the exact cutoff)
   int32_t exact;     // hard cutoff select (else the fast core-softened path)
   T dt, cut2, eps2;  // eps2: softening^2, or the fast path's core^2 when larger
 };
+
+// Chunks a split launch covers: [c_begin, c_end) minus [skip_begin, skip_end).
+template <typename T>
+inline int split_span(const KArgs<T>& a) {
+  const int sb = a.skip_begin < a.c_begin ? a.c_begin : (a.skip_begin > a.c_end ? a.c_end : a.skip_begin);
+  const int se = a.skip_end < sb ? sb : (a.skip_end > a.c_end ? a.c_end : a.skip_end);
+  return (a.c_end - a.c_begin) - (se - sb);
+}
 
 template <typename T>
 hipError_t launch_force_split(const KArgs<T>& a, int kernel, int ipl, int groups, hipStream_t s);

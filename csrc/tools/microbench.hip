@@ -9,6 +9,8 @@
 #include <stdio.h>
 #include <stdlib.h>
 
+#include <vector>
+
 #define CK(x)                                                                            \
   do {                                                                                   \
     hipError_t e = (x);                                                                  \
@@ -150,6 +152,49 @@ __global__ __launch_bounds__(256) void split_kernel(float* out, int iters, float
   out[blockIdx.x * 256 + threadIdx.x] = s;
 }
 
+// Accuracy of the raw v_rsq_f64 / v_rsq_f32 seeds vs a correctly rounded 1/sqrt (relative).
+__global__ void rsq_accuracy_kernel(double* out, int n) {
+  double worst64 = 0, worst32 = 0;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    // log-uniform inputs over [1e-20, 1e30]
+    const double u = (double)((i * 2654435761u) & 0xFFFFFF) / 16777216.0;
+    const double x = pow(10.0, -20.0 + 50.0 * u) * (1.0 + 1e-3 * (i & 1023));
+    const double ref = 1.0 / sqrt(x);
+    const double y64 = __builtin_amdgcn_rsq(x);
+    worst64 = fmax(worst64, fabs(y64 - ref) / ref);
+    const float xf = (float)x;
+    const double reff = 1.0 / sqrt((double)xf);
+    worst32 = fmax(worst32, fabs((double)__builtin_amdgcn_rsqf(xf) - reff) / reff);
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    worst64 = fmax(worst64, __shfl_down(worst64, off, 64));
+    worst32 = fmax(worst32, __shfl_down(worst32, off, 64));
+  }
+  if ((threadIdx.x & 63) == 0) {
+    out[2 * (blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64)] = worst64;
+    out[2 * (blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64) + 1] = worst32;
+  }
+}
+
+template <int OPS>
+__global__ __launch_bounds__(256) void f64_kernel(float* out, int iters, float a, float b) {
+  double x[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) x[u] = 1.0 + 0.001 * (threadIdx.x + u);
+  const double da = a, db = b;
+  for (int it = 0; it < iters; ++it) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      if constexpr (OPS == 0) x[u] = __builtin_fma(x[u], da, db);
+      else x[u] = __builtin_amdgcn_rsq(x[u]);
+    }
+  }
+  double s = 0;
+#pragma unroll
+  for (int u = 0; u < 8; ++u) s += x[u];
+  out[blockIdx.x * 256 + threadIdx.x] = (float)s;
+}
+
 __global__ void layout_kernel(float* out, int mode) {
   const int l = threadIdx.x;
   float a = 1.f, b = 1.f;
@@ -226,6 +271,23 @@ int main() {
     const float s2 = time_kernel(split_kernel<2>, out, iters, blocks, 5);
     printf("{\"test\": \"role split mfma-waves + valu-waves\", \"both_ms\": %.4f, \"mfma_only_ms\": %.4f, \"valu_only_ms\": %.4f, \"overlap\": %.3f}\n",
            s0, s1, s2, (s1 + s2 - s0) / (s1 < s2 ? s1 : s2));
+  }
+  {
+    const float f0 = time_kernel(f64_kernel<0>, out, iters, blocks, 5);
+    const float f1 = time_kernel(f64_kernel<1>, out, iters, blocks, 5);
+    const double wi = waves_per_simd * iters * 8;
+    printf("{\"test\": \"v_fma_f64 x8\", \"ns_per_wave_instr_per_simd\": %.4f}\n", f0 * 1e6 / wi);
+    printf("{\"test\": \"v_rsq_f64 x8\", \"ns_per_wave_instr_per_simd\": %.4f}\n", f1 * 1e6 / wi);
+    double* acc;
+    const int nb = 1024;
+    CK(hipMalloc(&acc, (size_t)nb * 4 * 2 * sizeof(double)));
+    hipLaunchKernelGGL(rsq_accuracy_kernel, dim3(nb), dim3(256), 0, 0, acc, 1 << 24);
+    std::vector<double> h(nb * 4 * 2);
+    CK(hipMemcpy(h.data(), acc, h.size() * sizeof(double), hipMemcpyDeviceToHost));
+    double w64 = 0, w32 = 0;
+    for (int i = 0; i < nb * 4; ++i) { w64 = fmax(w64, h[2 * i]); w32 = fmax(w32, h[2 * i + 1]); }
+    printf("{\"test\": \"rsq seed accuracy\", \"v_rsq_f64_max_rel_err\": %.3e, \"v_rsq_f32_max_rel_err\": %.3e}\n", w64, w32);
+    CK(hipFree(acc));
   }
   float h[256];
   for (int mode = 0; mode < 2; ++mode) {
