@@ -71,6 +71,7 @@ def build_cpu(force: bool = False) -> Path:
 HIP_FLAGS = ["-O3", "-std=c++17", f"--offload-arch={ARCH}", "-ffp-contract=off", "-fPIC"]
 if os.environ.get("GRAVSIM_SLP", "1") == "0":
     HIP_FLAGS.append("-fno-slp-vectorize")
+HIP_FLAGS += os.environ.get("GRAVSIM_HIP_EXTRA", "").split()
 
 
 def build_hip(force: bool = False) -> Path:

@@ -42,10 +42,19 @@ __device__ __forceinline__ float rsqrt_dev(float x) { return __builtin_amdgcn_rs
 // (5.2e-8)^3 is far below 2^-53, so one step reaches double precision in 5 f64 ops where two
 // Newton steps need 7.
 __device__ __forceinline__ double rsqrt_dev(double x) {
+#ifdef GS_FP64_NEWTON  // A/B reference: two Newton-Raphson steps
+  double y = __builtin_amdgcn_rsq(x);
+  const double hx = 0.5 * x;
+  double e = __builtin_fma(-hx * y, y, 0.5);
+  y = __builtin_fma(y, e, y);
+  e = __builtin_fma(-hx * y, y, 0.5);
+  return __builtin_fma(y, e, y);
+#else
   const double y = __builtin_amdgcn_rsq(x);
   const double e = __builtin_fma(-x * y, y, 1.0);
   const double p = __builtin_fma(e, 0.375, 0.5);
   return __builtin_fma(y * e, p, y);
+#endif
 }
 
 __device__ __forceinline__ float fma_(float a, float b, float c) { return __builtin_fmaf(a, b, c); }

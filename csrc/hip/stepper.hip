@@ -65,7 +65,8 @@ struct gs_stepper {
   gs_layout L;
   size_t esz = 4;  // element size
   hipStream_t s_comp = nullptr, s_comm = nullptr;
-  hipEvent_t ev_ready = nullptr, ev_gathered = nullptr;
+  hipStream_t s_rem = nullptr;  // second compute stream: remote chunks beside the local ones
+  hipEvent_t ev_ready = nullptr, ev_gathered = nullptr, ev_remote = nullptr, ev_fork = nullptr;
   hipEvent_t ev_t0 = nullptr, ev_local = nullptr, ev_end = nullptr;
   void* X[2] = {nullptr, nullptr};
   void* vel = nullptr;
@@ -225,27 +226,28 @@ int enqueue_step(gs_stepper* s, bool capturing, bool gathered_externally) {
     if (gathered_externally) s->full[cur] = true;
     else if (gather(s, cur)) return -1;
     // Rank-local chunks overlap the all-gather: they read only the own slice of X[cur].
+    // The remote chunks run on a second compute stream gated only by the gather, so the two
+    // launches share the GPU instead of serialising (the local launch alone holds only
+    // n_local/(256*ipl) x own-chunk workgroups). The reduce/integrate waits for both.
+    GS_HIP(hipEventRecord(s->ev_fork, s->s_comp));
+    GS_HIP(hipStreamWaitEvent(s->s_rem, s->ev_fork, 0));
     gs::KArgs<T> loc = a;
     loc.c_begin = s->own_c0;
     loc.c_end = s->own_c1;
     GS_HIP(gs::launch_force_split<T>(loc, kernel, ipl, choose_groups(s, s->own_c1 - s->own_c0, false),
                                      s->s_comp));
     if (timed) GS_HIP(hipEventRecord(s->ev_local, s->s_comp));
-    GS_HIP(hipStreamWaitEvent(s->s_comp, s->ev_gathered, 0));
-    if (fused) {
-      a.pre_begin = s->own_c0;
-      a.pre_end = s->own_c1;
-      GS_HIP(gs::launch_force_fused<T>(a, kernel, ipl, s->s_comp));
-    } else {
-      // One launch for every remote chunk: [0, n_chunks) minus the own range.
-      gs::KArgs<T> r = a;
-      r.skip_begin = s->own_c0;
-      r.skip_end = s->own_c1;
-      GS_HIP(gs::launch_force_split<T>(
-          r, kernel, ipl, choose_groups(s, s->L.n_chunks - (s->own_c1 - s->own_c0), false),
-          s->s_comp));
-      GS_HIP(gs::launch_reduce_integrate<T>(a, s->s_comp));
-    }
+    GS_HIP(hipStreamWaitEvent(s->s_rem, s->ev_gathered, 0));
+    // One launch for every remote chunk: [0, n_chunks) minus the own range.
+    gs::KArgs<T> r = a;
+    r.skip_begin = s->own_c0;
+    r.skip_end = s->own_c1;
+    GS_HIP(gs::launch_force_split<T>(
+        r, kernel, ipl, choose_groups(s, s->L.n_chunks - (s->own_c1 - s->own_c0), false),
+        s->s_rem));
+    GS_HIP(hipEventRecord(s->ev_remote, s->s_rem));
+    GS_HIP(hipStreamWaitEvent(s->s_comp, s->ev_remote, 0));
+    GS_HIP(gs::launch_reduce_integrate<T>(a, s->s_comp));
   } else {
     if (timed) GS_HIP(hipEventRecord(s->ev_local, s->s_comp));
     if (fused) {
@@ -417,6 +419,9 @@ int gs_stepper_create(const gs_config* cfg, gs_stepper** out) {
   FAIL_CLEAN(hipDeviceGetStreamPriorityRange(&lo, &hi));
   FAIL_CLEAN(hipStreamCreateWithFlags(&s->s_comp, hipStreamNonBlocking));
   FAIL_CLEAN(hipStreamCreateWithPriority(&s->s_comm, hipStreamNonBlocking, hi));
+  FAIL_CLEAN(hipStreamCreateWithFlags(&s->s_rem, hipStreamNonBlocking));
+  FAIL_CLEAN(hipEventCreateWithFlags(&s->ev_remote, hipEventDisableTiming));
+  FAIL_CLEAN(hipEventCreateWithFlags(&s->ev_fork, hipEventDisableTiming));
   FAIL_CLEAN(hipEventCreateWithFlags(&s->ev_ready, hipEventDisableTiming));
   FAIL_CLEAN(hipEventCreateWithFlags(&s->ev_gathered, hipEventDisableTiming));
   FAIL_CLEAN(hipEventCreate(&s->ev_t0));
@@ -442,15 +447,18 @@ int gs_stepper_destroy(gs_stepper* s) {
   if (!s) return 0;
   if (s->s_comp) (void)hipStreamSynchronize(s->s_comp);
   if (s->s_comm) (void)hipStreamSynchronize(s->s_comm);
+  if (s->s_rem) (void)hipStreamSynchronize(s->s_rem);
   if (s->graph) (void)hipGraphExecDestroy(s->graph);
   if (s->have_comm) (void)ncclCommDestroy(s->comm);
   for (void* p : {s->X[0], s->X[1], s->vel, s->partial, s->acc, (void*)s->mass_dev,
                   (void*)s->nonfinite})
     if (p) (void)hipFree(p);
-  for (hipEvent_t e : {s->ev_ready, s->ev_gathered, s->ev_t0, s->ev_local, s->ev_end})
+  for (hipEvent_t e : {s->ev_ready, s->ev_gathered, s->ev_t0, s->ev_local, s->ev_end,
+                       s->ev_remote, s->ev_fork})
     if (e) (void)hipEventDestroy(e);
   if (s->s_comp) (void)hipStreamDestroy(s->s_comp);
   if (s->s_comm) (void)hipStreamDestroy(s->s_comm);
+  if (s->s_rem) (void)hipStreamDestroy(s->s_rem);
   delete s;
   return 0;
 }
@@ -528,6 +536,7 @@ int gs_stepper_step(gs_stepper* s, int32_t nsteps) {
 
 int gs_stepper_sync(gs_stepper* s) {
   GS_HIP(hipStreamSynchronize(s->s_comm));
+  GS_HIP(hipStreamSynchronize(s->s_rem));
   GS_HIP(hipStreamSynchronize(s->s_comp));
   return 0;
 }
@@ -538,7 +547,8 @@ int gs_stepper_sync(gs_stepper* s) {
 int gs_stepper_wait(gs_stepper* s, double timeout_s) {
   const auto t0 = std::chrono::steady_clock::now();
   for (;;) {
-    const hipError_t a = hipStreamQuery(s->s_comp);
+    hipError_t a = hipStreamQuery(s->s_comp);
+    if (a == hipSuccess) a = hipStreamQuery(s->s_rem);
     const hipError_t b = hipStreamQuery(s->s_comm);
     if (a == hipSuccess && b == hipSuccess) return 0;
     if ((a != hipSuccess && a != hipErrorNotReady) || (b != hipSuccess && b != hipErrorNotReady)) {
