@@ -116,19 +116,28 @@ __device__ __forceinline__ void interact_all(IState<T, IPL>& s, const V4<T>& q, 
                      s.az[k], s.ph[k]);
 }
 
-// LDS tile geometry: 4 KiB per tile buffer (256 fp32 bodies / 128 fp64 bodies).
-template <typename T> struct Tile { static constexpr int kBodies = 4096 / sizeof(V4<T>); };
+// LDS tile geometry: kTileBytes per tile buffer (default 4 KiB = 256 fp32 / 128 fp64 bodies),
+// double-buffered. Each wave-instruction of the fill moves one 1-KiB piece.
+#ifndef GS_TILE_BYTES
+#define GS_TILE_BYTES 4096
+#endif
+constexpr int kTileBytes = GS_TILE_BYTES;
+static_assert(kTileBytes % 4096 == 0, "tile must be whole 4-wave x 1 KiB rounds");
+template <typename T> struct Tile { static constexpr int kBodies = kTileBytes / sizeof(V4<T>); };
 
-// Issue the LDS-DMA fill of one 4-KiB tile: each of the 4 waves moves one 1-KiB piece
+// Issue the LDS-DMA fill of one tile: per round each of the 4 waves moves one 1-KiB piece
 // (64 lanes x 16 B); the LDS destination is the wave-uniform base + lane*16.
 template <typename T>
 __device__ __forceinline__ void tile_fill(const V4<T>* __restrict__ src, V4<T>* dst) {
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
-  const char* g = reinterpret_cast<const char*>(src) + wave * 1024 + lane * 16;
-  char* l = reinterpret_cast<char*>(dst) + wave * 1024;
-  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
-                                   (__attribute__((address_space(3))) void*)l, 16, 0, 0);
+#pragma unroll
+  for (int r = 0; r < kTileBytes / 4096; ++r) {
+    const char* g = reinterpret_cast<const char*>(src) + r * 4096 + wave * 1024 + lane * 16;
+    char* l = reinterpret_cast<char*>(dst) + r * 4096 + wave * 1024;
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                     (__attribute__((address_space(3))) void*)l, 16, 0, 0);
+  }
 }
 
 // A contiguous run of virtual chunk indices [v0, v1) over the chunk sequence

@@ -80,6 +80,7 @@ struct gs_stepper {
   ncclComm_t comm = nullptr;
   bool have_comm = false;
   bool virt = false;  // member of a virtual-rank group (gather = device copies, gs_group_step)
+  bool emulate = false;  // GRAVSIM_EMULATE_RANK: run one rank's launch shapes, no exchange
   hipGraphExec_t graph = nullptr;
   bool timed = false;  // eager steps record phase events
   int own_c0 = 0, own_c1 = 0;  // this rank's chunks clipped to [0, n_chunks)
@@ -395,6 +396,7 @@ int gs_stepper_create(const gs_config* cfg, gs_stepper** out) {
   if (gs_layout_compute(cfg, &s->L)) { delete s; return -1; }
   s->esz = cfg->dtype == GS_FP64 ? 8 : 4;
   s->timed = getenv("GRAVSIM_PHASE_TIMING") != nullptr;
+  s->emulate = getenv("GRAVSIM_EMULATE_RANK") != nullptr && cfg->nranks > 1;
   const int64_t own_first = s->L.local_begin / s->L.chunk;
   const int64_t own_last = (s->L.local_begin + s->L.n_local) / s->L.chunk;
   s->own_c0 = (int)(own_first < s->L.n_chunks ? own_first : s->L.n_chunks);
@@ -508,9 +510,17 @@ int gs_stepper_get_state(gs_stepper* s, double* pos, double* vel, double* mass) 
 
 int gs_stepper_step(gs_stepper* s, int32_t nsteps) {
   GS_HIP(hipSetDevice(s->cfg.device));
-  if (s->cfg.nranks > 1 && !s->have_comm) {
+  if (s->cfg.nranks > 1 && !s->have_comm && !s->emulate) {
     gs_set_error("step: nranks > 1 but no RCCL communicator (call gs_stepper_comm_init)");
     return -1;
+  }
+  if (s->emulate) {
+    // Timing emulation of one rank of a P-rank run: the multi-rank launches with the
+    // all-gather treated as done (remote slices hold stale data; numbers are not physics).
+    s->virt = true;
+    for (int32_t i = 0; i < nsteps; ++i)
+      if (enqueue_step_any(s, false, true)) return -1;
+    return 0;
   }
   // hipGraph replay only for the single-rank schedule (nothing to gather); RCCL capture is
   // opt-in through use_graph >= 2.
