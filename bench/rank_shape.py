@@ -25,8 +25,8 @@ def main() -> int:
     ap.add_argument("--ranks", default="1,2,4,8")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--dtype", default="fp32")
-    ap.add_argument("--ipl", type=int, default=0)
-    ap.add_argument("--kernel", default="auto")
+    ap.add_argument("--ipl", default="0", help="comma list")
+    ap.add_argument("--kernel", default="auto", help="comma list")
     a = ap.parse_args()
     import torch  # noqa: F401
 
@@ -35,8 +35,12 @@ def main() -> int:
     from gravsim.runtime.engines import HipEngine
 
     base = None
-    for P in [int(x) for x in a.ranks.split(",")]:
-        cfg = SimConfig(n=a.n, dtype=a.dtype, device="gpu", ipl=a.ipl, kernel=a.kernel)
+    import itertools
+
+    grid = list(itertools.product([int(x) for x in a.ranks.split(",")],
+                                  [int(x) for x in a.ipl.split(",")], a.kernel.split(",")))
+    for P, ipl, kernel in grid:
+        cfg = SimConfig(n=a.n, dtype=a.dtype, device="gpu", ipl=ipl, kernel=kernel)
         r = P - 1 if P > 1 else 0  # a rank with its own chunks at the end
         e = HipEngine(cfg, r, P)
         e.init_ics("solar+random", cfg.seed)
@@ -47,7 +51,8 @@ def main() -> int:
         e.sync()
         ms = 1e3 * (time.perf_counter() - t0) / a.steps
         base = base or ms * P
-        print(json.dumps(dict(P=P, rank=r, n=a.n, dtype=a.dtype, ms_per_step=ms,
+        print(json.dumps(dict(P=P, rank=r, n=a.n, dtype=a.dtype, ipl=ipl, kernel=kernel,
+                              ms_per_step=ms,
                               predicted_efficiency=base / (P * ms),
                               predicted_body_updates_per_s=a.n / (ms * 1e-3),
                               layout=e.native_layout)), flush=True)

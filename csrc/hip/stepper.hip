@@ -175,9 +175,13 @@ void resolve_force_mode(gs_stepper* s) {
 
 // Chunk groups for one split launch of `span` chunks over the i-blocks: minimise
 // rounds(g) * chunks_per_group(g) with rounds = ceil(i_blocks * g / resident).
-int choose_groups(gs_stepper* s, int span, bool phi) {
+int choose_groups(gs_stepper* s, int span, bool phi, bool concurrent = false) {
   if (span <= 0) return 1;
   if (s->cfg.split_groups > 0) return s->cfg.split_groups < span ? s->cfg.split_groups : span;
+  // Local and remote launches share the GPU (two compute streams): one chunk per workgroup
+  // lets the dispatcher balance both launches dynamically (multi-chunk workgroups of the
+  // later launch would start behind the earlier one's and set a long tail).
+  if (concurrent) return span;
   const int fm = phi ? 2 : (s->exact ? 1 : 0);
   const int64_t resident = (int64_t)(s->occ[fm] > 0 ? s->occ[fm] : 4) * s->cus;
   const int64_t ib = s->L.n_local / (256 * s->L.ipl);
@@ -235,7 +239,8 @@ int enqueue_step(gs_stepper* s, bool capturing, bool gathered_externally) {
     gs::KArgs<T> loc = a;
     loc.c_begin = s->own_c0;
     loc.c_end = s->own_c1;
-    GS_HIP(gs::launch_force_split<T>(loc, kernel, ipl, choose_groups(s, s->own_c1 - s->own_c0, false),
+    GS_HIP(gs::launch_force_split<T>(loc, kernel, ipl,
+                                     choose_groups(s, s->own_c1 - s->own_c0, false, true),
                                      s->s_comp));
     if (timed) GS_HIP(hipEventRecord(s->ev_local, s->s_comp));
     GS_HIP(hipStreamWaitEvent(s->s_rem, s->ev_gathered, 0));
@@ -244,7 +249,7 @@ int enqueue_step(gs_stepper* s, bool capturing, bool gathered_externally) {
     r.skip_begin = s->own_c0;
     r.skip_end = s->own_c1;
     GS_HIP(gs::launch_force_split<T>(
-        r, kernel, ipl, choose_groups(s, s->L.n_chunks - (s->own_c1 - s->own_c0), false),
+        r, kernel, ipl, choose_groups(s, s->L.n_chunks - (s->own_c1 - s->own_c0), false, true),
         s->s_rem));
     GS_HIP(hipEventRecord(s->ev_remote, s->s_rem));
     GS_HIP(hipStreamWaitEvent(s->s_comp, s->ev_remote, 0));
