@@ -107,6 +107,16 @@ int gs_cpu_step_f32(const float* X4, float* Xn4, float* vel4, int64_t n_real, in
                     int64_t i1, int32_t chunk, float dt, float cut2, float eps2) {
   return step_range<float>(X4, Xn4, vel4, n_real, i0, i1, chunk, dt, cut2, eps2);
 }
+int gs_cpu_set_threads(int32_t n) {
+#ifdef _OPENMP
+  if (n > 0) omp_set_num_threads(n);
+  return omp_get_max_threads();
+#else
+  (void)n;
+  return 1;
+#endif
+}
+
 int gs_cpu_num_threads(void) {
 #ifdef _OPENMP
   return omp_get_max_threads();

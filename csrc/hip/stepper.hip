@@ -442,9 +442,12 @@ int gs_stepper_create(const gs_config* cfg, gs_stepper** out) {
   FAIL_CLEAN(hipMalloc(&s->partial, (size_t)s->L.n_chunks * s->L.n_local * rb));
   FAIL_CLEAN(hipMalloc(&s->mass_dev, (size_t)s->L.n_pad * sizeof(double)));
   FAIL_CLEAN(hipMalloc(&s->nonfinite, sizeof(unsigned long long)));
-  FAIL_CLEAN(hipMemset(s->X[0], 0, (size_t)s->L.n_pad * rb));
-  FAIL_CLEAN(hipMemset(s->X[1], 0, (size_t)s->L.n_pad * rb));
-  FAIL_CLEAN(hipMemset(s->vel, 0, (size_t)s->L.n_local * rb));
+  // Zero on the compute stream itself: it is non-blocking, so a legacy-stream hipMemset
+  // would NOT be ordered before later work on it (it could land after the IC kernel).
+  FAIL_CLEAN(hipMemsetAsync(s->X[0], 0, (size_t)s->L.n_pad * rb, s->s_comp));
+  FAIL_CLEAN(hipMemsetAsync(s->X[1], 0, (size_t)s->L.n_pad * rb, s->s_comp));
+  FAIL_CLEAN(hipMemsetAsync(s->vel, 0, (size_t)s->L.n_local * rb, s->s_comp));
+  FAIL_CLEAN(hipStreamSynchronize(s->s_comp));
 #undef FAIL_CLEAN
   *out = s;
   return 0;

@@ -99,6 +99,7 @@ int gs_cpu_step_f64(const double* X4, double* Xnext4, double* vel4, int64_t n_re
 int gs_cpu_step_f32(const float* X4, float* Xnext4, float* vel4, int64_t n_real, int64_t i0,
                     int64_t i1, int32_t chunk, float dt, float cut2, float eps2);
 int gs_cpu_num_threads(void);
+int gs_cpu_set_threads(int32_t n);  // OpenMP threads for the CPU engine (returns the new max)
 
 // ---------------------------------------------------------------- GPU Stepper (libgravsim_hip)
 typedef struct gs_stepper gs_stepper;

@@ -105,6 +105,7 @@ def cpu_lib():
             _sig(lib, f"gs_cpu_step_{t}", c_int32,
                  [P, P, P, c_int64, c_int64, c_int64, c_int32, T, T, T])
         _sig(lib, "gs_cpu_num_threads", c_int32, [])
+        _sig(lib, "gs_cpu_set_threads", c_int32, [c_int32])
         _cpu = lib
         return lib
 

@@ -180,9 +180,7 @@ class CpuEngine:
         self._accel = getattr(self.lib, f"gs_cpu_accel_{suf}")
         self._ptr = _native.dptr if cfg.dtype == "fp64" else _native.fptr
         if cfg.threads:
-            import os
-
-            os.environ["OMP_NUM_THREADS"] = str(cfg.threads)
+            self.lib.gs_cpu_set_threads(int(cfg.threads))
 
     def init_ics(self, family: str, seed: int) -> None:
         n, L = self.cfg.n, self.layout

@@ -1,0 +1,20 @@
+"""Summarise rocprofv3 --pmc CSVs (gpurun_out/pmc_*/**/pmc_counter_collection.csv) for the
+force kernels: per-counter totals over the profiled dispatches."""
+import collections
+import csv
+import glob
+import sys
+
+rows = collections.defaultdict(float)
+kern = collections.Counter()
+for path in glob.glob(sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc_*/**/*counter_collection.csv",
+                      recursive=True):
+    for r in csv.DictReader(open(path)):
+        name = r.get("Kernel_Name", "")
+        if "force_split_kernel" not in name and "force_fused_kernel" not in name:
+            continue
+        kern[name] += 1
+        rows[r["Counter_Name"]] += float(r["Counter_Value"])
+for k, v in sorted(rows.items()):
+    print(f"{k:32s} {v:.6g}")
+print("kernels:", dict(kern))
