@@ -40,11 +40,16 @@ extern "C" int gs_layout_compute(const gs_config* cfg, gs_layout* out) {
   out->n_local = out->n_pad / cfg->nranks;
   out->local_begin = (int64_t)cfg->rank * out->n_local;
   out->n_chunks = (int32_t)((cfg->n + chunk - 1) / chunk);
+  // j source: SGPR streaming through the scalar cache wins at >= 128K bodies per rank (no
+  // LDS barrier per tile); LDS-DMA tiles below that. i-bodies per lane: 4 for SGPR streaming
+  // and fp64, 8 for fp32 LDS tiles. Measured on MI355X: profiles/r1_rank_shape_v2.log,
+  // r1_sweep_64k_v2.log, r1_sweep_256k.log, r1_sweep_512k_fp64_halley.log.
+  out->kernel = cfg->kernel != GS_KERNEL_AUTO ? cfg->kernel
+                : (out->n_local >= 131072 ? GS_KERNEL_SMEM : GS_KERNEL_LDS);
   int32_t ipl = cfg->ipl;
   if (ipl <= 0) {
-    // Measured on MI355X (profiles/r1_rank_shape_v2.log, r1_sweep_512k_fp64_halley.log):
-    // 4 i-bodies per lane is best or tied for fp32 at 131K-1M bodies per rank and for fp64.
-    ipl = 4;
+    ipl = (cfg->dtype == GS_FP32 && out->kernel == GS_KERNEL_LDS) ? 8 : 4;
+    while (ipl > 1 && out->n_local % (256 * ipl) != 0) ipl /= 2;
   }
   if (ipl != 1 && ipl != 2 && ipl != 4 && !(ipl == 8 && cfg->dtype == GS_FP32)) {
     gs_set_error("layout: ipl must be 1, 2, 4 (or 8 for fp32)");
@@ -55,10 +60,6 @@ extern "C" int gs_layout_compute(const gs_config* cfg, gs_layout* out) {
     return -1;
   }
   out->ipl = ipl;
-  // j source: SGPR streaming through the scalar cache wins at >= 128K bodies per rank (no LDS
-  // barrier per tile); LDS-DMA tiles below that (profiles/r1_sweep_64k_*.log).
-  out->kernel = cfg->kernel != GS_KERNEL_AUTO ? cfg->kernel
-                : (out->n_local >= 131072 ? GS_KERNEL_SMEM : GS_KERNEL_LDS);
   const int64_t i_blocks = out->n_local / (256 * ipl);
   int32_t mode = cfg->mode;
   if (mode == GS_MODE_AUTO) {
