@@ -193,10 +193,29 @@ __device__ __forceinline__ void sweep_smem(const V4<T>* __restrict__ X, int64_t 
     const int c = seq.chunk(v);
     zero_chunk<T, IPL>(st);
     const V4<T>* p = X + (int64_t)c * chunk;
+#ifdef GS_SMEM_NO_PREFETCH
     for (int64_t j = 0; j < chunk; j += 4) {
 #pragma unroll
       for (int u = 0; u < 4; ++u) interact_all<T, IPL, FM>(st, p[j + u], cut2, eps2);
     }
+#else
+    // Software pipeline: the next 4 j-bodies (one s_load_dwordx16 for fp32) are requested
+    // before the current 4 are consumed, so scalar-cache / L2 latency overlaps the VALU work.
+    V4<T> q0 = p[0], q1 = p[1], q2 = p[2], q3 = p[3];
+    for (int64_t j = 4; j < chunk; j += 4) {
+      const V4<T> n0 = p[j], n1 = p[j + 1], n2 = p[j + 2], n3 = p[j + 3];
+      __builtin_amdgcn_sched_barrier(0);  // keep the loads at the top of the iteration
+      interact_all<T, IPL, FM>(st, q0, cut2, eps2);
+      interact_all<T, IPL, FM>(st, q1, cut2, eps2);
+      interact_all<T, IPL, FM>(st, q2, cut2, eps2);
+      interact_all<T, IPL, FM>(st, q3, cut2, eps2);
+      q0 = n0; q1 = n1; q2 = n2; q3 = n3;
+    }
+    interact_all<T, IPL, FM>(st, q0, cut2, eps2);
+    interact_all<T, IPL, FM>(st, q1, cut2, eps2);
+    interact_all<T, IPL, FM>(st, q2, cut2, eps2);
+    interact_all<T, IPL, FM>(st, q3, cut2, eps2);
+#endif
     on_chunk(c);
   }
 }
