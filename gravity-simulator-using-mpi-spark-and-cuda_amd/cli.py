@@ -32,6 +32,9 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--cutoff-mode", choices=["auto", "exact", "fast"], default=d.cutoff_mode,
                    help="GPU force path: exact hard-cutoff select, or fast (cutoff inside an "
                         "overflow-safe core; bit-identical for separations above ~mm)")
+    p.add_argument("--integrator", choices=["kd", "leapfrog"], default=d.integrator,
+                   help="kd: the reference's kick-drift update; leapfrog: the same kernel on "
+                        "half-step-staggered velocities (second order)")
     p.add_argument("--kernel", choices=["auto", "lds", "smem"], default=d.kernel)
     p.add_argument("--mode", choices=["auto", "fused", "split"], default=d.mode)
     p.add_argument("--ipl", type=int, default=d.ipl, choices=[0, 1, 2, 4, 8])
@@ -68,7 +71,7 @@ def config_from_args(a: argparse.Namespace) -> SimConfig:
             resume = ckpt.latest(resume)
     return SimConfig(n=a.n, dt=a.dt, steps=a.steps, dtype=a.dtype, device=a.device, init=a.init,
                      seed=a.seed, G=a.G, cutoff=a.cutoff, softening=a.softening,
-                     cutoff_mode=a.cutoff_mode, kernel=a.kernel,
+                     cutoff_mode=a.cutoff_mode, integrator=a.integrator, kernel=a.kernel,
                      mode=a.mode, ipl=a.ipl, chunk=a.chunk, graph=a.graph, threads=a.threads,
                      log_dir=a.log_dir, log_format=a.log_format, progress_every=a.progress_every,
                      print_positions=a.print_positions, dump_path=a.dump_path,
@@ -79,7 +82,6 @@ def config_from_args(a: argparse.Namespace) -> SimConfig:
 
 def run_one(cfg: SimConfig, dist, log, quiet: bool = False, final: bool = True) -> dict:
     from .runtime.simulation import Simulation
-    from .utils import checkpoint as ckpt
     from .utils.logs import format_positions_mpi
 
     sim = Simulation(cfg, dist)
@@ -87,21 +89,18 @@ def run_one(cfg: SimConfig, dist, log, quiet: bool = False, final: bool = True) 
         if log and dist.is_root:
             log.header(dist.world, cfg.n, cfg.steps, cfg.dt)
         m = sim.run(cfg.steps, log if dist.is_root else None)
-        state = sim.global_state()
+        state = sim.global_state()  # collective
+        if cfg.dump_path and cfg.dump_path.endswith(".gsck"):
+            sim.save_checkpoint(cfg.dump_path)  # collective; rank 0 writes
         if dist.is_root:
             if log:
                 log.stats(m.wall_s, m.steps)
                 log.positions(state.pos, cfg.print_positions)
                 if final:
                     log.completed()
-            if cfg.dump_path:
-                if cfg.dump_path.endswith(".gsck"):
-                    meta = dict(dt=cfg.dt, dtype=cfg.dtype, G=cfg.G, cutoff=cfg.cutoff,
-                                softening=cfg.softening, init=cfg.init, seed=cfg.seed)
-                    ckpt.save(cfg.dump_path, state, sim.step, meta)
-                else:
-                    with open(cfg.dump_path, "w") as f:
-                        f.write(format_positions_mpi(state.pos))
+            if cfg.dump_path and not cfg.dump_path.endswith(".gsck"):
+                with open(cfg.dump_path, "w") as f:
+                    f.write(format_positions_mpi(state.pos))
             if cfg.record_path:
                 sim.save_trajectory(cfg.record_path)
             line = m.to_json()

@@ -34,6 +34,7 @@ class SimConfig:
     cutoff: float = 1e-10         # hard cutoff radius (cuda.cu:39, mpi.c:64, pyspark.py:38)
     softening: float = 0.0        # Plummer softening length (0 = reference semantics)
     cutoff_mode: str = "auto"     # GPU: exact (select) | fast (overflow-safe core) | auto
+    integrator: str = "kd"        # kd (reference kick-drift) | leapfrog (staggered KDK)
     kernel: str = "auto"          # GPU j-source variant: lds | smem
     mode: str = "auto"            # GPU schedule: fused | split
     ipl: int = 0                  # i-bodies per lane (0 = auto)
@@ -78,6 +79,8 @@ class SimConfig:
             raise ValueError("ipl must be 0, 1, 2, 4 (or 8 for fp32)")
         if self.chunk and self.chunk % 1024:
             raise ValueError("chunk must be a multiple of 1024")
+        if self.integrator not in ("kd", "leapfrog"):
+            raise ValueError("integrator must be kd or leapfrog")
         if self.cutoff_mode not in ("auto", "exact", "fast"):
             raise ValueError("cutoff_mode must be auto, exact or fast")
         if self.cutoff < 0 or self.softening < 0:

@@ -59,11 +59,25 @@ def step(pos, vel, mass, dt, G=G_SI, cutoff=1e-10, softening=0.0):
     return x, v
 
 
-def simulate(pos, vel, mass, dt, steps, G=G_SI, cutoff=1e-10, softening=0.0, record_every=0):
-    """Run `steps` steps. Returns (pos, vel, trajectory list of positions if record_every)."""
+def simulate(pos, vel, mass, dt, steps, G=G_SI, cutoff=1e-10, softening=0.0, record_every=0,
+             integrator="kd"):
+    """Run `steps` steps. Returns (pos, vel, trajectory list of positions if record_every).
+
+    integrator "leapfrog": kick-drift-kick, v_{1/2} = v_0 + a_0 dt/2, x_1 = x_0 + v_{1/2} dt,
+    v_1 = v_{1/2} + a_1 dt/2 (velocities returned synchronized)."""
     x = np.array(pos, dtype=np.float64, copy=True)
     v = np.array(vel, dtype=np.float64, copy=True)
     traj = []
+    if integrator == "leapfrog":
+        a = accelerations(x, mass, G, cutoff, softening)
+        for s in range(steps):
+            v = v + 0.5 * dt * a
+            x = x + v * dt
+            a = accelerations(x, mass, G, cutoff, softening)
+            v = v + 0.5 * dt * a
+            if record_every and (s + 1) % record_every == 0:
+                traj.append(x.copy())
+        return x, v, traj
     for s in range(steps):
         x, v = step(x, v, mass, dt, G, cutoff, softening)
         if record_every and (s + 1) % record_every == 0:

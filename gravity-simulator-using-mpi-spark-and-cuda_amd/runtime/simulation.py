@@ -9,7 +9,13 @@ design:
   but ends with a device sync so the number is real;
 * NaN/Inf guard (the reference silently produced non-finite output, D1-D3) and RCCL health
   checks run at a configurable period;
-* checkpoints are rank-agnostic and a resumed run continues bit-exactly.
+* checkpoints are rank-agnostic and a resumed run continues bit-exactly;
+* integrator "kd" is the reference's kick-drift update (cuda.cu:73-76, mpi.c:207-215);
+  "leapfrog" runs the very same per-step kernel on velocities staggered by half a step
+  (v_{k-1/2}): a backward half-kick at the start, synchronized velocities
+  v_k = v_{k-1/2} + a(x_k) dt/2 on output — second-order (KDK) accuracy at no extra cost per
+  step. Checkpoints keep the staggered velocities (meta "velocity": "half-step") so resume
+  stays bit-exact.
 """
 from __future__ import annotations
 
@@ -52,14 +58,22 @@ class Simulation:
             self.engine = CpuEngine(cfg, d.rank, d.world, dist=d)
         self.step0 = 0
         self.trajectory: list[np.ndarray] = []
+        self.staggered = False  # velocities held as v_{k-1/2} (leapfrog)
         if cfg.resume:
             c = ckpt.load(cfg.resume)
             if c.bodies.n != cfg.n:
                 raise ValueError(f"checkpoint has n={c.bodies.n}, config n={cfg.n}")
             self.engine.load(c.bodies)
             self.step0 = c.step
+            self.staggered = c.meta.get("velocity") == "half-step"
         else:
             self.engine.init_ics(cfg.init, cfg.seed)
+        if cfg.integrator == "leapfrog" and not self.staggered:
+            self._half_kick(-1.0)
+            self.staggered = True
+        elif cfg.integrator == "kd" and self.staggered:
+            self._half_kick(+1.0)
+            self.staggered = False
 
     @property
     def device(self) -> str:
@@ -69,12 +83,39 @@ class Simulation:
     def step(self) -> int:
         return self.step0 + self.engine.steps_done
 
-    def global_state(self) -> BodySet:
-        """Full (pos, vel, mass) on every rank (collective when P > 1)."""
+    def _own_accel(self) -> np.ndarray:
+        """(n, 3) accelerations with this rank's rows filled (others zero)."""
+        L = self.engine.layout
+        acc = np.zeros((self.cfg.n, 3))
+        rows = L.real_local
+        if len(rows):
+            acc[rows.start:rows.stop] = self.engine.accel()[: len(rows), :3]
+        return acc
+
+    def _half_kick(self, sign: float) -> None:
+        """v += sign * a(x) dt/2 on every body (collective): the leapfrog stagger."""
+        b = self.engine.state()
+        acc = self._own_accel()
+        b.vel = b.vel + sign * 0.5 * self.cfg.dt * acc
+        self.engine.load(b)
+
+    def raw_state(self) -> BodySet:
+        """Full (pos, vel as stored, mass) on every rank (collective when P > 1)."""
         b = self.engine.state()
         if self.dist.world > 1:
             rows = self.engine.layout.real_local
             comm.gather_rows_to_root(self.dist, b.vel, slice(rows.start, rows.stop))
+        return b
+
+    def global_state(self) -> BodySet:
+        """Full (pos, synchronized vel, mass) on every rank (collective when P > 1)."""
+        b = self.raw_state()
+        if self.staggered:
+            acc = self._own_accel()
+            if self.dist.world > 1:
+                comm.gather_rows_to_root(self.dist, acc, slice(self.engine.layout.real_local.start,
+                                                               self.engine.layout.real_local.stop))
+            b.vel = b.vel + 0.5 * self.cfg.dt * acc
         return b
 
     def check_finite(self) -> None:
@@ -86,14 +127,15 @@ class Simulation:
             self.engine.comm_check()
 
     def save_checkpoint(self, path: Optional[str] = None) -> Optional[str]:
-        b = self.global_state()
+        b = self.raw_state()
         if not self.dist.is_root:
             return None
         cfg = self.cfg
         path = path or ckpt.path_for(cfg.checkpoint_dir or ".", self.step)
         meta = dict(dt=cfg.dt, dtype=cfg.dtype, G=cfg.G, cutoff=cfg.cutoff,
                     softening=cfg.softening, init=cfg.init, seed=cfg.seed,
-                    time=self.step * cfg.dt)
+                    time=self.step * cfg.dt, integrator=cfg.integrator,
+                    velocity="half-step" if self.staggered else "synchronized")
         return ckpt.save(path, b, self.step, meta)
 
     def run(self, steps: Optional[int] = None, log: Optional[RunLog] = None) -> RunMetrics:
@@ -113,7 +155,7 @@ class Simulation:
             if cfg.nan_check_every and s % cfg.nan_check_every == 0:
                 self.check_finite()
             if cfg.record_every and s % cfg.record_every == 0:
-                self.trajectory.append(self.global_state().pos.copy())
+                self.trajectory.append(self.raw_state().pos.copy())
             if cfg.checkpoint_every and s % cfg.checkpoint_every == 0 and cfg.checkpoint_dir:
                 self.save_checkpoint()
         self.engine.sync()

@@ -90,3 +90,17 @@ def test_plummer_model_on_gpu_energy(hip):
     b1 = sim.global_state()
     sim.close()
     assert abs(energy(b1.pos, b1.vel, b1.mass) - e0) / abs(e0) < 1e-3
+
+
+def test_gpu_leapfrog_matches_oracle_kdk(hip):
+    from gravsim.ops import oracle
+
+    cfg = SimConfig(n=800, steps=10, dtype="fp64", device="gpu", integrator="leapfrog")
+    sim = Simulation(cfg)
+    b0 = ic.solar_random(800, cfg.seed)
+    sim.run()
+    got = sim.global_state()
+    sim.close()
+    x, v, _ = oracle.simulate(b0.pos, b0.vel, b0.mass, cfg.dt, 10, integrator="leapfrog")
+    assert np.abs(got.pos - x).max() / np.abs(x).max() < 1e-12
+    assert np.abs(got.vel - v).max() / np.abs(v).max() < 1e-10
