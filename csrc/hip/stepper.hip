@@ -700,7 +700,9 @@ int gs_stepper_comm_init(gs_stepper* s, const void* id128, int32_t rank, int32_t
   ncclUniqueId id;
   memcpy(&id, id128, sizeof(id));
   GS_NCCL(ncclCommInitRank(&s->comm, nranks, id, rank));
-  s->have_comm = nranks > 1;
+  // GRAVSIM_FORCE_COMM keeps a 1-rank communicator live so the full multi-rank schedule
+  // (in-place ncclAllGather, local/remote split on two streams, events) runs on one GPU.
+  s->have_comm = nranks > 1 || getenv("GRAVSIM_FORCE_COMM") != nullptr;
   if (!s->have_comm) {
     (void)ncclCommDestroy(s->comm);
     s->comm = nullptr;

@@ -73,3 +73,40 @@ def test_rccl_two_ranks_match_single_rank(hip, tmp_path):
     ref = eng.state().pos
     eng.close()
     assert np.array_equal(np.load(tmp_path / "pos.npy"), ref)
+
+
+@pytest.mark.parametrize("graph", [1, 2])
+def test_rccl_one_rank_full_schedule_bitwise(hip, monkeypatch, graph):
+    """A live 1-rank RCCL communicator drives the whole multi-rank step (in-place
+    ncclAllGather, concurrent local/remote split, ordered reduce) — eagerly and captured into
+    a hipGraph (use_graph=2 captures the collective) — and must match the plain path."""
+    from gravsim.config import SimConfig
+    from gravsim.runtime.engines import HipEngine
+
+    monkeypatch.setenv("GRAVSIM_FORCE_COMM", "1")
+    cfg = SimConfig(n=6000, dtype="fp32", device="gpu", chunk=1024)
+    eng = HipEngine(cfg)
+    eng.lib.gs_stepper_destroy(eng._s)  # rebuild with the requested graph mode
+    import ctypes
+
+    from gravsim.ops import _native
+    from gravsim.runtime.engines import _gs_config
+
+    c = _gs_config(cfg, 0, 1, 0)
+    c.use_graph = graph
+    eng._s = ctypes.c_void_p()
+    _native.check(eng.lib, eng.lib.gs_stepper_create(ctypes.byref(c), ctypes.byref(eng._s)),
+                  "create")
+    eng.comm_init(HipEngine.unique_id())
+    eng.init_ics("solar+random", 4)
+    eng.step(7)
+    eng.sync(timeout_s=60)
+    got = eng.state().pos
+    eng.close()
+    monkeypatch.delenv("GRAVSIM_FORCE_COMM")
+    ref_eng = HipEngine(cfg)
+    ref_eng.init_ics("solar+random", 4)
+    ref_eng.step(7)
+    ref = ref_eng.state().pos
+    ref_eng.close()
+    assert np.array_equal(got, ref)
