@@ -292,45 +292,26 @@ __global__ __launch_bounds__(kBlock) void force_split_kernel(KArgs<T> a) {
     sweep_smem<T, IPL, FM>(X, a.chunk, seq, v0, v1, a.cut2, a.eps2, st, store);
 }
 
-// FUSED: grid (i_blocks). Sweep every chunk in canonical order; chunks in [pre_begin,
-// pre_end) are taken from partial (computed earlier, e.g. the rank-local tile that overlapped
-// the all-gather). Integrate in the epilogue.
+// FUSED: grid (i_blocks). One workgroup sweeps every chunk in canonical order and integrates
+// in its epilogue (no partial buffer); used when the i-blocks alone fill the GPU.
 template <typename T, int IPL, int KV, int FM>
 __global__ __launch_bounds__(kBlock) void force_fused_kernel(KArgs<T> a) {
   __shared__ __attribute__((aligned(16))) V4<T> tile[2][Tile<T>::kBodies];
   const int64_t ib = (int64_t)blockIdx.x * (kBlock * IPL);
   IState<T, IPL> st;
   load_i<T, IPL>(a, st, ib);
-  const V4<T>* part = reinterpret_cast<const V4<T>*>(a.partial);
   auto fold = [&](int) {
 #pragma unroll
     for (int k = 0; k < IPL; ++k) {
       st.tx[k] += st.ax[k]; st.ty[k] += st.ay[k]; st.tz[k] += st.az[k]; st.tp[k] += st.ph[k];
     }
   };
-  auto fold_pre = [&](int c) {
-#pragma unroll
-    for (int k = 0; k < IPL; ++k) {
-      const V4<T> p = part[(int64_t)c * a.n_local + ib + threadIdx.x + k * kBlock];
-      st.tx[k] += p.x; st.ty[k] += p.y; st.tz[k] += p.z; st.tp[k] += p.w;
-    }
-  };
   const V4<T>* X = reinterpret_cast<const V4<T>*>(a.X);
-  // Three canonical-order segments: [0, pre_begin) computed, [pre_begin, pre_end) loaded,
-  // [pre_end, n_chunks) computed.
-  const int pb = min(max(a.pre_begin, 0), a.n_chunks);
-  const int pe = min(max(a.pre_end, pb), a.n_chunks);
   const ChunkSeq seq{0, a.n_chunks, 0};
-  if constexpr (KV == GS_KERNEL_LDS) {
-    sweep_lds<T, IPL, FM>(X, a.chunk, seq, 0, pb, a.cut2, a.eps2, st, tile, fold);
-    for (int c = pb; c < pe; ++c) fold_pre(c);
-    __syncthreads();  // both LDS buffers are refilled by the next sweep
-    sweep_lds<T, IPL, FM>(X, a.chunk, seq, pe, a.n_chunks, a.cut2, a.eps2, st, tile, fold);
-  } else {
-    sweep_smem<T, IPL, FM>(X, a.chunk, seq, 0, pb, a.cut2, a.eps2, st, fold);
-    for (int c = pb; c < pe; ++c) fold_pre(c);
-    sweep_smem<T, IPL, FM>(X, a.chunk, seq, pe, a.n_chunks, a.cut2, a.eps2, st, fold);
-  }
+  if constexpr (KV == GS_KERNEL_LDS)
+    sweep_lds<T, IPL, FM>(X, a.chunk, seq, 0, a.n_chunks, a.cut2, a.eps2, st, tile, fold);
+  else
+    sweep_smem<T, IPL, FM>(X, a.chunk, seq, 0, a.n_chunks, a.cut2, a.eps2, st, fold);
   if (a.acc_out) {
     V4<T>* out = reinterpret_cast<V4<T>*>(a.acc_out);
 #pragma unroll

@@ -11,12 +11,15 @@
 //                    stream, overlapped with the rank-local j-chunks on the compute stream;
 //                    ordering by events, no barrier.
 // Step k (P ranks, ping-pong buffers X[0], X[1]):
-//   comm:    wait(own slice of X[k&1] written) -> ncclAllGather in place -> record gathered
-//   compute: split kernel over own chunks (reads only the own slice) -> partial
-//            wait(gathered) -> fused kernel over all chunks (own chunks read from partial)
-//            with the KD integrate in its epilogue -> own slice of X[(k+1)&1]
-// With one rank the step is a single fused launch (or split + reduce at small N); the loop
-// can be captured once into a hipGraph (two steps = one ping-pong period) and replayed.
+//   s_comm : wait(own slice of X[k&1] written) -> ncclAllGather in place -> record gathered
+//   s_comp : split kernel over own chunks (reads only the own slice)     -> partials
+//   s_rem  : wait(gathered) -> ONE split launch over every remote chunk  -> partials
+//   s_comp : wait(remote) -> reduce in canonical chunk order + KD integrate
+//            -> own slice of X[(k+1)&1]
+// The two split launches run concurrently (one chunk per workgroup). With one rank the step
+// is a single fused launch (KD integrate in its epilogue) or split + reduce; the loop is
+// captured once into a hipGraph (two steps = one ping-pong period) and replayed. With
+// use_graph >= 2 the multi-rank step, collective included, is captured too.
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <math.h>
@@ -143,7 +146,6 @@ gs::KArgs<T> base_args(gs_stepper* s, int cur) {
   a.n_chunks = s->L.n_chunks;
   a.c_begin = 0;
   a.c_end = s->L.n_chunks;
-  a.pre_begin = a.pre_end = 0;
   a.phi = 0;
   a.exact = s->exact ? 1 : 0;
   a.dt = (T)s->cfg.dt;

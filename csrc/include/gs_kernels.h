@@ -22,7 +22,6 @@ struct KArgs {
   int32_t n_chunks;  // chunks holding real bodies
   int32_t c_begin, c_end;      // split kernel: chunk range ...
   int32_t skip_begin, skip_end;  // ... minus this sub-range (the rank's own chunks)
-  int32_t pre_begin, pre_end;  // fused kernel: chunk range read from partial
   int32_t phi;       // accumulate the potential sum too (implies the exact cutoff)
   int32_t exact;     // hard cutoff select (else the fast core-softened path)
   T dt, cut2, eps2;  // eps2: softening^2, or the fast path's core^2 when larger
