@@ -36,6 +36,8 @@ def main() -> int:
     ap.add_argument("--mode", default="auto", choices=["auto", "fused", "split"])
     ap.add_argument("--ipl", type=int, default=0)
     ap.add_argument("--no-graph", dest="graph", action="store_false")
+    ap.add_argument("--graph-comm", action="store_true",
+                    help="capture the multi-rank step incl. the RCCL all-gather in a hipGraph")
     ap.add_argument("--dt", type=float, default=3600.0)
     ap.add_argument("--cutoff-mode", default="auto", choices=["auto", "exact", "fast"])
     a = ap.parse_args()
@@ -58,7 +60,8 @@ def main() -> int:
     torch.cuda.set_device(dev)
 
     cfg = SimConfig(n=a.n, dt=a.dt, dtype=a.dtype, device="gpu", kernel=a.kernel, mode=a.mode,
-                    ipl=a.ipl, graph=a.graph, cutoff_mode=a.cutoff_mode).validate()
+                    ipl=a.ipl, graph=a.graph, graph_comm=a.graph_comm,
+                    cutoff_mode=a.cutoff_mode).validate()
     eng = HipEngine(cfg, rank, world, device=dev, dist=dist)
     if world > 1:
         uid = HipEngine.unique_id() if rank == 0 else None

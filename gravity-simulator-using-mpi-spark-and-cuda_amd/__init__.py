@@ -19,4 +19,19 @@ from .config import SimConfig, G_SI  # noqa: F401
 
 __version__ = "0.1.0"
 
-__all__ = ["SimConfig", "G_SI", "__version__"]
+
+def __getattr__(name):  # lazy: keep `import gravsim` light (no torch / native load)
+    if name in ("GravitySimulator", "SparkGravitySimulator", "Particle", "create_solar_system",
+                "generate_random_particles"):
+        from . import api
+
+        return getattr(api, name)
+    if name == "Simulation":
+        from .runtime.simulation import Simulation
+
+        return Simulation
+    raise AttributeError(name)
+
+
+__all__ = ["SimConfig", "G_SI", "Simulation", "GravitySimulator", "SparkGravitySimulator",
+           "Particle", "create_solar_system", "generate_random_particles", "__version__"]

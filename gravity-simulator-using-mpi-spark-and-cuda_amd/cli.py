@@ -40,6 +40,8 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--ipl", type=int, default=d.ipl, choices=[0, 1, 2, 4, 8])
     p.add_argument("--chunk", type=int, default=d.chunk)
     p.add_argument("--no-graph", dest="graph", action="store_false")
+    p.add_argument("--graph-comm", action="store_true",
+                   help="capture the multi-rank step, RCCL all-gather included, in a hipGraph")
     p.add_argument("--threads", type=int, default=0)
     p.add_argument("--log-dir", default=None, help="write the text log under this directory")
     p.add_argument("--log-format", choices=["mpi", "spark", "cuda", "none"], default=d.log_format)
@@ -72,7 +74,8 @@ def config_from_args(a: argparse.Namespace) -> SimConfig:
     return SimConfig(n=a.n, dt=a.dt, steps=a.steps, dtype=a.dtype, device=a.device, init=a.init,
                      seed=a.seed, G=a.G, cutoff=a.cutoff, softening=a.softening,
                      cutoff_mode=a.cutoff_mode, integrator=a.integrator, kernel=a.kernel,
-                     mode=a.mode, ipl=a.ipl, chunk=a.chunk, graph=a.graph, threads=a.threads,
+                     mode=a.mode, ipl=a.ipl, chunk=a.chunk, graph=a.graph, graph_comm=a.graph_comm,
+                     threads=a.threads,
                      log_dir=a.log_dir, log_format=a.log_format, progress_every=a.progress_every,
                      print_positions=a.print_positions, dump_path=a.dump_path,
                      checkpoint_dir=a.checkpoint_dir, checkpoint_every=a.checkpoint_every,

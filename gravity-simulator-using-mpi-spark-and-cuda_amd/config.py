@@ -41,6 +41,7 @@ class SimConfig:
     chunk: int = 0                # canonical j-chunk (0 = auto from n)
     split_groups: int = 0
     graph: bool = True            # hipGraph replay of the step loop (single rank)
+    graph_comm: bool = False      # also capture the multi-rank step (RCCL collective included)
     comm: str = "auto"            # rccl (GPU) | gloo (CPU) | none
     threads: int = 0              # CPU engine OpenMP threads (0 = default)
     step_timeout_s: float = 600.0 # multi-rank hang detection: abort RCCL after this wait

@@ -29,7 +29,8 @@ def _gs_config(cfg: SimConfig, rank: int, nranks: int, device: int) -> _native.G
     return _native.GsConfig(
         n=cfg.n, dtype=_native.GS_FP64 if cfg.dtype == "fp64" else _native.GS_FP32,
         kernel=_native.KERNEL_IDS[cfg.kernel], mode=_native.MODE_IDS[cfg.mode], ipl=cfg.ipl,
-        chunk=cfg.chunk, rank=rank, nranks=nranks, device=device, use_graph=int(cfg.graph),
+        chunk=cfg.chunk, rank=rank, nranks=nranks, device=device,
+        use_graph=(2 if cfg.graph_comm else 1) if cfg.graph else 0,
         split_groups=cfg.split_groups, cutoff_mode=_native.CUTOFF_IDS[cfg.cutoff_mode], dt=cfg.dt,
         G=cfg.G, cutoff=cfg.cutoff, softening=cfg.softening)
 
