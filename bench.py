@@ -40,6 +40,8 @@ def main() -> int:
                     help="capture the multi-rank step incl. the RCCL all-gather in a hipGraph")
     ap.add_argument("--dt", type=float, default=3600.0)
     ap.add_argument("--cutoff-mode", default="auto", choices=["auto", "exact", "fast"])
+    ap.add_argument("--strategy", default="allgather", choices=["allgather", "ring"],
+                    help="multi-rank exchange: in-place all-gather or pipelined ring pass")
     a = ap.parse_args()
 
     import torch
@@ -61,7 +63,7 @@ def main() -> int:
 
     cfg = SimConfig(n=a.n, dt=a.dt, dtype=a.dtype, device="gpu", kernel=a.kernel, mode=a.mode,
                     ipl=a.ipl, graph=a.graph, graph_comm=a.graph_comm,
-                    cutoff_mode=a.cutoff_mode).validate()
+                    cutoff_mode=a.cutoff_mode, strategy=a.strategy).validate()
     eng = HipEngine(cfg, rank, world, device=dev, dist=dist)
     if world > 1:
         uid = HipEngine.unique_id() if rank == 0 else None
@@ -107,7 +109,8 @@ def main() -> int:
                 "global_batch": cfg.n,
                 "seq_len": 1,
                 "dt": cfg.dt,
-                "parallelism": f"body-decomposition x{world} (RCCL all-gather)" if world > 1
+                "parallelism": f"body-decomposition x{world} (RCCL "
+                f"{'ring send/recv' if a.strategy == 'ring' else 'all-gather'})" if world > 1
                 else "single GPU",
                 "kernel": _native.KERNEL_NAMES.get(lay["kernel"]),
                 "mode": _native.MODE_NAMES.get(lay["mode"]),

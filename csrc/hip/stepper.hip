@@ -69,6 +69,9 @@ struct gs_stepper {
   size_t esz = 4;  // element size
   hipStream_t s_comp = nullptr, s_comm = nullptr;
   hipStream_t s_rem = nullptr;  // second compute stream: remote chunks beside the local ones
+  hipStream_t s_rem2 = nullptr;  // third compute stream: ring sub-steps alternate rem/rem2
+  hipEvent_t ev_rem2 = nullptr;
+  std::vector<hipEvent_t> ev_recv;  // ring: per sub-step "slice arrived" events
   hipEvent_t ev_ready = nullptr, ev_gathered = nullptr, ev_remote = nullptr, ev_fork = nullptr;
   hipEvent_t ev_t0 = nullptr, ev_local = nullptr, ev_end = nullptr;
   void* X[2] = {nullptr, nullptr};
@@ -218,6 +221,66 @@ int gather(gs_stepper* s, int cur) {
   return 0;
 }
 
+// ---- ring pass (strategy 1) ------------------------------------------------------------
+// Rank r computes its own chunks first (sub-step 0), then at sub-step s the slice of rank
+// (r - s) mod P, which arrives from the left neighbour while sub-step s-1 computes; it is
+// forwarded to the right neighbour in the next sub-step. Each slice lands at its own offset
+// of X[cur], so no buffer is reused within a step; per-chunk partials + the canonical reduce
+// keep the result bit-identical to the all-gather schedule.
+int ring_src(const gs_stepper* s, int sub) {
+  const int P = s->cfg.nranks;
+  return ((s->cfg.rank - sub) % P + P) % P;
+}
+
+void rank_chunks(const gs_stepper* s, int src, int* c0, int* c1) {
+  const int64_t per = s->L.n_local / s->L.chunk;
+  int64_t a = (int64_t)src * per, b = a + per;
+  if (a > s->L.n_chunks) a = s->L.n_chunks;
+  if (b > s->L.n_chunks) b = s->L.n_chunks;
+  *c0 = (int)a;
+  *c1 = (int)b;
+}
+
+// Enqueue the transfer of ring sub-step `sub` (1..P-1) on the comm stream: send the slice
+// received at sub-step sub-1 (own slice for sub = 1) right, receive slice ring_src(sub) left.
+int ring_xfer_rccl(gs_stepper* s, int cur, int sub) {
+  const int P = s->cfg.nranks, r = s->cfg.rank;
+  char* buf = static_cast<char*>(s->X[cur]);
+  const size_t slice = (size_t)s->L.n_local * row_bytes(s);
+  const size_t count = (size_t)s->L.n_local * 4;
+  const ncclDataType_t dt = s->esz == 4 ? ncclFloat32 : ncclFloat64;
+  const int send_src = ring_src(s, sub - 1), recv_src = ring_src(s, sub);
+  GS_NCCL(ncclGroupStart());
+  GS_NCCL(ncclSend(buf + send_src * slice, count, dt, (r + 1) % P, s->comm, s->s_comm));
+  GS_NCCL(ncclRecv(buf + recv_src * slice, count, dt, (r - 1 + P) % P, s->comm, s->s_comm));
+  GS_NCCL(ncclGroupEnd());
+  return 0;
+}
+
+template <typename T>
+int ring_compute(gs_stepper* s, const gs::KArgs<T>& a, int sub, hipEvent_t ready) {
+  int c0, c1;
+  rank_chunks(s, ring_src(s, sub), &c0, &c1);
+  gs::KArgs<T> k = a;
+  k.c_begin = c0;
+  k.c_end = c1;
+  hipStream_t st = sub == 0 ? s->s_comp : ((sub & 1) ? s->s_rem : s->s_rem2);
+  if (ready) GS_HIP(hipStreamWaitEvent(st, ready, 0));
+  GS_HIP(gs::launch_force_split<T>(k, s->L.kernel, s->L.ipl, choose_groups(s, c1 - c0, false, true),
+                                   st));
+  return 0;
+}
+
+template <typename T>
+int ring_finish(gs_stepper* s, const gs::KArgs<T>& a) {
+  GS_HIP(hipEventRecord(s->ev_remote, s->s_rem));
+  GS_HIP(hipEventRecord(s->ev_rem2, s->s_rem2));
+  GS_HIP(hipStreamWaitEvent(s->s_comp, s->ev_remote, 0));
+  GS_HIP(hipStreamWaitEvent(s->s_comp, s->ev_rem2, 0));
+  GS_HIP(gs::launch_reduce_integrate<T>(a, s->s_comp));
+  return 0;
+}
+
 // Enqueue one step. `capturing` disables timing events.
 template <typename T>
 int enqueue_step(gs_stepper* s, bool capturing, bool gathered_externally) {
@@ -229,6 +292,30 @@ int enqueue_step(gs_stepper* s, bool capturing, bool gathered_externally) {
   const bool timed = s->timed && !capturing;
   if (timed) GS_HIP(hipEventRecord(s->ev_t0, s->s_comp));
   const bool need_gather = (s->have_comm || s->virt) && !s->full[cur];
+  const bool ring = s->cfg.strategy == GS_STRATEGY_RING;
+  if (need_gather && ring && (s->emulate || !gathered_externally)) {
+    // Ring pass with RCCL (or timing emulation: no transfer, slices treated as present).
+    GS_HIP(hipEventRecord(s->ev_fork, s->s_comp));
+    GS_HIP(hipStreamWaitEvent(s->s_rem, s->ev_fork, 0));
+    GS_HIP(hipStreamWaitEvent(s->s_rem2, s->ev_fork, 0));
+    if (s->have_comm) GS_HIP(hipStreamWaitEvent(s->s_comm, s->ev_fork, 0));
+    if (ring_compute<T>(s, a, 0, nullptr)) return -1;
+    for (int sub = 1; sub < s->cfg.nranks; ++sub) {
+      hipEvent_t ready = nullptr;
+      if (s->have_comm) {
+        if (ring_xfer_rccl(s, cur, sub)) return -1;
+        GS_HIP(hipEventRecord(s->ev_recv[sub], s->s_comm));
+        ready = s->ev_recv[sub];
+      }
+      if (ring_compute<T>(s, a, sub, ready)) return -1;
+    }
+    if (ring_finish<T>(s, a)) return -1;
+    if (timed) GS_HIP(hipEventRecord(s->ev_end, s->s_comp));
+    s->full[cur] = true;
+    s->full[cur ^ 1] = false;
+    s->k += 1;
+    return 0;
+  }
   if (need_gather) {
     if (gathered_externally) s->full[cur] = true;
     else if (gather(s, cur)) return -1;
@@ -429,6 +516,10 @@ int gs_stepper_create(const gs_config* cfg, gs_stepper** out) {
   FAIL_CLEAN(hipStreamCreateWithFlags(&s->s_comp, hipStreamNonBlocking));
   FAIL_CLEAN(hipStreamCreateWithPriority(&s->s_comm, hipStreamNonBlocking, hi));
   FAIL_CLEAN(hipStreamCreateWithFlags(&s->s_rem, hipStreamNonBlocking));
+  FAIL_CLEAN(hipStreamCreateWithFlags(&s->s_rem2, hipStreamNonBlocking));
+  FAIL_CLEAN(hipEventCreateWithFlags(&s->ev_rem2, hipEventDisableTiming));
+  s->ev_recv.assign((size_t)cfg->nranks, nullptr);
+  for (auto& e : s->ev_recv) FAIL_CLEAN(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   FAIL_CLEAN(hipEventCreateWithFlags(&s->ev_remote, hipEventDisableTiming));
   FAIL_CLEAN(hipEventCreateWithFlags(&s->ev_fork, hipEventDisableTiming));
   FAIL_CLEAN(hipEventCreateWithFlags(&s->ev_ready, hipEventDisableTiming));
@@ -460,17 +551,21 @@ int gs_stepper_destroy(gs_stepper* s) {
   if (s->s_comp) (void)hipStreamSynchronize(s->s_comp);
   if (s->s_comm) (void)hipStreamSynchronize(s->s_comm);
   if (s->s_rem) (void)hipStreamSynchronize(s->s_rem);
+  if (s->s_rem2) (void)hipStreamSynchronize(s->s_rem2);
   if (s->graph) (void)hipGraphExecDestroy(s->graph);
   if (s->have_comm) (void)ncclCommDestroy(s->comm);
   for (void* p : {s->X[0], s->X[1], s->vel, s->partial, s->acc, (void*)s->mass_dev,
                   (void*)s->nonfinite})
     if (p) (void)hipFree(p);
   for (hipEvent_t e : {s->ev_ready, s->ev_gathered, s->ev_t0, s->ev_local, s->ev_end,
-                       s->ev_remote, s->ev_fork})
+                       s->ev_remote, s->ev_fork, s->ev_rem2})
     if (e) (void)hipEventDestroy(e);
   if (s->s_comp) (void)hipStreamDestroy(s->s_comp);
   if (s->s_comm) (void)hipStreamDestroy(s->s_comm);
   if (s->s_rem) (void)hipStreamDestroy(s->s_rem);
+  if (s->s_rem2) (void)hipStreamDestroy(s->s_rem2);
+  for (hipEvent_t e : s->ev_recv)
+    if (e) (void)hipEventDestroy(e);
   delete s;
   return 0;
 }
@@ -557,6 +652,7 @@ int gs_stepper_step(gs_stepper* s, int32_t nsteps) {
 int gs_stepper_sync(gs_stepper* s) {
   GS_HIP(hipStreamSynchronize(s->s_comm));
   GS_HIP(hipStreamSynchronize(s->s_rem));
+  GS_HIP(hipStreamSynchronize(s->s_rem2));
   GS_HIP(hipStreamSynchronize(s->s_comp));
   return 0;
 }
@@ -569,6 +665,7 @@ int gs_stepper_wait(gs_stepper* s, double timeout_s) {
   for (;;) {
     hipError_t a = hipStreamQuery(s->s_comp);
     if (a == hipSuccess) a = hipStreamQuery(s->s_rem);
+    if (a == hipSuccess) a = hipStreamQuery(s->s_rem2);
     const hipError_t b = hipStreamQuery(s->s_comm);
     if (a == hipSuccess && b == hipSuccess) return 0;
     if ((a != hipSuccess && a != hipErrorNotReady) || (b != hipSuccess && b != hipErrorNotReady)) {
@@ -667,6 +764,48 @@ int gs_group_step(gs_stepper** sh, int32_t P, int32_t nsteps) {
   for (int32_t it = 0; it < nsteps; ++it) {
     const int cur = (int)(sh[0]->k & 1);
     const bool need = P > 1 && !sh[0]->full[cur];
+    if (need && sh[0]->cfg.strategy == GS_STRATEGY_RING) {
+      // Ring pass with device copies: at sub-step s shard r receives slice (r - s) mod P
+      // from shard r-1 (which holds it since sub-step s-1), on shard 0's comm stream.
+      for (int r = 0; r < P; ++r) GS_HIP(hipEventRecord(sh[r]->ev_ready, sh[r]->s_comp));
+      for (int r = 0; r < P; ++r) GS_HIP(hipStreamWaitEvent(gsm, sh[r]->ev_ready, 0));
+      for (int r = 0; r < P; ++r) {
+        GS_HIP(hipStreamWaitEvent(sh[r]->s_rem, sh[r]->ev_ready, 0));
+        GS_HIP(hipStreamWaitEvent(sh[r]->s_rem2, sh[r]->ev_ready, 0));
+      }
+      for (int r = 0; r < P; ++r) {
+        int rc = sh[r]->esz == 4
+                     ? ring_compute<float>(sh[r], base_args<float>(sh[r], cur), 0, nullptr)
+                     : ring_compute<double>(sh[r], base_args<double>(sh[r], cur), 0, nullptr);
+        if (rc) return -1;
+      }
+      for (int sub = 1; sub < P; ++sub) {
+        for (int r = 0; r < P; ++r) {
+          const int left = (r - 1 + P) % P, src = ring_src(sh[r], sub);
+          GS_HIP(hipMemcpyAsync(static_cast<char*>(sh[r]->X[cur]) + src * slice,
+                                static_cast<char*>(sh[left]->X[cur]) + src * slice, slice,
+                                hipMemcpyDeviceToDevice, gsm));
+        }
+        for (int r = 0; r < P; ++r) GS_HIP(hipEventRecord(sh[r]->ev_recv[sub], gsm));
+        for (int r = 0; r < P; ++r) {
+          int rc = sh[r]->esz == 4
+                       ? ring_compute<float>(sh[r], base_args<float>(sh[r], cur), sub,
+                                             sh[r]->ev_recv[sub])
+                       : ring_compute<double>(sh[r], base_args<double>(sh[r], cur), sub,
+                                              sh[r]->ev_recv[sub]);
+          if (rc) return -1;
+        }
+      }
+      for (int r = 0; r < P; ++r) {
+        int rc = sh[r]->esz == 4 ? ring_finish<float>(sh[r], base_args<float>(sh[r], cur))
+                                 : ring_finish<double>(sh[r], base_args<double>(sh[r], cur));
+        if (rc) return -1;
+        sh[r]->full[cur] = true;
+        sh[r]->full[cur ^ 1] = false;
+        sh[r]->k += 1;
+      }
+      continue;
+    }
     if (need) {
       for (int r = 0; r < P; ++r) GS_HIP(hipEventRecord(sh[r]->ev_ready, sh[r]->s_comp));
       for (int r = 0; r < P; ++r) GS_HIP(hipStreamWaitEvent(gsm, sh[r]->ev_ready, 0));

@@ -38,6 +38,12 @@ enum gs_mode {
 };
 
 // Initial-condition families (models). Same formulas in gravsim/models/initial_conditions.py.
+// Multi-rank exchange strategies.
+enum gs_strategy {
+  GS_STRATEGY_ALLGATHER = 0,  // one in-place ncclAllGather, overlapped with the local chunks
+  GS_STRATEGY_RING = 1,       // P-1 neighbour ncclSend/ncclRecv, each slice computed on arrival
+};
+
 enum gs_ic {
   GS_IC_SOLAR_RANDOM = 0,  // Sun/Earth/Mars + uniform cube bodies (cuda.cu:81-96,129-131)
   GS_IC_RANDOM = 1,        // uniform cube bodies only
@@ -56,6 +62,7 @@ typedef struct gs_config {
   int32_t use_graph;  // capture the step loop into a hipGraph and replay it
   int32_t split_groups;  // SPLIT mode: chunk groups per i-block (0 = auto)
   int32_t cutoff_mode;   // 0 auto, 1 exact hard cutoff (select), 2 fast (overflow-safe core)
+  int32_t strategy;      // 0 all-gather (default), 1 ring pass (neighbour send/recv, pipelined)
   double dt;          // time step [s]
   double G;           // gravitational constant
   double cutoff;      // hard cutoff radius [m]: zero force below it (mpi.c:64)

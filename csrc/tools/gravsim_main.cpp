@@ -5,6 +5,7 @@
 //   gravsim_bench --n 65536 --steps 100 [--dt 3600] [--dtype fp32|fp64] [--kernel lds|smem]
 //                 [--mode fused|split] [--ipl 2] [--seed S] [--init solar+random|random]
 //                 [--log-dir DIR] [--dump FILE] [--progress-every 100] [--no-graph]
+//                 [--strategy allgather|ring] [--cutoff-mode auto|exact|fast]
 // Multi-GPU (one process per GPU): set RANK / WORLD_SIZE / LOCAL_RANK and pass
 // --rendezvous FILE on a shared filesystem; rank 0 publishes the RCCL unique id there.
 #include <hip/hip_runtime.h>
@@ -70,6 +71,8 @@ Args parse(int argc, char** argv) {
     else if (k == "--rendezvous") a.rendezvous = val();
     else if (k == "--progress-every") a.progress_every = atoi(val());
     else if (k == "--no-graph") a.cfg.use_graph = 0;
+    else if (k == "--strategy") a.cfg.strategy = strcmp(val(), "ring") == 0 ? GS_STRATEGY_RING : GS_STRATEGY_ALLGATHER;
+    else if (k == "--cutoff-mode") { const char* v = val(); a.cfg.cutoff_mode = !strcmp(v, "exact") ? 1 : !strcmp(v, "fast") ? 2 : 0; }
     else if (k == "--help" || k == "-h") {
       printf("usage: gravsim_bench --n N --steps S [--dt DT] [--dtype fp32|fp64] ...\n");
       exit(0);

@@ -42,6 +42,9 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--no-graph", dest="graph", action="store_false")
     p.add_argument("--graph-comm", action="store_true",
                    help="capture the multi-rank step, RCCL all-gather included, in a hipGraph")
+    p.add_argument("--strategy", choices=["allgather", "ring"], default=d.strategy,
+                   help="multi-rank GPU exchange: one all-gather overlapped with the local "
+                        "chunks, or a ring of P-1 neighbour send/recv steps computed on arrival")
     p.add_argument("--threads", type=int, default=0)
     p.add_argument("--log-dir", default=None, help="write the text log under this directory")
     p.add_argument("--log-format", choices=["mpi", "spark", "cuda", "none"], default=d.log_format)
@@ -75,6 +78,7 @@ def config_from_args(a: argparse.Namespace) -> SimConfig:
                      seed=a.seed, G=a.G, cutoff=a.cutoff, softening=a.softening,
                      cutoff_mode=a.cutoff_mode, integrator=a.integrator, kernel=a.kernel,
                      mode=a.mode, ipl=a.ipl, chunk=a.chunk, graph=a.graph, graph_comm=a.graph_comm,
+                     strategy=a.strategy,
                      threads=a.threads,
                      log_dir=a.log_dir, log_format=a.log_format, progress_every=a.progress_every,
                      print_positions=a.print_positions, dump_path=a.dump_path,

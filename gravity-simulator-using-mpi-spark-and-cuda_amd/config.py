@@ -43,6 +43,7 @@ class SimConfig:
     graph: bool = True            # hipGraph replay of the step loop (single rank)
     graph_comm: bool = False      # also capture the multi-rank step (RCCL collective included)
     comm: str = "auto"            # rccl (GPU) | gloo (CPU) | none
+    strategy: str = "allgather"   # multi-rank exchange: allgather | ring (pipelined send/recv)
     threads: int = 0              # CPU engine OpenMP threads (0 = default)
     step_timeout_s: float = 600.0 # multi-rank hang detection: abort RCCL after this wait
     # observability / IO
@@ -84,6 +85,8 @@ class SimConfig:
             raise ValueError("integrator must be kd or leapfrog")
         if self.cutoff_mode not in ("auto", "exact", "fast"):
             raise ValueError("cutoff_mode must be auto, exact or fast")
+        if self.strategy not in ("allgather", "ring"):
+            raise ValueError("strategy must be allgather or ring")
         if self.cutoff < 0 or self.softening < 0:
             raise ValueError("cutoff and softening must be >= 0")
         return self

@@ -32,7 +32,7 @@ class GsConfig(ctypes.Structure):
         ("n", c_int64), ("dtype", c_int32), ("kernel", c_int32), ("mode", c_int32),
         ("ipl", c_int32), ("chunk", c_int32), ("rank", c_int32), ("nranks", c_int32),
         ("device", c_int32), ("use_graph", c_int32), ("split_groups", c_int32),
-        ("cutoff_mode", c_int32), ("dt", c_double), ("G", c_double), ("cutoff", c_double), ("softening", c_double),
+        ("cutoff_mode", c_int32), ("strategy", c_int32), ("dt", c_double), ("G", c_double), ("cutoff", c_double), ("softening", c_double),
     ]
 
 
@@ -51,6 +51,7 @@ GS_FP32, GS_FP64 = 0, 1
 KERNEL_IDS = {"auto": 0, "lds": 1, "smem": 2}
 MODE_IDS = {"auto": 0, "fused": 1, "split": 2}
 CUTOFF_IDS = {"auto": 0, "exact": 1, "fast": 2}
+STRATEGY_IDS = {"allgather": 0, "ring": 1}
 KERNEL_NAMES = {v: k for k, v in KERNEL_IDS.items()}
 MODE_NAMES = {v: k for k, v in MODE_IDS.items()}
 

@@ -31,7 +31,8 @@ def _gs_config(cfg: SimConfig, rank: int, nranks: int, device: int) -> _native.G
         kernel=_native.KERNEL_IDS[cfg.kernel], mode=_native.MODE_IDS[cfg.mode], ipl=cfg.ipl,
         chunk=cfg.chunk, rank=rank, nranks=nranks, device=device,
         use_graph=(2 if cfg.graph_comm else 1) if cfg.graph else 0,
-        split_groups=cfg.split_groups, cutoff_mode=_native.CUTOFF_IDS[cfg.cutoff_mode], dt=cfg.dt,
+        split_groups=cfg.split_groups, cutoff_mode=_native.CUTOFF_IDS[cfg.cutoff_mode],
+        strategy=_native.STRATEGY_IDS[cfg.strategy], dt=cfg.dt,
         G=cfg.G, cutoff=cfg.cutoff, softening=cfg.softening)
 
 

@@ -154,6 +154,27 @@ def test_virtual_ranks_bitwise(hip, P, mode):
     assert np.array_equal(got.vel, ref.vel)
 
 
+@pytest.mark.parametrize("P,dtype", [(2, "fp32"), (3, "fp64"), (5, "fp32")])
+def test_virtual_ranks_ring_bitwise(hip, P, dtype):
+    """Ring pass (P-1 neighbour transfers, each slice computed on arrival on alternating
+    streams) over P virtual shards == the 1-rank all-gather run, bitwise."""
+    from gravsim.runtime.engines import VirtualGroup
+
+    cfg = SimConfig(n=5000, dtype=dtype, device="gpu", chunk=1024, strategy="ring")
+    g = VirtualGroup(cfg, P)
+    g.init_ics("solar+random", 9)
+    g.step(5)
+    got = g.state()
+    g.close()
+    one = VirtualGroup(cfg.replace(strategy="allgather"), 1)
+    one.init_ics("solar+random", 9)
+    one.step(5)
+    ref = one.state()
+    one.close()
+    assert np.array_equal(got.pos, ref.pos)
+    assert np.array_equal(got.vel, ref.vel)
+
+
 def test_fp32_no_overflow_heavy_masses(hip):
     """D1: G*m_i*m_j overflows fp32 in the reference; mu = G*m per body does not."""
     rng = np.random.default_rng(0)

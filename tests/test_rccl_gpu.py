@@ -22,7 +22,7 @@ def _port():
     return p
 
 
-def _worker(rank, world, port, out_dir, n, steps):
+def _worker(rank, world, port, out_dir, n, steps, strategy="allgather"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK="0")
     import gravsim  # noqa: F401
@@ -33,7 +33,8 @@ def _worker(rank, world, port, out_dir, n, steps):
     dist = comm.init(timeout_s=120)
     status = "ok"
     try:
-        cfg = SimConfig(n=n, dtype="fp32", device="gpu", chunk=1024, step_timeout_s=120)
+        cfg = SimConfig(n=n, dtype="fp32", device="gpu", chunk=1024, step_timeout_s=120,
+                        strategy=strategy)
         eng = HipEngine(cfg, rank, world, device=0, dist=dist)
         uid = HipEngine.unique_id() if rank == 0 else None
         uid = comm.broadcast_bytes(dist, uid)
@@ -57,9 +58,10 @@ def _worker(rank, world, port, out_dir, n, steps):
         comm.shutdown(dist)
 
 
-def test_rccl_two_ranks_match_single_rank(hip, tmp_path):
+@pytest.mark.parametrize("strategy", ["allgather", "ring"])
+def test_rccl_two_ranks_match_single_rank(hip, tmp_path, strategy):
     n, steps = 5000, 6
-    mp.start_processes(_worker, args=(2, _port(), str(tmp_path), n, steps), nprocs=2,
+    mp.start_processes(_worker, args=(2, _port(), str(tmp_path), n, steps, strategy), nprocs=2,
                        start_method="spawn", join=True)
     status = open(tmp_path / "status.txt").read()
     if status != "ok":
@@ -75,8 +77,9 @@ def test_rccl_two_ranks_match_single_rank(hip, tmp_path):
     assert np.array_equal(np.load(tmp_path / "pos.npy"), ref)
 
 
-@pytest.mark.parametrize("graph", [1, 2])
-def test_rccl_one_rank_full_schedule_bitwise(hip, monkeypatch, graph):
+@pytest.mark.parametrize("graph,strategy", [(1, "allgather"), (2, "allgather"), (1, "ring"),
+                                            (2, "ring")])
+def test_rccl_one_rank_full_schedule_bitwise(hip, monkeypatch, graph, strategy):
     """A live 1-rank RCCL communicator drives the whole multi-rank step (in-place
     ncclAllGather, concurrent local/remote split, ordered reduce) — eagerly and captured into
     a hipGraph (use_graph=2 captures the collective) — and must match the plain path."""
@@ -84,7 +87,7 @@ def test_rccl_one_rank_full_schedule_bitwise(hip, monkeypatch, graph):
     from gravsim.runtime.engines import HipEngine
 
     monkeypatch.setenv("GRAVSIM_FORCE_COMM", "1")
-    cfg = SimConfig(n=6000, dtype="fp32", device="gpu", chunk=1024)
+    cfg = SimConfig(n=6000, dtype="fp32", device="gpu", chunk=1024, strategy=strategy)
     eng = HipEngine(cfg)
     eng.lib.gs_stepper_destroy(eng._s)  # rebuild with the requested graph mode
     import ctypes
