@@ -95,6 +95,34 @@ __device__ __forceinline__ void interact(T xi, T yi, T zi, T xj, T yj, T zj, T m
   if constexpr (FM == FM_PHI) ph += mi;
 }
 
+#ifndef GS_NO_EXPLICIT_PK
+// fp32, pairs of i per lane as 2-vectors: every op but the rsq is one v_pk_* for two
+// interactions, and the j scalar is broadcast by op_sel instead of SGPR-pair copies. Each
+// element sees exactly the scalar interact() arithmetic, so results are bit-identical.
+using f2 = float __attribute__((ext_vector_type(2)));
+
+template <int FM>
+__device__ __forceinline__ void interact_pk(f2 xi, f2 yi, f2 zi, float xj, float yj, float zj,
+                                            float muj, float cut2, float eps2, f2& ax, f2& ay,
+                                            f2& az) {
+  const f2 dx = f2(xj) - xi, dy = f2(yj) - yi, dz = f2(zj) - zi;
+  const f2 r2 = __builtin_elementwise_fma(
+      dz, dz, __builtin_elementwise_fma(dy, dy, __builtin_elementwise_fma(dx, dx, f2(eps2))));
+  f2 inv;
+  inv.x = rsqrt_dev(r2.x);
+  inv.y = rsqrt_dev(r2.y);
+  if constexpr (FM == FM_EXACT) {
+    inv.x = r2.x >= cut2 ? inv.x : 0.0f;
+    inv.y = r2.y >= cut2 ? inv.y : 0.0f;
+  }
+  const f2 mi = f2(muj) * inv;
+  const f2 s = mi * (inv * inv);
+  ax = __builtin_elementwise_fma(s, dx, ax);
+  ay = __builtin_elementwise_fma(s, dy, ay);
+  az = __builtin_elementwise_fma(s, dz, az);
+}
+#endif
+
 template <typename T, int IPL>
 struct IState {
   T x[IPL], y[IPL], z[IPL], mu[IPL];
@@ -110,11 +138,26 @@ __device__ __forceinline__ void zero_chunk(IState<T, IPL>& s) {
 
 template <typename T, int IPL, int FM>
 __device__ __forceinline__ void interact_all(IState<T, IPL>& s, const V4<T>& q, T cut2, T eps2) {
+#ifndef GS_NO_EXPLICIT_PK
+  if constexpr (sizeof(T) == 4 && IPL % 2 == 0 && FM != FM_PHI) {
+#pragma unroll
+    for (int k = 0; k < IPL; k += 2) {
+      f2 ax = {s.ax[k], s.ax[k + 1]}, ay = {s.ay[k], s.ay[k + 1]}, az = {s.az[k], s.az[k + 1]};
+      interact_pk<FM>(f2{s.x[k], s.x[k + 1]}, f2{s.y[k], s.y[k + 1]}, f2{s.z[k], s.z[k + 1]},
+                      q.x, q.y, q.z, q.w, cut2, eps2, ax, ay, az);
+      s.ax[k] = ax.x; s.ax[k + 1] = ax.y;
+      s.ay[k] = ay.x; s.ay[k + 1] = ay.y;
+      s.az[k] = az.x; s.az[k + 1] = az.y;
+    }
+    return;
+  }
+#endif
 #pragma unroll
   for (int k = 0; k < IPL; ++k)
     interact<T, FM>(s.x[k], s.y[k], s.z[k], q.x, q.y, q.z, q.w, cut2, eps2, s.ax[k], s.ay[k],
                      s.az[k], s.ph[k]);
 }
+
 
 // LDS tile geometry: kTileBytes per tile buffer (default 4 KiB = 256 fp32 / 128 fp64 bodies),
 // double-buffered. Each wave-instruction of the fill moves one 1-KiB piece.
@@ -202,6 +245,14 @@ __device__ __forceinline__ void sweep_smem(const V4<T>* __restrict__ X, int64_t 
     // Software pipeline: the next 4 j-bodies (one s_load_dwordx16 for fp32) are requested
     // before the current 4 are consumed, so scalar-cache / L2 latency overlaps the VALU work.
     V4<T> q0 = p[0], q1 = p[1], q2 = p[2], q3 = p[3];
+    // Scalar loads return out of order, so any wait is lgkmcnt(0). Drain the first batch
+    // here; otherwise the wait for it lands inside the loop after the next prefetch is
+    // issued and stalls on that prefetch every iteration.
+#ifndef GS_SMEM_NO_DRAIN
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+    __builtin_amdgcn_sched_barrier(0);
+#endif
     for (int64_t j = 4; j < chunk; j += 4) {
       const V4<T> n0 = p[j], n1 = p[j + 1], n2 = p[j + 2], n3 = p[j + 3];
       __builtin_amdgcn_sched_barrier(0);  // keep the loads at the top of the iteration
