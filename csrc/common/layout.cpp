@@ -40,15 +40,19 @@ extern "C" int gs_layout_compute(const gs_config* cfg, gs_layout* out) {
   out->n_local = out->n_pad / cfg->nranks;
   out->local_begin = (int64_t)cfg->rank * out->n_local;
   out->n_chunks = (int32_t)((cfg->n + chunk - 1) / chunk);
-  // j source: SGPR streaming through the scalar cache wins at >= 128K bodies per rank (no
-  // LDS barrier per tile); LDS-DMA tiles below that. i-bodies per lane: 4 for SGPR streaming
-  // and fp64, 8 for fp32 LDS tiles. Measured on MI355X: profiles/r1_rank_shape_v2.log,
-  // r1_sweep_64k_v2.log, r1_sweep_256k.log, r1_sweep_512k_fp64_halley.log.
+  // j source and i-bodies per lane, from in-process sweeps on MI355X with the explicit
+  // 2-vector fp32 loop (profiles/r1_tune2_*.log):
+  //  * fp32: SGPR streaming through the scalar cache at every size (no LDS barrier per tile;
+  //    1M: 239.4 vs 252.1 ms, 64K: 1.09 vs 1.12 ms). IPL 8 at >= 256K bodies per rank,
+  //    4 below (64K: IPL 8 leaves too few workgroups).
+  //  * fp64: SGPR streaming at >= 128K per rank, LDS tiles below; IPL 2 (512K: 190.9 ms,
+  //    IPL 4 192.3 ms).
+  const bool f32 = cfg->dtype == GS_FP32;
   out->kernel = cfg->kernel != GS_KERNEL_AUTO ? cfg->kernel
-                : (out->n_local >= 131072 ? GS_KERNEL_SMEM : GS_KERNEL_LDS);
+                : (f32 || out->n_local >= 131072 ? GS_KERNEL_SMEM : GS_KERNEL_LDS);
   int32_t ipl = cfg->ipl;
   if (ipl <= 0) {
-    ipl = (cfg->dtype == GS_FP32 && out->kernel == GS_KERNEL_LDS) ? 8 : 4;
+    ipl = f32 ? (out->n_local >= 262144 ? 8 : 4) : 2;
     while (ipl > 1 && out->n_local % (256 * ipl) != 0) ipl /= 2;
   }
   if (ipl != 1 && ipl != 2 && ipl != 4 && !(ipl == 8 && cfg->dtype == GS_FP32)) {
