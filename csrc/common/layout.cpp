@@ -50,7 +50,14 @@ extern "C" int gs_layout_compute(const gs_config* cfg, gs_layout* out) {
   const bool f32 = cfg->dtype == GS_FP32;
   out->kernel = cfg->kernel != GS_KERNEL_AUTO ? cfg->kernel
                 : (f32 || out->n_local >= 131072 ? GS_KERNEL_SMEM : GS_KERNEL_LDS);
-  int32_t ipl = cfg->ipl;
+  if (out->kernel == GS_KERNEL_MFMA) {
+    // Experimental MFMA variant: fp32, 256 i-bodies per workgroup, split schedule only.
+    if (cfg->dtype != GS_FP32 || (cfg->ipl > 1) || cfg->mode == GS_MODE_FUSED) {
+      gs_set_error("layout: the mfma kernel is fp32, ipl 1, split schedule only");
+      return -1;
+    }
+  }
+  int32_t ipl = out->kernel == GS_KERNEL_MFMA ? 1 : cfg->ipl;
   if (ipl <= 0) {
     ipl = f32 ? (out->n_local >= 262144 ? 8 : 4) : 2;
     while (ipl > 1 && out->n_local % (256 * ipl) != 0) ipl /= 2;
@@ -66,6 +73,7 @@ extern "C" int gs_layout_compute(const gs_config* cfg, gs_layout* out) {
   out->ipl = ipl;
   const int64_t i_blocks = out->n_local / (256 * ipl);
   int32_t mode = cfg->mode;
+  if (out->kernel == GS_KERNEL_MFMA) mode = GS_MODE_SPLIT;
   if (mode == GS_MODE_AUTO) {
     // Fused needs enough i-blocks to fill 256 CUs at >= 8 workgroups of 4 waves each;
     // otherwise split j over workgroups (deterministic per-chunk partials).

@@ -516,11 +516,21 @@ hipError_t launch_force_split(const KArgs<T>& a, int kernel, int ipl, int groups
   if (span <= 0) return hipSuccess;
   if (groups < 1) groups = 1;
   if (groups > span) groups = span;
+  if (kernel == GS_KERNEL_MFMA) {
+    if constexpr (sizeof(T) == 4) {
+      // The MFMA variant does not form the potential sum: accel queries (phi) use the
+      // SGPR-streaming VALU kernel on the same chunk range.
+      if (!a.phi) return launch_force_mfma(a, groups, s);
+      return dispatch<T>(a, GS_KERNEL_SMEM, ipl, false, groups, s);
+    }
+    return hipErrorInvalidValue;
+  }
   return dispatch<T>(a, kernel, ipl, false, groups, s);
 }
 
 template <typename T>
 hipError_t launch_force_fused(const KArgs<T>& a, int kernel, int ipl, hipStream_t s) {
+  if (kernel == GS_KERNEL_MFMA) return hipErrorInvalidValue;  // split schedule only
   return dispatch<T>(a, kernel, ipl, true, 1, s);
 }
 
@@ -570,6 +580,11 @@ static int occ_t(int fm) {
 
 template <typename T>
 int split_occupancy(int kernel, int ipl, int fm) {
+  if (kernel == GS_KERNEL_MFMA) {
+    if (sizeof(T) != 4) return 0;
+    if (fm != FM_PHI) return mfma_occupancy(fm);
+    kernel = GS_KERNEL_SMEM;
+  }
   const bool smem = kernel == GS_KERNEL_SMEM;
   switch (ipl) {
     case 1: return smem ? occ_t<T, 1, GS_KERNEL_SMEM>(fm) : occ_t<T, 1, GS_KERNEL_LDS>(fm);

@@ -444,7 +444,7 @@ int download_state(gs_stepper* s, double* pos, double* vel, double* mass) {
 }
 
 template <typename T>
-int accel_impl(gs_stepper* s, double* acc4) {
+int accel_impl(gs_stepper* s, double* acc4, bool step_path) {
   const int cur = (int)(s->k & 1);
   if (s->virt && !s->full[cur]) {
     gs_set_error("accel: virtual-rank shard is not gathered (use the group API)");
@@ -453,12 +453,14 @@ int accel_impl(gs_stepper* s, double* acc4) {
   if (gather(s, cur)) return -1;
   if (s->have_comm) GS_HIP(hipStreamWaitEvent(s->s_comp, s->ev_gathered, 0));
   gs::KArgs<T> a = base_args<T>(s, cur);
-  a.phi = 1;
-  a.exact = 1;
-  a.eps2 = (T)(s->cfg.softening * s->cfg.softening);
+  if (!step_path) {  // diagnostics: exact cutoff + potential
+    a.phi = 1;
+    a.exact = 1;
+    a.eps2 = (T)(s->cfg.softening * s->cfg.softening);
+  }
   a.acc_out = static_cast<T*>(s->acc);
-  GS_HIP(gs::launch_force_split<T>(a, s->L.kernel, s->L.ipl, choose_groups(s, s->L.n_chunks, true),
-                                   s->s_comp));
+  GS_HIP(gs::launch_force_split<T>(a, s->L.kernel, s->L.ipl,
+                                   choose_groups(s, s->L.n_chunks, !step_path), s->s_comp));
   GS_HIP(gs::launch_reduce_integrate<T>(a, s->s_comp));
   GS_HIP(hipStreamSynchronize(s->s_comp));
   std::vector<T> A((size_t)s->L.n_local * 4);
@@ -693,7 +695,12 @@ int gs_stepper_wait(gs_stepper* s, double timeout_s) {
 
 int gs_stepper_accel(gs_stepper* s, double* acc4) {
   GS_HIP(hipSetDevice(s->cfg.device));
-  return s->esz == 4 ? accel_impl<float>(s, acc4) : accel_impl<double>(s, acc4);
+  return s->esz == 4 ? accel_impl<float>(s, acc4, false) : accel_impl<double>(s, acc4, false);
+}
+
+int gs_stepper_accel_step_path(gs_stepper* s, double* acc4) {
+  GS_HIP(hipSetDevice(s->cfg.device));
+  return s->esz == 4 ? accel_impl<float>(s, acc4, true) : accel_impl<double>(s, acc4, true);
 }
 
 int64_t gs_stepper_count_nonfinite(gs_stepper* s) {

@@ -28,6 +28,7 @@ enum gs_kernel {
   GS_KERNEL_AUTO = 0,
   GS_KERNEL_LDS = 1,   // j-tiles staged into LDS by global_load_lds (LDS-DMA), broadcast ds_read_b128
   GS_KERNEL_SMEM = 2,  // wave-uniform j read through the scalar cache into SGPRs (s_load_dwordx16)
+  GS_KERNEL_MFMA = 3,  // experimental fp32: r^2 as a 16x16x4 f32 MFMA GEMM, re-centred tiles
 };
 
 // Step schedule.
@@ -128,6 +129,9 @@ int gs_stepper_sync(gs_stepper* s);
 int gs_stepper_wait(gs_stepper* s, double timeout_s);
 // Accelerations (+potential) of this rank's bodies for the current positions: acc4 = n_local*4.
 int gs_stepper_accel(gs_stepper* s, double* acc4);
+// Accelerations through the step's own force path (configured kernel and cutoff mode, no
+// potential): what the integrator sees. acc4[:, 3] is 0.
+int gs_stepper_accel_step_path(gs_stepper* s, double* acc4);
 // Non-finite guard: returns number of non-finite position/velocity components on this rank.
 int64_t gs_stepper_count_nonfinite(gs_stepper* s);
 int64_t gs_stepper_steps_done(gs_stepper* s);

@@ -42,6 +42,9 @@ hipError_t launch_force_fused(const KArgs<T>& a, int kernel, int ipl, hipStream_
 // Resident workgroups per CU of the split kernel (fm: 0 fast, 1 exact, 2 exact+phi).
 template <typename T>
 int split_occupancy(int kernel, int ipl, int fm);
+// Experimental MFMA-assisted fp32 split kernel (nbody_mfma.hip); no potential sum.
+hipError_t launch_force_mfma(const KArgs<float>& a, int groups, hipStream_t s);
+int mfma_occupancy(int fm);
 template <typename T>
 hipError_t launch_reduce_integrate(const KArgs<T>& a, hipStream_t s);
 template <typename T>

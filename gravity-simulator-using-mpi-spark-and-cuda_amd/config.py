@@ -15,7 +15,7 @@ G_SI = 6.67430e-11  # cuda.cu:11, mpi.c:9, pyspark.py:46
 
 DTYPES = ("fp32", "fp64")
 DEVICES = ("auto", "cpu", "gpu")
-KERNELS = ("auto", "lds", "smem")
+KERNELS = ("auto", "lds", "smem", "mfma")
 MODES = ("auto", "fused", "split")
 COMMS = ("auto", "rccl", "gloo", "none")
 LOG_FORMATS = ("mpi", "spark", "cuda", "none")
@@ -77,6 +77,9 @@ class SimConfig:
             raise ValueError(f"comm must be one of {COMMS}")
         if self.log_format not in LOG_FORMATS:
             raise ValueError(f"log_format must be one of {LOG_FORMATS}")
+        if self.kernel == "mfma" and (self.dtype != "fp32" or self.ipl > 1 or
+                                      self.mode == "fused"):
+            raise ValueError("kernel mfma is fp32, ipl 0/1, split schedule only")
         if self.ipl not in (0, 1, 2, 4, 8) or (self.ipl == 8 and self.dtype != "fp32"):
             raise ValueError("ipl must be 0, 1, 2, 4 (or 8 for fp32)")
         if self.chunk and self.chunk % 1024:

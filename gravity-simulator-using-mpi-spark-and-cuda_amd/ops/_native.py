@@ -48,7 +48,7 @@ class GsLayout(ctypes.Structure):
 
 
 GS_FP32, GS_FP64 = 0, 1
-KERNEL_IDS = {"auto": 0, "lds": 1, "smem": 2}
+KERNEL_IDS = {"auto": 0, "lds": 1, "smem": 2, "mfma": 3}
 MODE_IDS = {"auto": 0, "fused": 1, "split": 2}
 CUTOFF_IDS = {"auto": 0, "exact": 1, "fast": 2}
 STRATEGY_IDS = {"allgather": 0, "ring": 1}
@@ -138,6 +138,7 @@ def hip_lib():
         _sig(lib, "gs_stepper_sync", c_int32, [S])
         _sig(lib, "gs_stepper_wait", c_int32, [S, c_double])
         _sig(lib, "gs_stepper_accel", c_int32, [S, _PD])
+        _sig(lib, "gs_stepper_accel_step_path", c_int32, [S, _PD])
         _sig(lib, "gs_stepper_count_nonfinite", c_int64, [S])
         _sig(lib, "gs_stepper_steps_done", c_int64, [S])
         _sig(lib, "gs_stepper_phase_ms", c_int32, [S, _PF, _PF, _PF])

@@ -125,10 +125,13 @@ class HipEngine:
             self._s, _native.dptr(pos), _native.dptr(vel), _native.dptr(mass)), "get_state")
         return BodySet(pos, vel, mass)
 
-    def accel(self) -> np.ndarray:
-        """(n_local, 4) = (ax, ay, az, phi) of this rank's rows (ghost rows included)."""
+    def accel(self, step_path: bool = False) -> np.ndarray:
+        """(n_local, 4) = (ax, ay, az, phi) of this rank's rows (ghost rows included).
+        step_path=True evaluates the integrator's own force path (configured kernel and
+        cutoff mode; phi column 0) instead of the exact-cutoff diagnostic path."""
         out = np.zeros((self.layout.n_local, 4))
-        _native.check(self.lib, self.lib.gs_stepper_accel(self._s, _native.dptr(out)), "accel")
+        fn = self.lib.gs_stepper_accel_step_path if step_path else self.lib.gs_stepper_accel
+        _native.check(self.lib, fn(self._s, _native.dptr(out)), "accel")
         return out
 
     def nonfinite(self) -> int:

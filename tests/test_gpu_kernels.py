@@ -248,3 +248,53 @@ def test_fast_path_self_term_zero_with_coincident_bodies(hip):
     x, v, _ = oracle.simulate(pos, np.zeros((3, 3)), mass, 3600.0, 1)
     assert np.isfinite(got.pos).all()
     assert np.allclose(got.vel, v, rtol=1e-5, atol=1e-12)
+
+
+def _clustered(n, seed=5, center=(3.0e11, 2.0e11, -1.0e11), radius=1.0e9):
+    rng = np.random.default_rng(seed)
+    d = rng.normal(size=(n, 3))
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    pos = np.asarray(center) + d * (radius * rng.random(n) ** (1 / 3))[:, None]
+    return BodySet(pos, np.zeros((n, 3)), 10 ** rng.uniform(22, 24, n))
+
+
+@pytest.mark.parametrize("ics", ["clustered", "solar+random"])
+def test_mfma_variant_vs_oracle(hip, ics):
+    """Experimental MFMA kernel (r^2 as a 16x16x4 f32 GEMM on re-centred coordinates) vs the
+    fp64 oracle: a cluster 1e9 m wide, 3.7e11 m from the origin, would cancel completely
+    without re-centring (|x|^2 ~ 1e23 m^2 vs r^2 ~ 1e16). Bounds are from the measured
+    errors in profiles/r1_mfma_probe.jsonl, with margin; the VALU kernel is far tighter."""
+    from gravsim.config import G_SI
+    from gravsim.runtime.engines import HipEngine
+
+    b = _clustered(4096) if ics == "clustered" else ic.solar_random(4096, 3)
+    p = b.pos.astype(np.float32).astype(np.float64)
+    mu = (G_SI * b.mass).astype(np.float32).astype(np.float64)
+    ref = oracle.accelerations(p, mu, G=1.0)
+    e = HipEngine(SimConfig(n=b.n, dtype="fp32", device="gpu", kernel="mfma"))
+    assert e.native_layout["kernel"] == 3 and e.native_layout["mode"] == 2
+    e.load(b)
+    a = e.accel(step_path=True)[: b.n, :3]
+    e.close()
+    rel = np.linalg.norm(a - ref, axis=1) / np.linalg.norm(ref, axis=1)
+    assert np.isfinite(a).all()
+    assert np.median(rel) < 2e-5
+    assert np.linalg.norm(a - ref) / np.linalg.norm(ref) < 1e-2
+
+
+def test_mfma_variant_deterministic_and_rank_count_independent(hip):
+    """Same i-blocks and re-centring origin for every P: P virtual shards == 1 rank, bitwise,
+    and two runs agree (fixed in-lane order + fixed xor butterfly, no atomics)."""
+    from gravsim.runtime.engines import VirtualGroup
+
+    cfg = SimConfig(n=6000, dtype="fp32", device="gpu", chunk=1024, kernel="mfma")
+    outs = []
+    for P in (1, 3, 1):
+        g = VirtualGroup(cfg, P)
+        g.init_ics("solar+random", 2)
+        g.step(4)
+        outs.append(g.state())
+        g.close()
+    for o in outs[1:]:
+        assert np.array_equal(o.pos, outs[0].pos) and np.array_equal(o.vel, outs[0].vel)
+    assert np.isfinite(outs[0].pos).all()

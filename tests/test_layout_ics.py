@@ -98,3 +98,12 @@ def test_plummer_virial_ratio():
     b = ic.plummer(2000, 4)
     ratio = 2 * kinetic_energy(b.vel, b.mass) / -potential_energy(b.pos, b.mass)
     assert 0.8 < ratio < 1.2
+
+
+def test_mfma_kernel_config_validation():
+    from gravsim.config import SimConfig
+
+    SimConfig(n=1024, dtype="fp32", kernel="mfma").validate()
+    for bad in (dict(dtype="fp64"), dict(dtype="fp32", ipl=4), dict(dtype="fp32", mode="fused")):
+        with pytest.raises(ValueError):
+            SimConfig(n=1024, kernel="mfma", **bad).validate()
