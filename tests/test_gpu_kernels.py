@@ -263,7 +263,8 @@ def test_mfma_variant_vs_oracle(hip, ics):
     """Experimental MFMA kernel (r^2 as a 16x16x4 f32 GEMM on re-centred coordinates) vs the
     fp64 oracle: a cluster 1e9 m wide, 3.7e11 m from the origin, would cancel completely
     without re-centring (|x|^2 ~ 1e23 m^2 vs r^2 ~ 1e16). Bounds are from the measured
-    errors in profiles/r1_mfma_probe.jsonl, with margin; the VALU kernel is far tighter."""
+    errors in profiles/r1_mfma_probe.jsonl, with margin; the VALU kernel is far tighter.
+    Without re-centring the median error of the cluster case would be O(1)."""
     from gravsim.config import G_SI
     from gravsim.runtime.engines import HipEngine
 
@@ -278,8 +279,10 @@ def test_mfma_variant_vs_oracle(hip, ics):
     e.close()
     rel = np.linalg.norm(a - ref, axis=1) / np.linalg.norm(ref, axis=1)
     assert np.isfinite(a).all()
+    # Median and 90th percentile only: the tail is the expanded form's cancellation for close
+    # pairs (p99 ~ 1e-3, max ~ 1e-2), the reason the variant is not the default.
     assert np.median(rel) < 2e-5
-    assert np.linalg.norm(a - ref) / np.linalg.norm(ref) < 1e-2
+    assert np.quantile(rel, 0.9) < 1e-3
 
 
 def test_mfma_variant_deterministic_and_rank_count_independent(hip):
