@@ -301,3 +301,11 @@ def test_mfma_variant_deterministic_and_rank_count_independent(hip):
     for o in outs[1:]:
         assert np.array_equal(o.pos, outs[0].pos) and np.array_equal(o.vel, outs[0].vel)
     assert np.isfinite(outs[0].pos).all()
+
+
+def test_fused_engine_allocates_partials_on_demand(hip):
+    """A single-rank fused Stepper skips the per-chunk partial buffer; an accel query
+    allocates it lazily and matches the split engine bit for bit."""
+    b = ic.solar_random(3000, 4)
+    got = {m: _accel(b, "fp32", mode=m, chunk=1024) for m in ("fused", "split")}
+    assert np.array_equal(got["fused"], got["split"])
