@@ -18,7 +18,9 @@ def build_parser() -> argparse.ArgumentParser:
     d = SimConfig()
     p = argparse.ArgumentParser(prog="gravsim", description="MI355X-native direct-sum N-body "
                                 "gravity simulator (Sun/Earth/Mars + random bodies by default)")
-    p.add_argument("--n", type=int, default=d.n, help="number of bodies")
+    p.add_argument("--n", "--num-bodies", dest="n", type=int, default=d.n,
+                   help="number of bodies (use --num-bodies under torch.distributed.run, "
+                        "whose own options make --n ambiguous)")
     p.add_argument("--dt", type=float, default=d.dt, help="time step [s]")
     p.add_argument("--steps", type=int, default=d.steps, help="number of steps")
     p.add_argument("--dtype", choices=["fp32", "fp64"], default=d.dtype)

@@ -72,3 +72,23 @@ def test_gloo_world3_uneven_and_checkpoint(tmp_path):
     c = ck.load(ck.latest(str(tmp_path)))
     assert c.step == steps
     assert np.array_equal(c.bodies.pos, got["pos"]) and np.array_equal(c.bodies.vel, got["vel"])
+
+
+def test_torchrun_cli_world2_matches_single(tmp_path):
+    """`torch.distributed.run -m gravsim` (the `mpirun -np P ./mpi` equivalent) writes the same
+    mpi.c-format dump as a single-process run."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, OMP_NUM_THREADS="1", PYTHONPATH=root)
+    args = ["-m", "gravsim", "--num-bodies", "700", "--steps", "5", "--device", "cpu", "--quiet"]
+    one = tmp_path / "one.txt"
+    two = tmp_path / "two.txt"
+    subprocess.run([sys.executable, *args, "--dump", str(one)], cwd=root, env=env, check=True,
+                   timeout=300)
+    subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes", "1",
+                    "--nproc-per-node", "2", "--master-addr", "127.0.0.1", "--master-port",
+                    str(_free_port()), *args, "--dump", str(two)], cwd=root, env=env,
+                   check=True, timeout=300)
+    assert one.read_text() == two.read_text() and one.read_text().count("Particle ") == 700
