@@ -67,6 +67,25 @@ def test_accel_matches_oracle(hip, n, dtype, kernel):
         assert_close_sum(got[:, 3], phi, np.abs(phi), dtype)
 
 
+@pytest.mark.parametrize("n", SIZES)
+@pytest.mark.parametrize("dtype", ["fp32", "fp64"])
+@pytest.mark.parametrize("kernel", ["lds", "smem"])
+def test_step_path_accel_matches_oracle(hip, n, dtype, kernel):
+    """The integrator's own force path (fp32: explicit 2-vector loop; fp64: direct r^-3
+    refinement; fast cutoff core) on tile-edge sizes, against the fp64 oracle."""
+    from gravsim.runtime.engines import HipEngine
+
+    b = ic.solar_random(n, seed=3 + n)
+    ref, _, absref = quantized_ref(b.pos, b.mass, dtype)
+    e = HipEngine(SimConfig(n=n, dtype=dtype, device="gpu", kernel=kernel))
+    try:
+        e.load(b)
+        got = e.accel(step_path=True)[:n, :3]
+    finally:
+        e.close()
+    assert_close_sum(got, ref, absref, dtype)
+
+
 @pytest.mark.parametrize("dtype", ["fp32", "fp64"])
 def test_variants_and_schedules_bitwise(hip, dtype):
     """LDS vs SMEM and fused vs split, every ipl: identical bits (canonical chunk order)."""
