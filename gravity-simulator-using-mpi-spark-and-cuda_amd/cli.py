@@ -65,6 +65,9 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--metrics-json", default=None, help="append the run's JSON metrics line here")
     p.add_argument("--sweep", default=None,
                    help="comma-separated N values: run each config in turn (pyspark.py sweep)")
+    p.add_argument("--nproc", "--gpus", dest="nproc", type=int, default=0,
+                   help="launch this many ranks (one per GPU) on this node through "
+                        "torch.distributed.run, like `mpirun -np N` (mpi.c); 0 = as launched")
     p.add_argument("--quiet", action="store_true")
     return p
 
@@ -125,11 +128,48 @@ def run_one(cfg: SimConfig, dist, log, quiet: bool = False, final: bool = True) 
         sim.close()
 
 
+def _launch(nproc: int, argv: list[str]) -> int:
+    """Re-run this CLI as `nproc` ranks under torch.distributed.run in a child process (no
+    exec, nothing has touched the GPU yet); rendezvous on 127.0.0.1."""
+    import os
+    import socket
+    import subprocess
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    rest, skip = [], False
+    for x in argv:  # drop --nproc/--gpus N; torchrun's own options make --n ambiguous
+        if skip:
+            skip = False
+            continue
+        if x in ("--nproc", "--gpus"):
+            skip = True
+            continue
+        if x.startswith(("--nproc=", "--gpus=")):
+            continue
+        rest.append("--num-bodies" if x == "--n" else
+                    "--num-bodies=" + x[4:] if x.startswith("--n=") else x)
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ)
+    env["PYTHONPATH"] = root + (os.pathsep + env["PYTHONPATH"] if env.get("PYTHONPATH") else "")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node",
+           str(nproc), "--master-addr", "127.0.0.1", "--master-port", str(port), "-m",
+           "gravsim", *rest]
+    return subprocess.call(cmd, env=env)
+
+
 def main(argv: Optional[list[str]] = None) -> int:
+    import os
+
     from .parallel import comm
     from .utils.logs import RunLog
 
-    a = build_parser().parse_args(argv)
+    raw = list(sys.argv[1:] if argv is None else argv)
+    a = build_parser().parse_args(raw)
+    if a.nproc > 1 and "WORLD_SIZE" not in os.environ:
+        return _launch(a.nproc, raw)
     cfg = config_from_args(a)
     dist = comm.init()
     try:

@@ -92,3 +92,8 @@ def test_torchrun_cli_world2_matches_single(tmp_path):
                     str(_free_port()), *args, "--dump", str(two)], cwd=root, env=env,
                    check=True, timeout=300)
     assert one.read_text() == two.read_text() and one.read_text().count("Particle ") == 700
+    # `--nproc 3` launches the ranks itself (the `mpirun -np 3` form)
+    three = tmp_path / "three.txt"
+    subprocess.run([sys.executable, *args, "--nproc", "3", "--dump", str(three)], cwd=root,
+                   env=env, check=True, timeout=300)
+    assert three.read_text() == one.read_text()
