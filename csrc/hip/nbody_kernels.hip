@@ -258,7 +258,10 @@ __device__ __forceinline__ void sweep_smem(const V4<T>* __restrict__ X, int64_t 
   for (int v = v0; v < v1; ++v) {
     const int c = seq.chunk(v);
     zero_chunk<T, IPL>(st);
-    const V4<T>* p = X + (int64_t)c * chunk;
+    // Constant address space: the j stream is read-only for the kernel's lifetime, and this
+    // guarantees scalar (s_load) loads even where the compiler cannot prove no-clobber.
+    using CV4 = const __attribute__((address_space(4))) V4<T>;
+    CV4* p = (CV4*)(X + (int64_t)c * chunk);
 #ifdef GS_SMEM_NO_PREFETCH
     for (int64_t j = 0; j < chunk; j += 4) {
 #pragma unroll
