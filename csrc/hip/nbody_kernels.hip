@@ -182,6 +182,13 @@ __device__ __forceinline__ void interact_all(IState<T, IPL>& s, const V4<T>& q, 
 }
 
 
+// Optional occupancy floor for the force kernels (A/B knob): waves per SIMD.
+#ifdef GS_WAVES_PER_EU
+#define GS_WPE __attribute__((amdgpu_waves_per_eu(GS_WAVES_PER_EU)))
+#else
+#define GS_WPE
+#endif
+
 // LDS tile geometry: kTileBytes per tile buffer (default 4 KiB = 256 fp32 / 128 fp64 bodies),
 // double-buffered. Each wave-instruction of the fill moves one 1-KiB piece.
 #ifndef GS_TILE_BYTES
@@ -341,7 +348,7 @@ __device__ __forceinline__ void integrate_store(const KArgs<T>& a, const IState<
 // SPLIT: grid (i_blocks, groups). Workgroup (b, g) sweeps chunks of group g and stores one
 // partial (ax, ay, az, sum mu/r) per chunk: partial[c * n_local + i].
 template <typename T, int IPL, int KV, int FM>
-__global__ __launch_bounds__(kBlock) void force_split_kernel(KArgs<T> a) {
+__global__ __launch_bounds__(kBlock) GS_WPE void force_split_kernel(KArgs<T> a) {
   __shared__ __attribute__((aligned(16))) V4<T> tile[2][Tile<T>::kBodies];
   const int64_t ib = (int64_t)blockIdx.x * (kBlock * IPL);
   const int sb = min(max(a.skip_begin, a.c_begin), a.c_end);
@@ -372,7 +379,7 @@ __global__ __launch_bounds__(kBlock) void force_split_kernel(KArgs<T> a) {
 // FUSED: grid (i_blocks). One workgroup sweeps every chunk in canonical order and integrates
 // in its epilogue (no partial buffer); used when the i-blocks alone fill the GPU.
 template <typename T, int IPL, int KV, int FM>
-__global__ __launch_bounds__(kBlock) void force_fused_kernel(KArgs<T> a) {
+__global__ __launch_bounds__(kBlock) GS_WPE void force_fused_kernel(KArgs<T> a) {
   __shared__ __attribute__((aligned(16))) V4<T> tile[2][Tile<T>::kBodies];
   const int64_t ib = (int64_t)blockIdx.x * (kBlock * IPL);
   IState<T, IPL> st;

@@ -869,7 +869,22 @@ int gs_stepper_comm_init(gs_stepper* s, const void* id128, int32_t rank, int32_t
     s->comm = nullptr;
   }
   if (s->graph) { (void)hipGraphExecDestroy(s->graph); s->graph = nullptr; }
-  // The current buffer is full only if every rank holds identical positions (fresh ICs).
+  if (s->have_comm) {
+    // Warm-up: RCCL builds its transports lazily on the first collective and on the first
+    // send/recv to each peer. Do both here on scratch memory (the accel buffer holds
+    // n_local * 4 >= P elements) so that no timed or captured step pays for it.
+    char* buf = static_cast<char*>(s->acc);
+    const ncclDataType_t dt = s->esz == 4 ? ncclFloat32 : ncclFloat64;
+    GS_NCCL(ncclAllGather(buf + (size_t)rank * s->esz, buf, 1, dt, s->comm, s->s_comm));
+    if (nranks > 1 && s->cfg.strategy == GS_STRATEGY_RING) {
+      GS_NCCL(ncclGroupStart());
+      GS_NCCL(ncclSend(buf, 1, dt, (rank + 1) % nranks, s->comm, s->s_comm));
+      GS_NCCL(ncclRecv(buf + (size_t)nranks * s->esz, 1, dt, (rank - 1 + nranks) % nranks,
+                       s->comm, s->s_comm));
+      GS_NCCL(ncclGroupEnd());
+    }
+    GS_HIP(hipStreamSynchronize(s->s_comm));
+  }
   return 0;
 }
 
