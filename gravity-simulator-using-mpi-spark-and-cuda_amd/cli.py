@@ -56,6 +56,10 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--print-positions", type=int, default=d.print_positions)
     p.add_argument("--dump", dest="dump_path", default=None,
                    help="final state: .txt (mpi.c 'Particle i: (x, y, z)' lines) or .gsck")
+    p.add_argument("--dump-every", type=int, default=0,
+                   help="also write mpi.c-format positions every k steps "
+                        "(<dump stem>_stepNNNNNNNN.txt, or positions_stepNNNNNNNN.txt in "
+                        "--log-dir / the working directory)")
     p.add_argument("--checkpoint-dir", default=None)
     p.add_argument("--checkpoint-every", type=int, default=0)
     p.add_argument("--resume", default=None, help="checkpoint file (or directory: latest)")
@@ -89,6 +93,7 @@ def config_from_args(a: argparse.Namespace) -> SimConfig:
                      threads=a.threads,
                      log_dir=a.log_dir, log_format=a.log_format, progress_every=a.progress_every,
                      print_positions=a.print_positions, dump_path=a.dump_path,
+                     dump_every=a.dump_every,
                      checkpoint_dir=a.checkpoint_dir, checkpoint_every=a.checkpoint_every,
                      resume=resume, record_every=a.record_every, record_path=a.record_path,
                      nan_check_every=a.nan_check_every, metrics_json=a.metrics_json).validate()

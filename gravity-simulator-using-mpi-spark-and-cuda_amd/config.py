@@ -52,6 +52,7 @@ class SimConfig:
     progress_every: int = 100         # "Step s/steps" progress lines (mpi.c:192, cuda.cu:164)
     print_positions: int = 10         # final-position lines on stdout (cuda.cu:101)
     dump_path: Optional[str] = None   # final state dump (text, mpi.c format) or .npz
+    dump_every: int = 0               # also dump positions (mpi.c format) every k steps
     checkpoint_dir: Optional[str] = None
     checkpoint_every: int = 0
     resume: Optional[str] = None

@@ -19,6 +19,7 @@ design:
 """
 from __future__ import annotations
 
+import os
 import time
 from typing import Optional
 
@@ -142,7 +143,8 @@ class Simulation:
         cfg = self.cfg
         steps = cfg.steps if steps is None else int(steps)
         periods = [p for p in (cfg.progress_every if log else 0, cfg.checkpoint_every,
-                               cfg.record_every, cfg.nan_check_every) if p and p > 0]
+                               cfg.record_every, cfg.nan_check_every, cfg.dump_every)
+                   if p and p > 0]
         comm.barrier(self.dist)
         t0 = time.perf_counter()
         s = 0
@@ -158,6 +160,8 @@ class Simulation:
                 self.trajectory.append(self.raw_state().pos.copy())
             if cfg.checkpoint_every and s % cfg.checkpoint_every == 0 and cfg.checkpoint_dir:
                 self.save_checkpoint()
+            if cfg.dump_every and s % cfg.dump_every == 0:
+                self.dump_positions()
         self.engine.sync()
         wall = time.perf_counter() - t0
         wall = comm.allreduce_max(self.dist, wall)
@@ -169,6 +173,27 @@ class Simulation:
                           nranks=self.dist.world, wall_s=wall,
                           kernel=KERNEL_NAMES.get(lay.get("kernel", 0), "cpu"),
                           mode=MODE_NAMES.get(lay.get("mode", 0), "cpu"))
+
+    def dump_path_for(self, step: int) -> str:
+        cfg = self.cfg
+        if cfg.dump_path and not cfg.dump_path.endswith(".gsck"):
+            stem, ext = os.path.splitext(cfg.dump_path)
+            return f"{stem}_step{step:08d}{ext or '.txt'}"
+        return os.path.join(cfg.log_dir or ".", f"positions_step{step:08d}.txt")
+
+    def dump_positions(self, path: Optional[str] = None) -> Optional[str]:
+        """Periodic text dump of all positions in the mpi.c format (mpi.c:249-257);
+        collective, rank 0 writes."""
+        from ..utils.logs import format_positions_mpi
+
+        b = self.raw_state()
+        if not self.dist.is_root:
+            return None
+        path = path or self.dump_path_for(self.step)
+        os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+        with open(path, "w") as f:
+            f.write(format_positions_mpi(b.pos[: self.cfg.n]))
+        return path
 
     def save_trajectory(self, path: str) -> None:
         if self.dist.is_root and self.trajectory:

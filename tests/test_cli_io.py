@@ -155,3 +155,15 @@ def test_config_validation():
 def test_cli_model_families(fam, capsys):
     assert main(["--n", "64", "--steps", "3", "--device", "cpu", "--init", fam, "--log-format",
                  "none"]) == 0
+
+
+def test_dump_every_writes_periodic_mpi_dumps(tmp_path, capsys):
+    from gravsim.utils.logs import format_positions_mpi
+
+    final = tmp_path / "pos.txt"
+    assert main(["--n", "50", "--steps", "6", "--device", "cpu", "--dump", str(final),
+                 "--dump-every", "3", "--quiet"]) == 0
+    d3, d6 = tmp_path / "pos_step00000003.txt", tmp_path / "pos_step00000006.txt"
+    assert d3.exists() and d6.exists()
+    assert d6.read_text() == final.read_text() and d3.read_text() != d6.read_text()
+    assert d3.read_text().count("Particle ") == 50
