@@ -487,8 +487,9 @@ int gs_hip_device_count(void) {
 }
 
 const char* gs_hip_kernel_info(void) {
-  return "gfx950 direct-sum: LDS-DMA tiles (global_load_lds_dwordx4) | SGPR scalar-cache j; "
-         "fused KD epilogue; canonical chunk order; RCCL in-place all-gather";
+  return "gfx950 direct-sum: packed-fp32 SGPR j-stream (s_load_dwordx16) | LDS-DMA tiles "
+         "(global_load_lds_dwordx4) | experimental MFMA r^2; fused KD epilogue; canonical "
+         "chunk order; RCCL in-place all-gather or ring send/recv";
 }
 
 int gs_stepper_create(const gs_config* cfg, gs_stepper** out) {
