@@ -60,18 +60,18 @@ extern "C" int gs_layout_compute(const gs_config* cfg, gs_layout* out) {
   int32_t ipl = out->kernel == GS_KERNEL_MFMA ? 1 : cfg->ipl;
   if (ipl <= 0) {
     ipl = f32 ? (out->n_local >= 262144 ? 8 : 4) : 2;
-    while (ipl > 1 && out->n_local % (256 * ipl) != 0) ipl /= 2;
+    while (ipl > 1 && out->n_local % (GS_BLOCK * ipl) != 0) ipl /= 2;
   }
   if (ipl != 1 && ipl != 2 && ipl != 4 && !(ipl == 8 && cfg->dtype == GS_FP32)) {
     gs_set_error("layout: ipl must be 1, 2, 4 (or 8 for fp32)");
     return -1;
   }
-  if ((out->n_local % (256 * ipl)) != 0) {
-    gs_set_error("layout: 256*ipl must divide the per-rank body count (raise chunk)");
+  if ((out->n_local % (GS_BLOCK * ipl)) != 0) {
+    gs_set_error("layout: block*ipl must divide the per-rank body count (raise chunk)");
     return -1;
   }
   out->ipl = ipl;
-  const int64_t i_blocks = out->n_local / (256 * ipl);
+  const int64_t i_blocks = out->n_local / (GS_BLOCK * ipl);
   int32_t mode = cfg->mode;
   if (out->kernel == GS_KERNEL_MFMA) mode = GS_MODE_SPLIT;
   if (mode == GS_MODE_AUTO) {

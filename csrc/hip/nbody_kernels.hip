@@ -33,7 +33,7 @@ template <> struct VecT<float> { using type = float __attribute__((ext_vector_ty
 template <> struct VecT<double> { using type = double __attribute__((ext_vector_type(4))); };
 template <typename T> using V4 = typename VecT<T>::type;
 
-constexpr int kBlock = 256;  // 4 waves of 64
+constexpr int kBlock = GS_BLOCK;  // default 256 = 4 waves of 64
 
 __device__ __forceinline__ float rsqrt_dev(float x) { return __builtin_amdgcn_rsqf(x); }
 
@@ -195,19 +195,21 @@ __device__ __forceinline__ void interact_all(IState<T, IPL>& s, const V4<T>& q, 
 #define GS_TILE_BYTES 4096
 #endif
 constexpr int kTileBytes = GS_TILE_BYTES;
-static_assert(kTileBytes % 4096 == 0, "tile must be whole 4-wave x 1 KiB rounds");
+static_assert(kTileBytes % 1024 == 0, "tile must be whole 1 KiB wave pieces");
 template <typename T> struct Tile { static constexpr int kBodies = kTileBytes / sizeof(V4<T>); };
 
 // Issue the LDS-DMA fill of one tile: per round each of the 4 waves moves one 1-KiB piece
 // (64 lanes x 16 B); the LDS destination is the wave-uniform base + lane*16.
 template <typename T>
 __device__ __forceinline__ void tile_fill(const V4<T>* __restrict__ src, V4<T>* dst) {
+  constexpr int kRound = kBlock * 16;  // bytes one pass of the workgroup moves
+  static_assert(kTileBytes % kRound == 0, "tile must be whole workgroup x 1 KiB-per-wave passes");
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
 #pragma unroll
-  for (int r = 0; r < kTileBytes / 4096; ++r) {
-    const char* g = reinterpret_cast<const char*>(src) + r * 4096 + wave * 1024 + lane * 16;
-    char* l = reinterpret_cast<char*>(dst) + r * 4096 + wave * 1024;
+  for (int r = 0; r < kTileBytes / kRound; ++r) {
+    const char* g = reinterpret_cast<const char*>(src) + r * kRound + wave * 1024 + lane * 16;
+    char* l = reinterpret_cast<char*>(dst) + r * kRound + wave * 1024;
     __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
                                      (__attribute__((address_space(3))) void*)l, 16, 0, 0);
   }

@@ -195,7 +195,7 @@ int choose_groups(gs_stepper* s, int span, bool phi, bool concurrent = false) {
   if (concurrent) return span;
   const int fm = phi ? 2 : (s->exact ? 1 : 0);
   const int64_t resident = (int64_t)(s->occ[fm] > 0 ? s->occ[fm] : 4) * s->cus;
-  const int64_t ib = s->L.n_local / (256 * s->L.ipl);
+  const int64_t ib = s->L.n_local / (GS_BLOCK * s->L.ipl);
   int best = 1;
   double best_cost = 1e300;
   for (int g = 1; g <= span; ++g) {

@@ -75,4 +75,10 @@ GS_HD int32_t auto_chunk(int64_t n) {
 
 GS_HD int64_t round_up(int64_t a, int64_t b) { return (a + b - 1) / b * b; }
 
+// Threads per force-kernel workgroup (i-bodies per workgroup = GS_BLOCK * ipl). 256 = 4
+// waves; other values exist for the block-size sweep (scripts/gpu_block_sweep.sh).
+#ifndef GS_BLOCK
+#define GS_BLOCK 256
+#endif
+
 }  // namespace gs
