@@ -33,7 +33,7 @@ def main() -> int:
     ap.add_argument("--n", type=int, default=1 << 20)
     ap.add_argument("--dtype", choices=["fp32", "fp64"], default="fp32")
     ap.add_argument("--kernel", default="auto", choices=["auto", "lds", "smem", "mfma"])
-    ap.add_argument("--mode", default="auto", choices=["auto", "fused", "split"])
+    ap.add_argument("--mode", default="auto", choices=["auto", "fused", "split", "sym"])
     ap.add_argument("--ipl", type=int, default=0)
     ap.add_argument("--no-graph", dest="graph", action="store_false")
     ap.add_argument("--graph-comm", action="store_true",

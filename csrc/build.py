@@ -28,6 +28,7 @@ ARCH = os.environ.get("GRAVSIM_ARCH", "gfx950")
 HEADERS = sorted((CSRC / "include").glob("*.h"))
 CPU_SRC = [CSRC / "common" / "layout.cpp", CSRC / "cpu" / "cpu_engine.cpp"]
 HIP_SRC = [CSRC / "common" / "layout.cpp", CSRC / "hip" / "nbody_kernels.hip",
+           CSRC / "hip" / "nbody_sym.hip",
            CSRC / "hip" / "nbody_mfma.hip", CSRC / "hip" / "stepper.hip"]
 TOOL_SRC = [CSRC / "tools" / "gravsim_main.cpp"]
 

@@ -37,6 +37,22 @@ extern "C" int gs_layout_compute(const gs_config* cfg, gs_layout* out) {
   out->n = cfg->n;
   out->chunk = chunk;
   out->n_pad = gs::round_up(cfg->n, (int64_t)cfg->nranks * chunk);
+  // Newton-3 symmetric schedule (fp32, fast cutoff, P | 8). Its chunk/row/group structure
+  // must not depend on P, so the padding is the one an 8-rank run would use.
+  const bool sym_ok = cfg->dtype == GS_FP32 && cfg->cutoff_mode != 1 && 8 % cfg->nranks == 0 &&
+                      cfg->kernel != GS_KERNEL_MFMA;
+  if (cfg->mode == GS_MODE_SYM && !sym_ok) {
+    gs_set_error("layout: the sym schedule is fp32, fast-cutoff, with nranks dividing 8");
+    return -1;
+  }
+  const int64_t sym_unit = 8 * (int64_t)(chunk % 2048 == 0 ? chunk : 2 * chunk);
+  const int64_t sym_pad = gs::round_up(cfg->n, sym_unit);
+  bool sym = cfg->mode == GS_MODE_SYM;
+  if (cfg->mode == GS_MODE_AUTO && sym_ok && cfg->n >= 262144 && sym_pad * 20 <= out->n_pad * 21) {
+    // Partial buffers: n_local * (S + H) * 12 B (gs_sym_bytes); keep well inside 288 GB.
+    sym = gs_sym_bytes(sym_pad, cfg->nranks) <= ((int64_t)96 << 30);
+  }
+  if (sym) out->n_pad = sym_pad;
   out->n_local = out->n_pad / cfg->nranks;
   out->local_begin = (int64_t)cfg->rank * out->n_local;
   out->n_chunks = (int32_t)((cfg->n + chunk - 1) / chunk);
@@ -72,7 +88,7 @@ extern "C" int gs_layout_compute(const gs_config* cfg, gs_layout* out) {
   }
   out->ipl = ipl;
   const int64_t i_blocks = out->n_local / (GS_BLOCK * ipl);
-  int32_t mode = cfg->mode;
+  int32_t mode = sym ? GS_MODE_SYM : cfg->mode;
   if (out->kernel == GS_KERNEL_MFMA) mode = GS_MODE_SPLIT;
   if (mode == GS_MODE_AUTO) {
     // Fused needs enough i-blocks to fill 256 CUs at >= 8 workgroups of 4 waves each;
@@ -90,6 +106,28 @@ extern "C" int gs_layout_compute(const gs_config* cfg, gs_layout* out) {
   }
   out->split_groups = groups;
   return 0;
+}
+
+// Symmetric-schedule geometry (gs_kernels.h SymArgs): NC chunks of 2048, shell H = NC / 2,
+// segment length L = max(1, NC / 512) chunks, S = ceil(H / L) segments per row.
+extern "C" int gs_sym_geometry(int64_t n_pad, int32_t* NC, int32_t* H, int32_t* L, int32_t* S) {
+  if (n_pad % (8 * 2048) != 0) { gs_set_error("sym: n_pad must be a multiple of 16384"); return -1; }
+  const int32_t nc = (int32_t)(n_pad / 2048);
+  const int32_t h = nc / 2;
+  const int32_t l = nc / 512 > 1 ? nc / 512 : 1;
+  if (NC) *NC = nc;
+  if (H) *H = h;
+  if (L) *L = l;
+  if (S) *S = (h + l - 1) / l;
+  return 0;
+}
+
+extern "C" int64_t gs_sym_bytes(int64_t n_pad, int32_t nranks) {
+  int32_t nc, h, l, sg;
+  if (gs_sym_geometry(n_pad, &nc, &h, &l, &sg)) return -1;
+  const int64_t n_local = n_pad / nranks;
+  // Pi + Pj + Pd (3 floats per body per slot) + two group-sum buffers (8 groups x 3 floats)
+  return n_local * 12 * ((int64_t)sg + h + 1) + 2 * n_local * 8 * 12;
 }
 
 extern "C" void gs_ic_fill_host(int32_t ic, uint64_t seed, int64_t n, int64_t begin, int64_t end,

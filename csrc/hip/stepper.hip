@@ -94,6 +94,14 @@ struct gs_stepper {
   double eps2 = 0.0;           // r^2 offset used by the kernels
   int cus = 256;               // compute units
   int occ[3] = {0, 0, 0};      // split-kernel workgroups per CU by force mode
+  // Newton-3 symmetric schedule (GS_MODE_SYM): partial slots, group sums, geometry.
+  float* sym_Pi = nullptr;
+  float* sym_Pj = nullptr;
+  float* sym_Pd = nullptr;
+  float* sym_S = nullptr;  // group sums by destination rank
+  float* sym_R = nullptr;  // group sums by source rank (== sym_S with one rank)
+  int32_t sym_NC = 0, sym_H = 0, sym_L = 0, sym_S_n = 0;
+  hipEvent_t ev_sym = nullptr;
 };
 
 namespace {
@@ -155,6 +163,73 @@ gs::KArgs<T> base_args(gs_stepper* s, int cur) {
   a.cut2 = (T)(s->cfg.cutoff * s->cfg.cutoff);
   a.eps2 = (T)s->eps2;
   return a;
+}
+
+bool use_sym(const gs_stepper* s) { return s->L.mode == GS_MODE_SYM && !s->exact; }
+
+gs::SymArgs sym_args(gs_stepper* s, int cur) {
+  gs::SymArgs a;
+  memset(&a, 0, sizeof(a));
+  a.X = static_cast<const float*>(s->X[cur]);
+  a.X_next = static_cast<float*>(s->X[cur ^ 1]);
+  a.vel = static_cast<float*>(s->vel);
+  a.Pi = s->sym_Pi;
+  a.Pj = s->sym_Pj;
+  a.Pd = s->sym_Pd;
+  a.Sbuf = s->sym_S;
+  a.Rbuf = s->sym_R;
+  a.n_real = s->L.n;
+  a.n_local = s->L.n_local;
+  a.i_begin = s->L.local_begin;
+  a.NC = s->sym_NC;
+  a.P = s->cfg.nranks;
+  a.rows = s->sym_NC / s->cfg.nranks;
+  a.a0 = s->cfg.rank * a.rows;
+  a.S = s->sym_S_n;
+  a.L = s->sym_L;
+  a.H = s->sym_H;
+  a.real_chunks = (int32_t)((s->L.n + gs::kSymC - 1) / gs::kSymC);
+  a.dt = (float)s->cfg.dt;
+  a.eps2 = (float)s->eps2;
+  return a;
+}
+
+// Group-sum exchange of the symmetric schedule: rank r sends S_g(x) of its groups for the
+// bodies of rank q to q (ncclSend/ncclRecv pairs, one group call) and keeps its own block.
+int sym_exchange_rccl(gs_stepper* s) {
+  const int P = s->cfg.nranks, r = s->cfg.rank;
+  const size_t cnt = (size_t)(gs::kSymGroups / P) * 3 * s->L.n_local;
+  GS_HIP(hipEventRecord(s->ev_ready, s->s_comp));
+  GS_HIP(hipStreamWaitEvent(s->s_comm, s->ev_ready, 0));
+  GS_HIP(hipMemcpyAsync(s->sym_R + (size_t)r * cnt, s->sym_S + (size_t)r * cnt, cnt * 4,
+                        hipMemcpyDeviceToDevice, s->s_comm));
+  if (P > 1) {
+    GS_NCCL(ncclGroupStart());
+    for (int q = 0; q < P; ++q) {
+      if (q == r) continue;
+      GS_NCCL(ncclSend(s->sym_S + (size_t)q * cnt, cnt, ncclFloat32, q, s->comm, s->s_comm));
+      GS_NCCL(ncclRecv(s->sym_R + (size_t)q * cnt, cnt, ncclFloat32, q, s->comm, s->s_comm));
+    }
+    GS_NCCL(ncclGroupEnd());
+  }
+  GS_HIP(hipEventRecord(s->ev_sym, s->s_comm));
+  GS_HIP(hipStreamWaitEvent(s->s_comp, s->ev_sym, 0));
+  return 0;
+}
+
+int ensure_sym(gs_stepper* s) {
+  if (s->L.mode != GS_MODE_SYM || s->sym_Pi) return 0;
+  if (gs_sym_geometry(s->L.n_pad, &s->sym_NC, &s->sym_H, &s->sym_L, &s->sym_S_n)) return -1;
+  const size_t nl = (size_t)s->L.n_local, rows = (size_t)s->sym_NC / s->cfg.nranks;
+  GS_HIP(hipMalloc(&s->sym_Pi, rows * s->sym_S_n * 3 * gs::kSymC * sizeof(float)));
+  GS_HIP(hipMalloc(&s->sym_Pj, rows * s->sym_H * 3 * gs::kSymC * sizeof(float)));
+  GS_HIP(hipMalloc(&s->sym_Pd, rows * 3 * gs::kSymC * sizeof(float)));
+  GS_HIP(hipMalloc(&s->sym_S, (size_t)gs::kSymGroups * 3 * nl * sizeof(float)));
+  if (s->cfg.nranks > 1)
+    GS_HIP(hipMalloc(&s->sym_R, (size_t)gs::kSymGroups * 3 * nl * sizeof(float)));
+  else
+    s->sym_R = s->sym_S;
+  return 0;
 }
 
 // Choose the fast or exact force path once the masses are known. The fast path adds a core
@@ -287,6 +362,28 @@ int ring_finish(gs_stepper* s, const gs::KArgs<T>& a) {
   return 0;
 }
 
+// Symmetric schedule, parts: 1 = force + group reduce (+ RCCL group-sum exchange),
+// 2 = finalize (sum + integrate), 3 = both. Virtual-rank groups run part 1 on every shard,
+// exchange by device copies, then part 2 (gs_group_step).
+int enqueue_sym(gs_stepper* s, int cur, bool need_gather, bool gathered_externally, int part,
+                bool timed) {
+  gs::SymArgs a = sym_args(s, cur);
+  if (s->emulate) a.Rbuf = s->sym_S;  // timing emulation: no exchange, stale sums
+  if (part & 1) {
+    if (need_gather) {
+      if (gathered_externally) s->full[cur] = true;
+      else if (gather(s, cur)) return -1;
+      GS_HIP(hipStreamWaitEvent(s->s_comp, s->ev_gathered, 0));
+    }
+    GS_HIP(gs::launch_force_sym(a, s->s_comp));
+    if (timed) GS_HIP(hipEventRecord(s->ev_local, s->s_comp));
+    GS_HIP(gs::launch_sym_group_reduce(a, s->s_comp));
+    if (s->have_comm && sym_exchange_rccl(s)) return -1;
+  }
+  if (part & 2) GS_HIP(gs::launch_sym_finalize(a, s->s_comp));
+  return 0;
+}
+
 // Enqueue one step. `capturing` disables timing events.
 template <typename T>
 int enqueue_step(gs_stepper* s, bool capturing, bool gathered_externally) {
@@ -298,6 +395,15 @@ int enqueue_step(gs_stepper* s, bool capturing, bool gathered_externally) {
   const bool timed = s->timed && !capturing;
   if (timed) GS_HIP(hipEventRecord(s->ev_t0, s->s_comp));
   const bool need_gather = (s->have_comm || s->virt) && !s->full[cur];
+  if constexpr (sizeof(T) == 4) {
+    if (use_sym(s)) {
+      if (enqueue_sym(s, cur, need_gather, gathered_externally, 3, timed)) return -1;
+      if (timed) GS_HIP(hipEventRecord(s->ev_end, s->s_comp));
+      s->full[cur ^ 1] = !(s->have_comm || s->virt);
+      s->k += 1;
+      return 0;
+    }
+  }
   const bool ring = s->cfg.strategy == GS_STRATEGY_RING;
   if (need_gather && ring && (s->emulate || !gathered_externally)) {
     // Ring pass with RCCL (or timing emulation: no transfer, slices treated as present).
@@ -459,6 +565,25 @@ int accel_impl(gs_stepper* s, double* acc4, bool step_path) {
   }
   if (gather(s, cur)) return -1;
   if (s->have_comm) GS_HIP(hipStreamWaitEvent(s->s_comp, s->ev_gathered, 0));
+  if constexpr (sizeof(T) == 4) {
+    if (step_path && use_sym(s)) {
+      if (s->virt && s->cfg.nranks > 1) {
+        gs_set_error("accel: the sym step path of a virtual-rank shard needs the group");
+        return -1;
+      }
+      gs::SymArgs sa = sym_args(s, cur);
+      sa.acc_out = static_cast<float*>(s->acc);
+      GS_HIP(gs::launch_force_sym(sa, s->s_comp));
+      GS_HIP(gs::launch_sym_group_reduce(sa, s->s_comp));
+      if (s->have_comm && sym_exchange_rccl(s)) return -1;
+      GS_HIP(gs::launch_sym_finalize(sa, s->s_comp));
+      GS_HIP(hipStreamSynchronize(s->s_comp));
+      std::vector<float> A((size_t)s->L.n_local * 4);
+      GS_HIP(hipMemcpy(A.data(), s->acc, A.size() * sizeof(float), hipMemcpyDeviceToHost));
+      for (size_t i = 0; i < A.size(); ++i) acc4[i] = (double)A[i];
+      return 0;
+    }
+  }
   gs::KArgs<T> a = base_args<T>(s, cur);
   if (!step_path) {  // diagnostics: exact cutoff + potential
     a.phi = 1;
@@ -531,6 +656,7 @@ int gs_stepper_create(const gs_config* cfg, gs_stepper** out) {
   s->ev_recv.assign((size_t)cfg->nranks, nullptr);
   for (auto& e : s->ev_recv) FAIL_CLEAN(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   FAIL_CLEAN(hipEventCreateWithFlags(&s->ev_remote, hipEventDisableTiming));
+  FAIL_CLEAN(hipEventCreateWithFlags(&s->ev_sym, hipEventDisableTiming));
   FAIL_CLEAN(hipEventCreateWithFlags(&s->ev_fork, hipEventDisableTiming));
   FAIL_CLEAN(hipEventCreateWithFlags(&s->ev_ready, hipEventDisableTiming));
   FAIL_CLEAN(hipEventCreateWithFlags(&s->ev_gathered, hipEventDisableTiming));
@@ -544,7 +670,12 @@ int gs_stepper_create(const gs_config* cfg, gs_stepper** out) {
   FAIL_CLEAN(hipMalloc(&s->acc, (size_t)s->L.n_local * rb));
   // Per-chunk partials (n_chunks x n_local rows) only for the split schedule; a single-rank
   // fused run never touches them (16M bodies: 64 GB saved), and allocates on demand.
-  if ((s->L.mode == GS_MODE_SPLIT || cfg->nranks > 1) && ensure_partial(s)) {
+  if ((s->L.mode == GS_MODE_SPLIT || (cfg->nranks > 1 && s->L.mode != GS_MODE_SYM)) &&
+      ensure_partial(s)) {
+    gs_stepper_destroy(s);
+    return -1;
+  }
+  if (ensure_sym(s)) {
     gs_stepper_destroy(s);
     return -1;
   }
@@ -569,11 +700,13 @@ int gs_stepper_destroy(gs_stepper* s) {
   if (s->s_rem2) (void)hipStreamSynchronize(s->s_rem2);
   if (s->graph) (void)hipGraphExecDestroy(s->graph);
   if (s->have_comm) (void)ncclCommDestroy(s->comm);
+  if (s->sym_R == s->sym_S) s->sym_R = nullptr;
   for (void* p : {s->X[0], s->X[1], s->vel, s->partial, s->acc, (void*)s->mass_dev,
-                  (void*)s->nonfinite})
+                  (void*)s->nonfinite, (void*)s->sym_Pi, (void*)s->sym_Pj, (void*)s->sym_Pd,
+                  (void*)s->sym_S, (void*)s->sym_R})
     if (p) (void)hipFree(p);
   for (hipEvent_t e : {s->ev_ready, s->ev_gathered, s->ev_t0, s->ev_local, s->ev_end,
-                       s->ev_remote, s->ev_fork, s->ev_rem2})
+                       s->ev_remote, s->ev_fork, s->ev_rem2, s->ev_sym})
     if (e) (void)hipEventDestroy(e);
   if (s->s_comp) (void)hipStreamDestroy(s->s_comp);
   if (s->s_comm) (void)hipStreamDestroy(s->s_comm);
@@ -630,6 +763,8 @@ int gs_stepper_get_state(gs_stepper* s, double* pos, double* vel, double* mass) 
 
 int gs_stepper_step(gs_stepper* s, int32_t nsteps) {
   GS_HIP(hipSetDevice(s->cfg.device));
+  // A sym layout whose masses resolved to the exact-cutoff path runs the split schedule.
+  if (s->L.mode == GS_MODE_SYM && s->exact && ensure_partial(s)) return -1;
   if (s->cfg.nranks > 1 && !s->have_comm && !s->emulate) {
     gs_set_error("step: nranks > 1 but no RCCL communicator (call gs_stepper_comm_init)");
     return -1;
@@ -838,6 +973,27 @@ int gs_group_step(gs_stepper** sh, int32_t P, int32_t nsteps) {
         }
       for (int r = 0; r < P; ++r) GS_HIP(hipEventRecord(sh[r]->ev_gathered, gsm));
     }
+    if (use_sym(sh[0]) && P > 1) {
+      // Symmetric schedule: force + group reduce on every shard, then the group-sum
+      // exchange as device copies (shard r's block for q -> shard q's slot r), then finalize.
+      const size_t cnt = (size_t)(gs::kSymGroups / P) * 3 * sh[0]->L.n_local;
+      for (int r = 0; r < P; ++r)
+        if (enqueue_sym(sh[r], cur, need, true, 1, false)) return -1;
+      for (int r = 0; r < P; ++r) GS_HIP(hipEventRecord(sh[r]->ev_ready, sh[r]->s_comp));
+      for (int r = 0; r < P; ++r) GS_HIP(hipStreamWaitEvent(gsm, sh[r]->ev_ready, 0));
+      for (int q = 0; q < P; ++q)
+        for (int r = 0; r < P; ++r)
+          GS_HIP(hipMemcpyAsync(sh[q]->sym_R + (size_t)r * cnt, sh[r]->sym_S + (size_t)q * cnt,
+                                cnt * sizeof(float), hipMemcpyDeviceToDevice, gsm));
+      GS_HIP(hipEventRecord(sh[0]->ev_sym, gsm));
+      for (int r = 0; r < P; ++r) {
+        GS_HIP(hipStreamWaitEvent(sh[r]->s_comp, sh[0]->ev_sym, 0));
+        if (enqueue_sym(sh[r], cur, false, true, 2, false)) return -1;
+        sh[r]->full[cur ^ 1] = false;
+        sh[r]->k += 1;
+      }
+      continue;
+    }
     for (int r = 0; r < P; ++r)
       if (enqueue_step_any(sh[r], false, need)) return -1;
   }
@@ -860,7 +1016,9 @@ int gs_stepper_comm_init(gs_stepper* s, const void* id128, int32_t rank, int32_t
   GS_HIP(hipSetDevice(s->cfg.device));
   ncclUniqueId id;
   memcpy(&id, id128, sizeof(id));
-  if (ensure_partial(s)) return -1;  // the multi-rank schedule is always split
+  // The one-sided multi-rank schedule is always split (the sym layout falls back to it only
+  // when its masses resolve to the exact-cutoff path, see gs_stepper_step).
+  if (s->L.mode != GS_MODE_SYM && ensure_partial(s)) return -1;
   GS_NCCL(ncclCommInitRank(&s->comm, nranks, id, rank));
   // GRAVSIM_FORCE_COMM keeps a 1-rank communicator live so the full multi-rank schedule
   // (in-place ncclAllGather, local/remote split on two streams, events) runs on one GPU.

@@ -36,6 +36,7 @@ enum gs_mode {
   GS_MODE_AUTO = 0,
   GS_MODE_FUSED = 1,   // one workgroup per i-block sweeps every j-chunk, KD integrate in the epilogue
   GS_MODE_SPLIT = 2,   // i-block x chunk-group grid writes per-chunk partials; reduce+integrate kernel
+  GS_MODE_SYM = 3,     // fp32 Newton-3: each unordered pair once, both sides (nbody_sym.hip)
 };
 
 // Initial-condition families (models). Same formulas in gravsim/models/initial_conditions.py.
@@ -87,6 +88,10 @@ typedef struct gs_layout {
 // Canonical, world-size-independent decomposition (shared by CPU and GPU engines).
 int gs_layout_compute(const gs_config* cfg, gs_layout* out);
 int32_t gs_auto_chunk(int64_t n);
+// Symmetric (Newton-3) schedule geometry for a padded body count, and its partial-buffer
+// bytes per rank (GS_MODE_SYM).
+int gs_sym_geometry(int64_t n_pad, int32_t* NC, int32_t* H, int32_t* L, int32_t* S);
+int64_t gs_sym_bytes(int64_t n_pad, int32_t nranks);
 
 // ---------------------------------------------------------------- counter-based RNG / ICs (host)
 // Fill bodies [begin, end) of the IC family into fp64 arrays (pos/vel: 3 per body, mass: 1).

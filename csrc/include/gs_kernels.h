@@ -35,6 +35,39 @@ inline int split_span(const KArgs<T>& a) {
   return (a.c_end - a.c_begin) - (se - sb);
 }
 
+// ---- Newton-3 symmetric schedule (fp32, fast cutoff; nbody_sym.hip) -------------------
+// Canonical decomposition, a function of the padded body count only (so every rank count
+// P | 8 produces the same bits): chunks of kSymC = 2048 bodies, NC = n_pad / 2048 of them,
+// G = 8 row groups of NC / 8 chunks. Chunk A pairs with the next h(A) chunks cyclically
+// (h = NC/2 for A < NC/2, NC/2 - 1 above: every unordered chunk pair exactly once) and with
+// itself (one-sided). Row A's shell is cut into segments of L chunks; one workgroup per
+// (row, segment) unit writes an i-side partial Pi[row][segment] and, per shell chunk, a
+// j-side partial Pj[row][d-1]. Group reduce: S_g(x) = sum over rows A of group g (A
+// ascending) of Pj[A][x - A]. Final: a = Pd + sum_s Pi[s] (s ascending) + sum_g S_g
+// (g ascending), then the KD integrate.
+constexpr int kSymC = 2048;
+constexpr int kSymGroups = 8;
+
+struct SymArgs {
+  const float* X;      // [n_pad * 4] gathered positions (x, y, z, mu)
+  float* Pi;           // [rows][S][3][kSymC] i-side partials
+  float* Pj;           // [rows][H][3][kSymC] j-side partials, H = NC / 2
+  float* Pd;           // [rows][3][kSymC] diagonal-chunk partials
+  float* Sbuf;         // [P][G/P][3][n_local] group sums by destination rank
+  const float* Rbuf;   // [P][G/P][3][n_local] group sums received, by source rank
+  float* X_next;       // [n_pad * 4]
+  float* vel;          // [n_local * 4]
+  float* acc_out;      // optional [n_local * 4]: emit accelerations instead of integrating
+  int64_t n_real, n_local, i_begin;
+  int32_t NC, a0, rows, S, L, H, P, real_chunks;
+  float dt, eps2;
+};
+
+hipError_t launch_force_sym(const SymArgs& a, hipStream_t s);
+hipError_t launch_sym_group_reduce(const SymArgs& a, hipStream_t s);
+hipError_t launch_sym_finalize(const SymArgs& a, hipStream_t s);
+int sym_occupancy();
+
 template <typename T>
 hipError_t launch_force_split(const KArgs<T>& a, int kernel, int ipl, int groups, hipStream_t s);
 template <typename T>

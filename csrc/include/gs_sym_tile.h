@@ -1,0 +1,211 @@
+// Newton-3 (symmetric) register tile for the fp32 direct sum on gfx950.
+//
+// The reference's cuda.cu:53-60 visits each unordered pair once (j > i) and scatters the
+// equal-and-opposite force into both bodies (cuda.cu:43-49), but does it with racy
+// non-atomic global read-modify-writes. This tile keeps the "one pair,
+// two interactions" saving without any scatter: each wave holds an i-set of 64*I bodies and
+// a j-set of 64*J bodies in registers and visits all (64 I) x (64 J) pairs, accumulating
+//   * the i side in per-lane registers (as the asymmetric kernel does), and
+//   * the j side in per-lane "carrier" registers that travel with the j-bodies.
+//
+// Data movement is all DPP. Within a 16-lane row, step k (k = 0..15) reads the j positions
+// of lane l-(k+1) with `v_mov_b32_dpp row_ror:(k+1)`. The carriers advance one lane per step with
+// a single `v_sub_f32_dpp row_ror:1` that also adds the step's contribution, so the carrier
+// of a j-body always sits in the lane that is currently interacting with it. After 16 steps
+// the carriers are home; the j positions and carriers then move one row (16 lanes) with
+// ds_bpermute, and after 4 such phases every lane has met every j of the wave.
+//
+// Cost per pair (two interactions): 3 sub + 3 FMA (r^2) + v_rsq_f32 + 2 mul (r^-3)
+// + 2 mul (s_i, s_j) + 6 FMA/mul (both accumulators), all packed two pairs per v_pk_*
+// instruction: 4 v_pk + 0.5 v_rsq per interaction, against 6 v_pk + 1 v_rsq for the
+// one-sided loop (nbody_kernels.hip interact_pk).
+//
+// Numerics: the pair term uses the fast-cutoff core (r^2 + eps2, nbody_kernels.hip FM_FAST),
+// and r^-3 = (y*y)*y with y = rsq(r^2 + eps2). The j-side term of a pair is the exact
+// negation of what body j would compute for body i (x_i - x_j = -(x_j - x_i) in IEEE).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <utility>
+
+namespace gs {
+namespace sym {
+
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+  return __builtin_bit_cast(
+      float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xf, 0xf, true));
+}
+
+// Value of `v` held by lane (l - O) of the same 16-lane row (row_ror:O); O = 16 is identity.
+template <int O>
+__device__ __forceinline__ float row_from(float v) {
+  if constexpr (O % 16 == 0) {
+    return v;
+  } else {
+    return dpp<0x120 + O>(v);
+  }
+}
+
+// a - b with `a` taken from lane l-O of the row, as one v_sub_f32_dpp. The compiler's DPP
+// combiner folds a v_mov_b32_dpp only into a single use, so this is written out. Used by the
+// DPP issue-cost probe (csrc/tools/sym_probe.hip): a DPP-modified VALU op measured ~2.1 ns
+// per wave-instruction against ~1.3 ns plain, so the tile fetches each j value once per step
+// with v_mov_b32_dpp instead of folding DPP into its I consumers. The caller must not have
+// written `a` with a VALU op in the two preceding instructions (DPP read hazard).
+template <int O>
+__device__ __forceinline__ float sub_from(float a, float b) {
+  if constexpr (O % 16 == 0) {
+    return a - b;
+  } else {
+    float d;
+    asm("v_sub_f32_dpp %0, %1, %2 row_ror:%3 row_mask:0xf bank_mask:0xf bound_ctrl:1"
+        : "=v"(d) : "v"(a), "v"(b), "i"(O));
+    return d;
+  }
+}
+
+// Value of `v` held by lane (l - 16) mod 64 (next row down, wave-wide).
+__device__ __forceinline__ float wave_from_minus16(float v, int addr) {
+  return __builtin_bit_cast(float,
+                            __builtin_amdgcn_ds_bpermute(addr, __builtin_bit_cast(int, v)));
+}
+
+template <int I>
+struct ISet {
+  float x[I], y[I], z[I], mu[I];
+  float ax[I], ay[I], az[I];
+};
+
+template <int J>
+struct JSet {
+  float x[J], y[J], z[J], mu[J];
+  float cx[J], cy[J], cz[J];  // carriers: j-side accumulators travelling with the j-bodies
+};
+
+// One step: every lane meets the j-bodies of lane l-O of its row. SYM = false is the
+// one-sided variant (diagonal tiles: i-set == j-set, each ordered pair once on the i side).
+using f2 = float __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ f2 pk_fma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+
+// One step: every lane meets the j-bodies of lane l-O of its row. SYM = false is the
+// one-sided variant (diagonal tiles: i-set == j-set, each ordered pair once on the i side).
+//
+// Arithmetic runs on pairs of i-bodies as 2-vectors, so everything but the rsq issues as
+// v_pk_{add,mul,fma}_f32 (two interactions per instruction; a scalar VALU op costs the same
+// issue slot as a packed one on gfx950, profiles/r1_sym_probe.jsonl). The j values are
+// fetched once per step with v_mov_b32_dpp (DPP cannot modify VOP3P) and broadcast by op_sel.
+// Per 2 pairs (4 interactions): 16 v_pk + 2 v_rsq_f32; per j and step: 4 v_mov_dpp +
+// 3 v_add + 3 v_sub_dpp for the carriers.
+#ifndef GS_SYM_U
+#define GS_SYM_U 2
+#endif
+template <int I, int J, bool SYM, int O>
+__device__ __forceinline__ void step(ISet<I>& a, JSet<J>& b, float eps2) {
+  static_assert(I % 2 == 0, "i-bodies are processed in pairs");
+  // U i-pairs go through each stage together (stage-major source order), so consecutive
+  // instructions are independent and the packed-result read hazard needs no s_nop.
+  constexpr int U = (I / 2) % GS_SYM_U == 0 ? GS_SYM_U : 1;
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    const float xj = row_from<O>(b.x[j]), yj = row_from<O>(b.y[j]);
+    const float zj = row_from<O>(b.z[j]), mj = row_from<O>(b.mu[j]);
+    f2 tx, ty, tz;
+#pragma unroll
+    for (int i0 = 0; i0 < I; i0 += 2 * U) {
+      f2 dx[U], dy[U], dz[U], r2[U], y[U], y3[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int i = i0 + 2 * u;
+        dx[u] = f2(xj) - f2{a.x[i], a.x[i + 1]};
+        dy[u] = f2(yj) - f2{a.y[i], a.y[i + 1]};
+        dz[u] = f2(zj) - f2{a.z[i], a.z[i + 1]};
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) r2[u] = pk_fma(dx[u], dx[u], f2(eps2));
+#pragma unroll
+      for (int u = 0; u < U; ++u) r2[u] = pk_fma(dy[u], dy[u], r2[u]);
+#pragma unroll
+      for (int u = 0; u < U; ++u) r2[u] = pk_fma(dz[u], dz[u], r2[u]);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        y[u].x = __builtin_amdgcn_rsqf(r2[u].x);
+        y[u].y = __builtin_amdgcn_rsqf(r2[u].y);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) y3[u] = y[u] * y[u];
+#pragma unroll
+      for (int u = 0; u < U; ++u) y3[u] = y3[u] * y[u];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int i = i0 + 2 * u;
+        const f2 si = f2(mj) * y3[u];
+        f2 ax = {a.ax[i], a.ax[i + 1]}, ay = {a.ay[i], a.ay[i + 1]}, az = {a.az[i], a.az[i + 1]};
+        ax = pk_fma(si, dx[u], ax);
+        ay = pk_fma(si, dy[u], ay);
+        az = pk_fma(si, dz[u], az);
+        a.ax[i] = ax.x; a.ax[i + 1] = ax.y;
+        a.ay[i] = ay.x; a.ay[i + 1] = ay.y;
+        a.az[i] = az.x; a.az[i + 1] = az.y;
+      }
+      if constexpr (SYM) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int i = i0 + 2 * u;
+          const f2 sj = f2{a.mu[i], a.mu[i + 1]} * y3[u];
+          if (i == 0) {
+            tx = sj * dx[u]; ty = sj * dy[u]; tz = sj * dz[u];
+          } else {
+            tx = pk_fma(sj, dx[u], tx);
+            ty = pk_fma(sj, dy[u], ty);
+            tz = pk_fma(sj, dz[u], tz);
+          }
+        }
+      }
+    }
+    if constexpr (SYM) {
+      // carrier of lane l-1 (the j this lane just met) moves here and takes -t.
+      b.cx[j] = row_from<1>(b.cx[j]) - (tx.x + tx.y);
+      b.cy[j] = row_from<1>(b.cy[j]) - (ty.x + ty.y);
+      b.cz[j] = row_from<1>(b.cz[j]) - (tz.x + tz.y);
+    }
+  }
+}
+
+template <int I, int J, bool SYM, int... Os>
+__device__ __forceinline__ void row_pass(ISet<I>& a, JSet<J>& b, float eps2,
+                                         std::integer_sequence<int, Os...>) {
+  (step<I, J, SYM, Os + 1>(a, b, eps2), ...);
+}
+
+template <int J, bool SYM>
+__device__ __forceinline__ void next_row(JSet<J>& b, int addr) {
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    b.x[j] = wave_from_minus16(b.x[j], addr);
+    b.y[j] = wave_from_minus16(b.y[j], addr);
+    b.z[j] = wave_from_minus16(b.z[j], addr);
+    b.mu[j] = wave_from_minus16(b.mu[j], addr);
+    if constexpr (SYM) {
+      b.cx[j] = wave_from_minus16(b.cx[j], addr);
+      b.cy[j] = wave_from_minus16(b.cy[j], addr);
+      b.cz[j] = wave_from_minus16(b.cz[j], addr);
+    }
+  }
+}
+
+// All (64 I) x (64 J) pairs of the wave's i-set and j-set. On return the j-set (positions
+// and carriers) is back in its original lanes. Must be called by all 64 lanes (full exec).
+template <int I, int J, bool SYM>
+__device__ __forceinline__ void tile(ISet<I>& a, JSet<J>& b, float eps2) {
+  const int addr = ((static_cast<int>(__lane_id()) + 48) & 63) << 2;
+#pragma unroll 1
+  for (int p = 0; p < 4; ++p) {
+    row_pass<I, J, SYM>(a, b, eps2, std::make_integer_sequence<int, 16>{});
+    next_row<J, SYM>(b, addr);
+  }
+}
+
+}  // namespace sym
+}  // namespace gs

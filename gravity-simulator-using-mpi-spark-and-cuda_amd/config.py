@@ -16,7 +16,7 @@ G_SI = 6.67430e-11  # cuda.cu:11, mpi.c:9, pyspark.py:46
 DTYPES = ("fp32", "fp64")
 DEVICES = ("auto", "cpu", "gpu")
 KERNELS = ("auto", "lds", "smem", "mfma")
-MODES = ("auto", "fused", "split")
+MODES = ("auto", "fused", "split", "sym")
 COMMS = ("auto", "rccl", "gloo", "none")
 LOG_FORMATS = ("mpi", "spark", "cuda", "none")
 
@@ -36,7 +36,7 @@ class SimConfig:
     cutoff_mode: str = "auto"     # GPU: exact (select) | fast (overflow-safe core) | auto
     integrator: str = "kd"        # kd (reference kick-drift) | leapfrog (staggered KDK)
     kernel: str = "auto"          # GPU j-source variant: lds | smem
-    mode: str = "auto"            # GPU schedule: fused | split
+    mode: str = "auto"            # GPU schedule: fused | split | sym (Newton-3, fp32)
     ipl: int = 0                  # i-bodies per lane (0 = auto)
     chunk: int = 0                # canonical j-chunk (0 = auto from n)
     split_groups: int = 0
@@ -81,6 +81,9 @@ class SimConfig:
         if self.kernel == "mfma" and (self.dtype != "fp32" or self.ipl > 1 or
                                       self.mode == "fused"):
             raise ValueError("kernel mfma is fp32, ipl 0/1, split schedule only")
+        if self.mode == "sym" and (self.dtype != "fp32" or self.cutoff_mode == "exact" or
+                                   self.kernel == "mfma"):
+            raise ValueError("mode sym is fp32 with the fast cutoff path (Newton-3 pairs)")
         if self.ipl not in (0, 1, 2, 4, 8) or (self.ipl == 8 and self.dtype != "fp32"):
             raise ValueError("ipl must be 0, 1, 2, 4 (or 8 for fp32)")
         if self.chunk and self.chunk % 1024:

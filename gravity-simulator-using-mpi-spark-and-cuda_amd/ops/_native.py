@@ -49,7 +49,7 @@ class GsLayout(ctypes.Structure):
 
 GS_FP32, GS_FP64 = 0, 1
 KERNEL_IDS = {"auto": 0, "lds": 1, "smem": 2, "mfma": 3}
-MODE_IDS = {"auto": 0, "fused": 1, "split": 2}
+MODE_IDS = {"auto": 0, "fused": 1, "split": 2, "sym": 3}
 CUTOFF_IDS = {"auto": 0, "exact": 1, "fast": 2}
 STRATEGY_IDS = {"allgather": 0, "ring": 1}
 KERNEL_NAMES = {v: k for k, v in KERNEL_IDS.items()}

@@ -54,7 +54,46 @@ class Layout:
         return range(c0, c1)
 
 
-def layout(n: int, rank: int = 0, nranks: int = 1, chunk: int = 0) -> Layout:
+SYM_CHUNK = 2048  # Newton-3 schedule chunk (csrc/include/gs_kernels.h kSymC)
+SYM_GROUPS = 8
+
+
+def sym_pad(n: int, chunk: int) -> int:
+    """Padding of the Newton-3 (sym) schedule: what an 8-rank run would use, so its chunk,
+    row and group structure (hence its bits) is the same for every P dividing 8."""
+    unit = 8 * (chunk if chunk % SYM_CHUNK == 0 else 2 * chunk)
+    return round_up(n, unit)
+
+
+def sym_geometry(n_pad: int) -> dict:
+    """NC chunks, shell H = NC/2, segment length L, segments S (layout.cpp gs_sym_geometry)."""
+    if n_pad % (SYM_GROUPS * SYM_CHUNK):
+        raise ValueError("sym n_pad must be a multiple of 16384")
+    nc = n_pad // SYM_CHUNK
+    h = nc // 2
+    seg = max(1, nc // 512)
+    return {"NC": nc, "H": h, "L": seg, "S": -(-h // seg)}
+
+
+def sym_bytes(n_pad: int, nranks: int) -> int:
+    g = sym_geometry(n_pad)
+    n_local = n_pad // nranks
+    return n_local * 12 * (g["S"] + g["H"] + 1) + 2 * n_local * SYM_GROUPS * 12
+
+
+def sym_auto(n: int, nranks: int, chunk: int = 0, dtype: str = "fp32",
+             cutoff_mode: str = "auto") -> bool:
+    """Whether mode=auto picks the sym schedule (mirror of gs_layout_compute)."""
+    c = chunk or auto_chunk(n)
+    if dtype != "fp32" or cutoff_mode == "exact" or 8 % nranks or n < 262144:
+        return False
+    sp = sym_pad(n, c)
+    if sp * 20 > round_up(n, nranks * c) * 21:
+        return False
+    return sym_bytes(sp, nranks) <= 96 << 30
+
+
+def layout(n: int, rank: int = 0, nranks: int = 1, chunk: int = 0, sym: bool = False) -> Layout:
     if n < 1:
         raise ValueError("n must be >= 1")
     if not (0 <= rank < nranks):
@@ -62,7 +101,9 @@ def layout(n: int, rank: int = 0, nranks: int = 1, chunk: int = 0) -> Layout:
     c = chunk or auto_chunk(n)
     if c % 1024:
         raise ValueError("chunk must be a multiple of 1024")
-    n_pad = round_up(n, nranks * c)
+    if sym and 8 % nranks:
+        raise ValueError("the sym schedule needs nranks dividing 8")
+    n_pad = sym_pad(n, c) if sym else round_up(n, nranks * c)
     n_local = n_pad // nranks
     return Layout(n=n, n_pad=n_pad, n_local=n_local, local_begin=rank * n_local, chunk=c,
                   n_chunks=(n + c - 1) // c, rank=rank, nranks=nranks)

@@ -65,7 +65,9 @@ class HipEngine:
         L = _native.GsLayout()
         _native.check(self.lib, self.lib.gs_stepper_layout(self._s, ctypes.byref(L)), "layout")
         self.native_layout = L.as_dict()
-        self.layout: Layout = make_layout(cfg.n, rank, nranks, L.chunk)
+        self.layout: Layout = make_layout(cfg.n, rank, nranks, L.chunk,
+                                          sym=L.mode == _native.MODE_IDS["sym"])
+        assert self.layout.n_pad == L.n_pad, "Python layout mirror disagrees with native"
         self.mass: Optional[np.ndarray] = None
 
     # -- communicator ---------------------------------------------------------------------

@@ -22,7 +22,9 @@ def test_python_layout_matches_native(n, P):
         c = _native.GsConfig(n=n, dtype=0, rank=r, nranks=P, device=0)
         L = _native.GsLayout()
         assert lib.gs_layout_compute(ctypes.byref(c), ctypes.byref(L)) == 0
-        p = partition.layout(n, r, P)
+        sym = partition.sym_auto(n, P)
+        assert (L.mode == _native.MODE_IDS["sym"]) == sym
+        p = partition.layout(n, r, P, sym=sym)
         assert (L.n_pad, L.n_local, L.local_begin, L.chunk, L.n_chunks) == \
             (p.n_pad, p.n_local, p.local_begin, p.chunk, p.n_chunks)
         assert p.n_pad % (P * p.chunk) == 0 and p.n_pad >= n
@@ -107,3 +109,37 @@ def test_mfma_kernel_config_validation():
     for bad in (dict(dtype="fp64"), dict(dtype="fp32", ipl=4), dict(dtype="fp32", mode="fused")):
         with pytest.raises(ValueError):
             SimConfig(n=1024, kernel="mfma", **bad).validate()
+
+
+@pytest.mark.parametrize("n", [1000, 20000, 100_003, 1 << 20])
+@pytest.mark.parametrize("P", [1, 2, 4, 8])
+def test_sym_layout_independent_of_world_size(n, P):
+    """mode=sym pads as an 8-rank run would: n_pad (hence the chunk/row/group structure and
+    the summation order) is the same for every P dividing 8, and matches the native layout."""
+    lib = _native.cpu_lib()
+    c = _native.GsConfig(n=n, dtype=0, rank=P - 1, nranks=P, device=0,
+                         mode=_native.MODE_IDS["sym"])
+    L = _native.GsLayout()
+    assert lib.gs_layout_compute(ctypes.byref(c), ctypes.byref(L)) == 0
+    assert L.mode == _native.MODE_IDS["sym"]
+    p = partition.layout(n, P - 1, P, sym=True)
+    assert (L.n_pad, L.n_local, L.local_begin) == (p.n_pad, p.n_local, p.local_begin)
+    assert p.n_pad == partition.layout(n, 0, 1, sym=True).n_pad
+    g = partition.sym_geometry(p.n_pad)
+    assert g["NC"] % (partition.SYM_GROUPS) == 0 and g["S"] * g["L"] >= g["H"]
+
+
+def test_sym_layout_rejects_unsupported():
+    lib = _native.cpu_lib()
+    for kw in (dict(dtype=1), dict(nranks=3, rank=0), dict(cutoff_mode=1)):
+        base = dict(n=50000, dtype=0, rank=0, nranks=1, device=0, mode=_native.MODE_IDS["sym"])
+        base.update(kw)
+        L = _native.GsLayout()
+        assert lib.gs_layout_compute(ctypes.byref(_native.GsConfig(**base)), ctypes.byref(L)) != 0
+
+
+def test_sym_auto_at_headline_size():
+    """N = 1M fp32 picks the Newton-3 schedule for P = 1, 2, 4, 8 with unchanged padding."""
+    for P in (1, 2, 4, 8):
+        assert partition.sym_auto(1 << 20, P)
+        assert partition.layout(1 << 20, 0, P, sym=True).n_pad == 1 << 20
