@@ -2,9 +2,12 @@
 
 BASELINE.json metric: "body-updates/sec (whole node) at N=1M direct O(N^2), 1/2/4/8 MI355X"
 (config "1,048,576 bodies fp32 on 8xMI355X, RCCL all-gather ring over xGMI each step").
-N is fixed as the GPU count grows (strong scaling): every rank owns N/P bodies, sums their
-full rows against all N, integrates them (kick-drift fused into the force kernel) and joins
-an in-place RCCL all-gather of positions every step.
+N is fixed as the GPU count grows (strong scaling). The default (mode auto) at this size is
+the Newton-3 schedule: every unordered pair is evaluated once and applied to both bodies
+(csrc/hip/nbody_sym.hip). Each rank owns N/P bodies (a block of 2048-body chunk rows), joins
+an in-place RCCL all-gather of positions, evaluates its rows' cyclic half-shell of chunk
+pairs, exchanges the group sums of the far sides with ncclSend/ncclRecv, and integrates its
+own bodies (kick-drift). --mode split runs the one-sided schedule instead.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--n BODIES] [--dtype fp32|fp64]
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
@@ -90,6 +93,20 @@ def main() -> int:
     eng.close()
     if rank == 0:
         value = cfg.n * a.steps / wall
+        mode = _native.MODE_NAMES.get(lay["mode"])
+        sym = mode == "sym" and not fmode["exact"]
+        if sym:
+            # Newton-3 schedule: each unordered pair once, both sides (nbody_sym.hip).
+            kernel_info = {"kernel": "sym: DPP/LDS register tile, 8 i x 2 j per lane, "
+                                     "cyclic half-shell of 2048-body chunks",
+                           "n_pad": lay["n_pad"]}
+            exch = "all-gather + group-sum send/recv"
+        else:
+            kernel_info = {"kernel": _native.KERNEL_NAMES.get(lay["kernel"]), "ipl": lay["ipl"],
+                           "chunk": lay["chunk"]}
+            exch = "ring send/recv" if a.strategy == "ring" else "all-gather"
+        parallelism = (f"body-decomposition x{world} (RCCL {exch})" if world > 1
+                       else "single GPU")
         out = {
             "metric": "body-updates/sec (whole node) at N=1M direct O(N^2), 1/2/4/8 MI355X",
             "value": value,
@@ -109,16 +126,14 @@ def main() -> int:
                 "global_batch": cfg.n,
                 "seq_len": 1,
                 "dt": cfg.dt,
-                "parallelism": f"body-decomposition x{world} (RCCL "
-                f"{'ring send/recv' if a.strategy == 'ring' else 'all-gather'})" if world > 1
-                else "single GPU",
-                "kernel": _native.KERNEL_NAMES.get(lay["kernel"]),
-                "mode": _native.MODE_NAMES.get(lay["mode"]),
-                "ipl": lay["ipl"],
-                "chunk": lay["chunk"],
+                "parallelism": parallelism,
+                "mode": mode,
+                **kernel_info,
                 "cutoff_path": "exact-select" if fmode["exact"] else
                 f"fast (core^2={fmode['eps2']:.3g} m^2; bit-identical to the 1e-10 m hard cutoff "
                 "for separations above ~mm)",
+                # N^2 pair terms per step (the sym schedule evaluates each unordered pair
+                # once and applies it to both bodies: N(N-1)/2 pair evaluations).
                 "interactions_per_s": float(cfg.n) * cfg.n * a.steps / wall,
                 "nonfinite": int(bad),
             },

@@ -24,89 +24,175 @@
 namespace gs {
 namespace {
 
-constexpr int kW = 8;                 // waves per workgroup
-constexpr int kI = 4, kJ = 4;         // i / j bodies per lane
-constexpr int kTile = 64 * kI;        // 256-body wave tile
-constexpr int kThreads = 64 * kW;     // 512
-constexpr int kTilesPerChunk = kSymC / kTile;
-static_assert(64 * kJ == kTile, "i and j tiles have the same size");
-static_assert(kW * kTile == kSymC, "one workgroup holds one chunk on its i side");
+// Workgroup shape: W waves, I i-bodies and J j-bodies per lane; one workgroup holds one
+// 2048-body chunk on its i side (W * 64 * I == kSymC). GS_SYM_SHAPE picks the A/B variant:
+// 0 = (8 waves, I 4, J 4), 1 = (4 waves, I 8, J 2).
+#ifndef GS_SYM_SHAPE
+#define GS_SYM_SHAPE 1
+#endif
+#if GS_SYM_SHAPE == 1
+constexpr int kW = 4, kI = 8, kJ = 2;
+#else
+constexpr int kW = 8, kI = 4, kJ = 4;
+#endif
+// Occupancy floor (waves per SIMD) as an A/B knob.
+#ifdef GS_SYM_WAVES_PER_EU
+#define GS_SYM_WPE __attribute__((amdgpu_waves_per_eu(GS_SYM_WAVES_PER_EU)))
+#else
+#define GS_SYM_WPE
+#endif
+constexpr int kTileI = 64 * kI;       // i bodies per wave
+constexpr int kTileJ = 64 * kJ;       // j bodies per tile
+constexpr int kThreads = 64 * kW;
+constexpr int kTilesPerChunk = kSymC / kTileJ;
+static_assert(kW * kTileI == kSymC, "one workgroup holds one chunk on its i side");
+
+#ifndef GS_SYM_JLDS
+#define GS_SYM_JLDS 1
+#endif
+// j positions: staged in LDS and read per step (1), or held in registers and rotated with
+// DPP (0). See gs_sym_tile.h tile_lds / tile.
+constexpr bool kJlds = GS_SYM_JLDS;
 
 __device__ __forceinline__ int shell_len(int A, int NC) { return A < NC / 2 ? NC / 2 : NC / 2 - 1; }
 
-__device__ __forceinline__ void load_jset(const float4* __restrict__ X4, int64_t row0,
-                                          sym::JSet<kJ>& b) {
-  const int lane = threadIdx.x & 63;
+// Unit (row a, segment s) -> the sequence of j-tiles it visits, in order, skipping all-ghost
+// column chunks (mu = 0 there, and their rows are never read). s == S is the diagonal chunk.
+struct TileSeq {
+  int A, NC, real_chunks, d1, d, t;
+  bool diag;
+  __device__ __forceinline__ int valid(int dd) const {
+    while (dd <= d1 && (A + dd) % NC >= real_chunks) ++dd;
+    return dd;
+  }
+  __device__ __forceinline__ bool done() const { return d > d1; }
+  __device__ __forceinline__ int64_t row0() const {
+    const int B = diag ? A : (A + d) % NC;
+    return (int64_t)B * kSymC + t * kTileJ;
+  }
+  __device__ __forceinline__ void next() {
+    if (++t == kTilesPerChunk) {
+      t = 0;
+      d = diag ? d1 + 1 : valid(d + 1);
+    }
+  }
+};
+
+// Stage the j-tile at row0 into the tile_lds layout (64 * kJ bodies, each stored twice).
+__device__ __forceinline__ void stage_store(float4* dst, int b, const float4& q) {
+  const int j = b / 64, l = b % 64;
+  dst[j * sym::kStagedRows + sym::staged_entry(l, 0)] = q;
+  dst[j * sym::kStagedRows + sym::staged_entry(l, 1)] = q;
+}
+
+using SlotT = float[2][kW][3][kTileJ];
+using JtT = float4[2][kJ * sym::kStagedRows];
+
+// Visit the unit's j-tiles. SYM: pairs both ways, j-side partials to Pj (the diagonal chunk
+// runs with SYM = false: every ordered pair once on the i side).
+template <bool SYM>
+__device__ __forceinline__ void run_tiles(const SymArgs& a, sym::ISet<kI>& is, TileSeq seq,
+                                          int ar, SlotT& slot, JtT& jt) {
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const float4* X4 = reinterpret_cast<const float4*>(a.X);
+  int buf = 0, cur = 0;
+  if constexpr (kJlds) {
+    if (!seq.done() && threadIdx.x < kTileJ)
+      stage_store(jt[0], threadIdx.x, X4[seq.row0() + threadIdx.x]);
+    __syncthreads();
+  }
+  while (!seq.done()) {
+    TileSeq nx = seq;
+    nx.next();
+    const int d = seq.d, t = seq.t;
+    float4 q_next;
+    const bool stage_next = kJlds && !nx.done() && threadIdx.x < kTileJ;
+    if (stage_next) q_next = X4[nx.row0() + threadIdx.x];  // lands during the arithmetic
+    float cx[kJ], cy[kJ], cz[kJ];
+    if constexpr (kJlds) {
+      sym::CSet<kJ> cs;
 #pragma unroll
-  for (int j = 0; j < kJ; ++j) {
-    const float4 q = X4[row0 + j * 64 + lane];
-    b.x[j] = q.x; b.y[j] = q.y; b.z[j] = q.z; b.mu[j] = q.w;
-    b.cx[j] = b.cy[j] = b.cz[j] = 0.f;
+      for (int j = 0; j < kJ; ++j) cs.cx[j] = cs.cy[j] = cs.cz[j] = 0.f;
+      sym::tile_lds<kI, kJ, SYM>(is, cs, jt[cur], a.eps2);
+#pragma unroll
+      for (int j = 0; j < kJ; ++j) { cx[j] = cs.cx[j]; cy[j] = cs.cy[j]; cz[j] = cs.cz[j]; }
+    } else {
+      sym::JSet<kJ> js;
+      const int64_t row0 = seq.row0();
+#pragma unroll
+      for (int j = 0; j < kJ; ++j) {
+        const float4 q = X4[row0 + j * 64 + lane];
+        js.x[j] = q.x; js.y[j] = q.y; js.z[j] = q.z; js.mu[j] = q.w;
+        js.cx[j] = js.cy[j] = js.cz[j] = 0.f;
+      }
+      sym::tile<kI, kJ, SYM>(is, js, a.eps2);
+#pragma unroll
+      for (int j = 0; j < kJ; ++j) { cx[j] = js.cx[j]; cy[j] = js.cy[j]; cz[j] = js.cz[j]; }
+    }
+    if constexpr (SYM) {
+#pragma unroll
+      for (int j = 0; j < kJ; ++j) {
+        slot[buf][w][0][j * 64 + lane] = cx[j];
+        slot[buf][w][1][j * 64 + lane] = cy[j];
+        slot[buf][w][2][j * 64 + lane] = cz[j];
+      }
+    }
+    // jt[cur ^ 1] was last read in the previous tile, before the previous barrier.
+    if (stage_next) stage_store(jt[cur ^ 1], threadIdx.x, q_next);
+    if (kJlds || SYM) __syncthreads();
+    if constexpr (SYM) {
+      // Sum the waves' carriers in wave order (fixed) and store the tile's j-side partial.
+      float* pj = a.Pj + ((int64_t)ar * a.H + (d - 1)) * 3 * kSymC;
+      for (int v = threadIdx.x; v < 3 * kTileJ; v += kThreads) {
+        const int c = v / kTileJ, b = v % kTileJ;
+        float acc = slot[buf][0][c][b];
+#pragma unroll
+        for (int u = 1; u < kW; ++u) acc += slot[buf][u][c][b];
+        pj[(int64_t)c * kSymC + t * kTileJ + b] = acc;
+      }
+      buf ^= 1;  // the other buffer was last read before this tile's barrier
+    }
+    cur ^= 1;
+    seq = nx;
   }
 }
 
 // One workgroup per unit (row a, segment s); s == S is the row's diagonal chunk.
-__global__ __launch_bounds__(kThreads) void force_sym_kernel(SymArgs a) {
-  __shared__ float slot[2][kW][3][kTile];  // j-side carriers of each wave, double-buffered
+__global__ __launch_bounds__(kThreads) GS_SYM_WPE void force_sym_kernel(SymArgs a) {
+  __shared__ SlotT slot;  // j-side carriers of each wave, double-buffered
+  __shared__ JtT jt;      // staged j-tiles (kJlds), double-buffered
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int ar = blockIdx.x / (a.S + 1), s = blockIdx.x % (a.S + 1);
   const int A = a.a0 + ar;
   if ((int64_t)A * kSymC >= a.n_real) return;  // all-ghost row: never read
   const float4* X4 = reinterpret_cast<const float4*>(a.X);
   sym::ISet<kI> is;
-  const int64_t i_row0 = (int64_t)A * kSymC + w * kTile;
+  const int64_t i_row0 = (int64_t)A * kSymC + w * kTileI;
 #pragma unroll
   for (int i = 0; i < kI; ++i) {
     const float4 q = X4[i_row0 + i * 64 + lane];
     is.x[i] = q.x; is.y[i] = q.y; is.z[i] = q.z; is.mu[i] = q.w;
     is.ax[i] = is.ay[i] = is.az[i] = 0.f;
   }
+  const bool diag = s == a.S;
+  TileSeq seq{A, a.NC, a.real_chunks, 0, 0, 0, diag};
   float* out;
-  if (s == a.S) {
-    // Diagonal chunk: all ordered pairs on the i side (the self term is 0 through the core).
-    for (int t = 0; t < kTilesPerChunk; ++t) {
-      sym::JSet<kJ> js;
-      load_jset(X4, (int64_t)A * kSymC + t * kTile, js);
-      sym::tile<kI, kJ, false>(is, js, a.eps2);
-    }
+  if (diag) {
+    // One pseudo-shell step: the 2048-body diagonal chunk (self term 0 through the core).
+    run_tiles<false>(a, is, seq, ar, slot, jt);
     out = a.Pd + (int64_t)ar * 3 * kSymC;
   } else {
     const int h = shell_len(A, a.NC);
     const int d0 = s * a.L + 1;
     if (d0 > h) return;
-    const int d1 = min(d0 + a.L - 1, h);
-    int buf = 0;
-    for (int d = d0; d <= d1; ++d) {
-      const int B = (A + d) % a.NC;
-      if (B >= a.real_chunks) continue;  // all-ghost column chunk: mu = 0, never read
-      float* pj = a.Pj + ((int64_t)ar * a.H + (d - 1)) * 3 * kSymC;
-      for (int t = 0; t < kTilesPerChunk; ++t) {
-        sym::JSet<kJ> js;
-        load_jset(X4, (int64_t)B * kSymC + t * kTile, js);
-        sym::tile<kI, kJ, true>(is, js, a.eps2);
-#pragma unroll
-        for (int j = 0; j < kJ; ++j) {
-          slot[buf][w][0][j * 64 + lane] = js.cx[j];
-          slot[buf][w][1][j * 64 + lane] = js.cy[j];
-          slot[buf][w][2][j * 64 + lane] = js.cz[j];
-        }
-        __syncthreads();
-        // Sum the 8 waves' carriers in wave order (fixed) and store the tile's j-side partial.
-        for (int v = threadIdx.x; v < 3 * kTile; v += kThreads) {
-          const int c = v / kTile, b = v % kTile;
-          float acc = slot[buf][0][c][b];
-#pragma unroll
-          for (int u = 1; u < kW; ++u) acc += slot[buf][u][c][b];
-          pj[(int64_t)c * kSymC + t * kTile + b] = acc;
-        }
-        buf ^= 1;  // the other buffer was last read before this tile's barrier
-      }
-    }
+    seq.d1 = min(d0 + a.L - 1, h);
+    seq.d = seq.valid(d0);
+    run_tiles<true>(a, is, seq, ar, slot, jt);
     out = a.Pi + ((int64_t)ar * a.S + s) * 3 * kSymC;
   }
 #pragma unroll
   for (int i = 0; i < kI; ++i) {
-    const int b = w * kTile + i * 64 + lane;
+    const int b = w * kTileI + i * 64 + lane;
     out[b] = is.ax[i];
     out[kSymC + b] = is.ay[i];
     out[2 * kSymC + b] = is.az[i];

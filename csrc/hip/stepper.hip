@@ -1042,6 +1042,16 @@ int gs_stepper_comm_init(gs_stepper* s, const void* id128, int32_t rank, int32_t
                        s->comm, s->s_comm));
       GS_NCCL(ncclGroupEnd());
     }
+    if (nranks > 1 && s->L.mode == GS_MODE_SYM) {
+      // The sym schedule's group-sum exchange talks to every peer: connect them all now.
+      GS_NCCL(ncclGroupStart());
+      for (int q = 0; q < nranks; ++q) {
+        if (q == rank) continue;
+        GS_NCCL(ncclSend(buf + (size_t)q * s->esz, 1, dt, q, s->comm, s->s_comm));
+        GS_NCCL(ncclRecv(buf + (size_t)(nranks + q) * s->esz, 1, dt, q, s->comm, s->s_comm));
+      }
+      GS_NCCL(ncclGroupEnd());
+    }
     GS_HIP(hipStreamSynchronize(s->s_comm));
   }
   return 0;

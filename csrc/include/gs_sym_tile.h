@@ -101,69 +101,76 @@ __device__ __forceinline__ f2 pk_fma(f2 a, f2 b, f2 c) { return __builtin_elemen
 #ifndef GS_SYM_U
 #define GS_SYM_U 2
 #endif
-template <int I, int J, bool SYM, int O>
-__device__ __forceinline__ void step(ISet<I>& a, JSet<J>& b, float eps2) {
+// All I i-bodies of the lane against one j-body (xj, yj, zj, mj): i-side accumulators updated;
+// with SYM the j side's sum over the lane's i-bodies is returned as t (two packed halves).
+template <int I, bool SYM>
+__device__ __forceinline__ void meet_j(ISet<I>& a, float xj, float yj, float zj, float mj,
+                                       float eps2, f2& tx, f2& ty, f2& tz) {
   static_assert(I % 2 == 0, "i-bodies are processed in pairs");
   // U i-pairs go through each stage together (stage-major source order), so consecutive
   // instructions are independent and the packed-result read hazard needs no s_nop.
   constexpr int U = (I / 2) % GS_SYM_U == 0 ? GS_SYM_U : 1;
 #pragma unroll
-  for (int j = 0; j < J; ++j) {
-    const float xj = row_from<O>(b.x[j]), yj = row_from<O>(b.y[j]);
-    const float zj = row_from<O>(b.z[j]), mj = row_from<O>(b.mu[j]);
-    f2 tx, ty, tz;
+  for (int i0 = 0; i0 < I; i0 += 2 * U) {
+    f2 dx[U], dy[U], dz[U], r2[U], y[U], y3[U];
 #pragma unroll
-    for (int i0 = 0; i0 < I; i0 += 2 * U) {
-      f2 dx[U], dy[U], dz[U], r2[U], y[U], y3[U];
+    for (int u = 0; u < U; ++u) {
+      const int i = i0 + 2 * u;
+      dx[u] = f2(xj) - f2{a.x[i], a.x[i + 1]};
+      dy[u] = f2(yj) - f2{a.y[i], a.y[i + 1]};
+      dz[u] = f2(zj) - f2{a.z[i], a.z[i + 1]};
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) r2[u] = pk_fma(dx[u], dx[u], f2(eps2));
+#pragma unroll
+    for (int u = 0; u < U; ++u) r2[u] = pk_fma(dy[u], dy[u], r2[u]);
+#pragma unroll
+    for (int u = 0; u < U; ++u) r2[u] = pk_fma(dz[u], dz[u], r2[u]);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      y[u].x = __builtin_amdgcn_rsqf(r2[u].x);
+      y[u].y = __builtin_amdgcn_rsqf(r2[u].y);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) y3[u] = y[u] * y[u];
+#pragma unroll
+    for (int u = 0; u < U; ++u) y3[u] = y3[u] * y[u];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = i0 + 2 * u;
+      const f2 si = f2(mj) * y3[u];
+      f2 ax = {a.ax[i], a.ax[i + 1]}, ay = {a.ay[i], a.ay[i + 1]}, az = {a.az[i], a.az[i + 1]};
+      ax = pk_fma(si, dx[u], ax);
+      ay = pk_fma(si, dy[u], ay);
+      az = pk_fma(si, dz[u], az);
+      a.ax[i] = ax.x; a.ax[i + 1] = ax.y;
+      a.ay[i] = ay.x; a.ay[i + 1] = ay.y;
+      a.az[i] = az.x; a.az[i + 1] = az.y;
+    }
+    if constexpr (SYM) {
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int i = i0 + 2 * u;
-        dx[u] = f2(xj) - f2{a.x[i], a.x[i + 1]};
-        dy[u] = f2(yj) - f2{a.y[i], a.y[i + 1]};
-        dz[u] = f2(zj) - f2{a.z[i], a.z[i + 1]};
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) r2[u] = pk_fma(dx[u], dx[u], f2(eps2));
-#pragma unroll
-      for (int u = 0; u < U; ++u) r2[u] = pk_fma(dy[u], dy[u], r2[u]);
-#pragma unroll
-      for (int u = 0; u < U; ++u) r2[u] = pk_fma(dz[u], dz[u], r2[u]);
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        y[u].x = __builtin_amdgcn_rsqf(r2[u].x);
-        y[u].y = __builtin_amdgcn_rsqf(r2[u].y);
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) y3[u] = y[u] * y[u];
-#pragma unroll
-      for (int u = 0; u < U; ++u) y3[u] = y3[u] * y[u];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int i = i0 + 2 * u;
-        const f2 si = f2(mj) * y3[u];
-        f2 ax = {a.ax[i], a.ax[i + 1]}, ay = {a.ay[i], a.ay[i + 1]}, az = {a.az[i], a.az[i + 1]};
-        ax = pk_fma(si, dx[u], ax);
-        ay = pk_fma(si, dy[u], ay);
-        az = pk_fma(si, dz[u], az);
-        a.ax[i] = ax.x; a.ax[i + 1] = ax.y;
-        a.ay[i] = ay.x; a.ay[i + 1] = ay.y;
-        a.az[i] = az.x; a.az[i + 1] = az.y;
-      }
-      if constexpr (SYM) {
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const int i = i0 + 2 * u;
-          const f2 sj = f2{a.mu[i], a.mu[i + 1]} * y3[u];
-          if (i == 0) {
-            tx = sj * dx[u]; ty = sj * dy[u]; tz = sj * dz[u];
-          } else {
-            tx = pk_fma(sj, dx[u], tx);
-            ty = pk_fma(sj, dy[u], ty);
-            tz = pk_fma(sj, dz[u], tz);
-          }
+        const f2 sj = f2{a.mu[i], a.mu[i + 1]} * y3[u];
+        if (i == 0) {
+          tx = sj * dx[u]; ty = sj * dy[u]; tz = sj * dz[u];
+        } else {
+          tx = pk_fma(sj, dx[u], tx);
+          ty = pk_fma(sj, dy[u], ty);
+          tz = pk_fma(sj, dz[u], tz);
         }
       }
     }
+  }
+}
+
+template <int I, int J, bool SYM, int O>
+__device__ __forceinline__ void step(ISet<I>& a, JSet<J>& b, float eps2) {
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    f2 tx, ty, tz;
+    meet_j<I, SYM>(a, row_from<O>(b.x[j]), row_from<O>(b.y[j]), row_from<O>(b.z[j]),
+                   row_from<O>(b.mu[j]), eps2, tx, ty, tz);
     if constexpr (SYM) {
       // carrier of lane l-1 (the j this lane just met) moves here and takes -t.
       b.cx[j] = row_from<1>(b.cx[j]) - (tx.x + tx.y);
@@ -204,6 +211,73 @@ __device__ __forceinline__ void tile(ISet<I>& a, JSet<J>& b, float eps2) {
   for (int p = 0; p < 4; ++p) {
     row_pass<I, J, SYM>(a, b, eps2, std::make_integer_sequence<int, 16>{});
     next_row<J, SYM>(b, addr);
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// LDS-position variant: the j positions are not held in registers and rotated with DPP;
+// the workgroup stages each j-tile once into LDS and every lane reads the body it meets with
+// one ds_read_b128 per j and step (the LDS pipe, not the VALU). Only the carriers rotate
+// (DPP row_ror:1 each step, ds_bpermute by 16 lanes each phase), so per j and step the VALU
+// overhead drops from 4 v_mov_dpp + 3 v_add + 3 v_sub_dpp to 3 v_add + 3 v_sub_dpp, and the
+// 4*J position registers are freed.
+//
+// Staged layout, [J][4 row groups][32] float4: body (slot j, lane 16 g + c') is stored at
+// entries 15 - c' and 31 - c' of (j, g). At phase p (row group data shifted by p) and step k,
+// lane 16 R + c meets lane 16 ((R - p) & 3) + ((c - k - 1) & 15) (DPP row_ror:n reads lane
+// l - n of the row; verified on gfx950), which sits at entry 16 - c + k in [1, 31]: a
+// per-phase base address plus the immediate offset k.
+template <int J>
+struct CSet {
+  float cx[J], cy[J], cz[J];
+};
+
+constexpr int kStagedRows = 128;  // float4 rows per j-slot in the staged layout
+
+__device__ __forceinline__ int staged_entry(int lane_src, int copy) {
+  const int g = lane_src >> 4, c = lane_src & 15;
+  return g * 32 + (copy ? 31 - c : 15 - c);
+}
+
+template <int I, int J, bool SYM, int K>
+__device__ __forceinline__ void lds_step(ISet<I>& a, CSet<J>& c, const float4* base, float eps2) {
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    const float4 q = base[j * kStagedRows + K];
+    f2 tx, ty, tz;
+    meet_j<I, SYM>(a, q.x, q.y, q.z, q.w, eps2, tx, ty, tz);
+    if constexpr (SYM) {
+      c.cx[j] = row_from<1>(c.cx[j]) - (tx.x + tx.y);
+      c.cy[j] = row_from<1>(c.cy[j]) - (ty.x + ty.y);
+      c.cz[j] = row_from<1>(c.cz[j]) - (tz.x + tz.y);
+    }
+  }
+}
+
+template <int I, int J, bool SYM, int... Ks>
+__device__ __forceinline__ void lds_row_pass(ISet<I>& a, CSet<J>& c, const float4* base,
+                                             float eps2, std::integer_sequence<int, Ks...>) {
+  (lds_step<I, J, SYM, Ks>(a, c, base, eps2), ...);
+}
+
+// All (64 I) x (64 J) pairs against the staged j-tile `tile` (LDS). Carriers return home.
+template <int I, int J, bool SYM>
+__device__ __forceinline__ void tile_lds(ISet<I>& a, CSet<J>& c, const float4* tile, float eps2) {
+  const int lane = static_cast<int>(__lane_id());
+  const int R = lane >> 4, col = lane & 15;
+  const int addr = ((lane + 48) & 63) << 2;
+#pragma unroll 1
+  for (int p = 0; p < 4; ++p) {
+    const float4* base = tile + ((R - p) & 3) * 32 + (16 - col);
+    lds_row_pass<I, J, SYM>(a, c, base, eps2, std::make_integer_sequence<int, 16>{});
+    if constexpr (SYM) {
+#pragma unroll
+      for (int j = 0; j < J; ++j) {
+        c.cx[j] = wave_from_minus16(c.cx[j], addr);
+        c.cy[j] = wave_from_minus16(c.cy[j], addr);
+        c.cz[j] = wave_from_minus16(c.cz[j], addr);
+      }
+    }
   }
 }
 

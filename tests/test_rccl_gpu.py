@@ -78,7 +78,7 @@ def test_rccl_two_ranks_match_single_rank(hip, tmp_path, strategy):
 
 
 @pytest.mark.parametrize("graph,strategy", [(1, "allgather"), (2, "allgather"), (1, "ring"),
-                                            (2, "ring")])
+                                            (2, "ring"), (1, "sym"), (2, "sym")])
 def test_rccl_one_rank_full_schedule_bitwise(hip, monkeypatch, graph, strategy):
     """A live 1-rank RCCL communicator drives the whole multi-rank step (in-place
     ncclAllGather, concurrent local/remote split, ordered reduce) — eagerly and captured into
@@ -87,7 +87,10 @@ def test_rccl_one_rank_full_schedule_bitwise(hip, monkeypatch, graph, strategy):
     from gravsim.runtime.engines import HipEngine
 
     monkeypatch.setenv("GRAVSIM_FORCE_COMM", "1")
-    cfg = SimConfig(n=6000, dtype="fp32", device="gpu", chunk=1024, strategy=strategy)
+    # "sym": the Newton-3 schedule (all-gather, then the group-sum exchange through RCCL).
+    mode = "sym" if strategy == "sym" else "auto"
+    cfg = SimConfig(n=6000, dtype="fp32", device="gpu", chunk=1024, mode=mode,
+                    strategy="allgather" if strategy == "sym" else strategy)
     eng = HipEngine(cfg)
     eng.lib.gs_stepper_destroy(eng._s)  # rebuild with the requested graph mode
     import ctypes
