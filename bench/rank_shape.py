@@ -28,6 +28,7 @@ def main() -> int:
     ap.add_argument("--ipl", default="0", help="comma list")
     ap.add_argument("--kernel", default="auto", help="comma list")
     ap.add_argument("--strategy", default="allgather", help="comma list: allgather,ring")
+    ap.add_argument("--mode", default="auto", help="comma list: auto,split,sym")
     a = ap.parse_args()
     import torch  # noqa: F401
 
@@ -40,10 +41,10 @@ def main() -> int:
 
     grid = list(itertools.product([int(x) for x in a.ranks.split(",")],
                                   [int(x) for x in a.ipl.split(",")], a.kernel.split(","),
-                                  a.strategy.split(",")))
-    for P, ipl, kernel, strategy in grid:
+                                  a.strategy.split(","), a.mode.split(",")))
+    for P, ipl, kernel, strategy, mode in grid:
         cfg = SimConfig(n=a.n, dtype=a.dtype, device="gpu", ipl=ipl, kernel=kernel,
-                        strategy=strategy)
+                        strategy=strategy, mode=mode)
         r = P - 1 if P > 1 else 0  # a rank with its own chunks at the end
         e = HipEngine(cfg, r, P)
         e.init_ics("solar+random", cfg.seed)
@@ -55,7 +56,7 @@ def main() -> int:
         ms = 1e3 * (time.perf_counter() - t0) / a.steps
         base = base or ms * P
         print(json.dumps(dict(P=P, rank=r, n=a.n, dtype=a.dtype, ipl=ipl, kernel=kernel,
-                              strategy=strategy, ms_per_step=ms,
+                              strategy=strategy, mode=e.native_layout["mode"], ms_per_step=ms,
                               predicted_efficiency=base / (P * ms),
                               predicted_body_updates_per_s=a.n / (ms * 1e-3),
                               layout=e.native_layout)), flush=True)

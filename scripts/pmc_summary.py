@@ -11,7 +11,8 @@ for path in glob.glob(sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc_*/**
                       recursive=True):
     for r in csv.DictReader(open(path)):
         name = r.get("Kernel_Name", "")
-        if "force_split_kernel" not in name and "force_fused_kernel" not in name:
+        if not any(k in name for k in ("force_split_kernel", "force_fused_kernel",
+                                       "force_sym_kernel")):
             continue
         kern[name] += 1
         rows[r["Counter_Name"]] += float(r["Counter_Value"])
