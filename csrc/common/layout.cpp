@@ -39,18 +39,19 @@ extern "C" int gs_layout_compute(const gs_config* cfg, gs_layout* out) {
   out->n_pad = gs::round_up(cfg->n, (int64_t)cfg->nranks * chunk);
   // Newton-3 symmetric schedule (fp32, fast cutoff, P | 8). Its chunk/row/group structure
   // must not depend on P, so the padding is the one an 8-rank run would use.
-  const bool sym_ok = cfg->dtype == GS_FP32 && cfg->cutoff_mode != 1 && 8 % cfg->nranks == 0 &&
+  const bool sym_ok = cfg->cutoff_mode != 1 && 8 % cfg->nranks == 0 &&
                       cfg->kernel != GS_KERNEL_MFMA;
   if (cfg->mode == GS_MODE_SYM && !sym_ok) {
-    gs_set_error("layout: the sym schedule is fp32, fast-cutoff, with nranks dividing 8");
+    gs_set_error("layout: the sym schedule needs the fast cutoff and nranks dividing 8");
     return -1;
   }
   const int64_t sym_unit = 8 * (int64_t)(chunk % 2048 == 0 ? chunk : 2 * chunk);
   const int64_t sym_pad = gs::round_up(cfg->n, sym_unit);
   bool sym = cfg->mode == GS_MODE_SYM;
   if (cfg->mode == GS_MODE_AUTO && sym_ok && cfg->n >= 262144 && sym_pad * 20 <= out->n_pad * 21) {
-    // Partial buffers: n_local * (S + H) * 12 B (gs_sym_bytes); keep well inside 288 GB.
-    sym = gs_sym_bytes(sym_pad, cfg->nranks) <= ((int64_t)96 << 30);
+    // Partial buffers: n_local * (S + H) * 3 elements (gs_sym_bytes); keep them well
+    // inside the 288 GB of HBM.
+    sym = gs_sym_bytes(sym_pad, cfg->nranks, cfg->dtype == GS_FP64 ? 8 : 4) <= ((int64_t)160 << 30);
   }
   if (sym) out->n_pad = sym_pad;
   out->n_local = out->n_pad / cfg->nranks;
@@ -122,12 +123,12 @@ extern "C" int gs_sym_geometry(int64_t n_pad, int32_t* NC, int32_t* H, int32_t* 
   return 0;
 }
 
-extern "C" int64_t gs_sym_bytes(int64_t n_pad, int32_t nranks) {
+extern "C" int64_t gs_sym_bytes(int64_t n_pad, int32_t nranks, int32_t esz) {
   int32_t nc, h, l, sg;
   if (gs_sym_geometry(n_pad, &nc, &h, &l, &sg)) return -1;
   const int64_t n_local = n_pad / nranks;
-  // Pi + Pj + Pd (3 floats per body per slot) + two group-sum buffers (8 groups x 3 floats)
-  return n_local * 12 * ((int64_t)sg + h + 1) + 2 * n_local * 8 * 12;
+  // Pi + Pj + Pd (3 elements per body per slot) + two group-sum buffers (8 groups x 3)
+  return n_local * 3 * esz * ((int64_t)sg + h + 1) + 2 * n_local * 8 * 3 * esz;
 }
 
 extern "C" void gs_ic_fill_host(int32_t ic, uint64_t seed, int64_t n, int64_t begin, int64_t end,

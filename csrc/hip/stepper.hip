@@ -95,11 +95,11 @@ struct gs_stepper {
   int cus = 256;               // compute units
   int occ[3] = {0, 0, 0};      // split-kernel workgroups per CU by force mode
   // Newton-3 symmetric schedule (GS_MODE_SYM): partial slots, group sums, geometry.
-  float* sym_Pi = nullptr;
-  float* sym_Pj = nullptr;
-  float* sym_Pd = nullptr;
-  float* sym_S = nullptr;  // group sums by destination rank
-  float* sym_R = nullptr;  // group sums by source rank (== sym_S with one rank)
+  char* sym_Pi = nullptr;  // element type: float or double (esz)
+  char* sym_Pj = nullptr;
+  char* sym_Pd = nullptr;
+  char* sym_S = nullptr;  // group sums by destination rank
+  char* sym_R = nullptr;  // group sums by source rank (== sym_S with one rank)
   int32_t sym_NC = 0, sym_H = 0, sym_L = 0, sym_S_n = 0;
   hipEvent_t ev_sym = nullptr;
 };
@@ -165,14 +165,16 @@ gs::KArgs<T> base_args(gs_stepper* s, int cur) {
   return a;
 }
 
-bool use_sym(const gs_stepper* s) { return s->L.mode == GS_MODE_SYM && !s->exact; }
+// The sym kernels implement both cutoff paths (fast core and exact select).
+bool use_sym(const gs_stepper* s) { return s->L.mode == GS_MODE_SYM; }
 
 gs::SymArgs sym_args(gs_stepper* s, int cur) {
   gs::SymArgs a;
   memset(&a, 0, sizeof(a));
-  a.X = static_cast<const float*>(s->X[cur]);
-  a.X_next = static_cast<float*>(s->X[cur ^ 1]);
-  a.vel = static_cast<float*>(s->vel);
+  a.X = s->X[cur];
+  a.X_next = s->X[cur ^ 1];
+  a.vel = s->vel;
+  a.fp64 = s->esz == 8;
   a.Pi = s->sym_Pi;
   a.Pj = s->sym_Pj;
   a.Pd = s->sym_Pd;
@@ -189,8 +191,10 @@ gs::SymArgs sym_args(gs_stepper* s, int cur) {
   a.L = s->sym_L;
   a.H = s->sym_H;
   a.real_chunks = (int32_t)((s->L.n + gs::kSymC - 1) / gs::kSymC);
-  a.dt = (float)s->cfg.dt;
-  a.eps2 = (float)s->eps2;
+  a.dt = s->cfg.dt;
+  a.eps2 = s->eps2;
+  a.exact = s->exact ? 1 : 0;
+  a.cut2 = s->cfg.cutoff * s->cfg.cutoff;
   return a;
 }
 
@@ -198,17 +202,19 @@ gs::SymArgs sym_args(gs_stepper* s, int cur) {
 // bodies of rank q to q (ncclSend/ncclRecv pairs, one group call) and keeps its own block.
 int sym_exchange_rccl(gs_stepper* s) {
   const int P = s->cfg.nranks, r = s->cfg.rank;
-  const size_t cnt = (size_t)(gs::kSymGroups / P) * 3 * s->L.n_local;
+  const size_t cnt = (size_t)(gs::kSymGroups / P) * 3 * s->L.n_local;  // elements
+  const size_t bytes = cnt * s->esz;
+  const ncclDataType_t dt = s->esz == 8 ? ncclFloat64 : ncclFloat32;
   GS_HIP(hipEventRecord(s->ev_ready, s->s_comp));
   GS_HIP(hipStreamWaitEvent(s->s_comm, s->ev_ready, 0));
-  GS_HIP(hipMemcpyAsync(s->sym_R + (size_t)r * cnt, s->sym_S + (size_t)r * cnt, cnt * 4,
+  GS_HIP(hipMemcpyAsync(s->sym_R + (size_t)r * bytes, s->sym_S + (size_t)r * bytes, bytes,
                         hipMemcpyDeviceToDevice, s->s_comm));
   if (P > 1) {
     GS_NCCL(ncclGroupStart());
     for (int q = 0; q < P; ++q) {
       if (q == r) continue;
-      GS_NCCL(ncclSend(s->sym_S + (size_t)q * cnt, cnt, ncclFloat32, q, s->comm, s->s_comm));
-      GS_NCCL(ncclRecv(s->sym_R + (size_t)q * cnt, cnt, ncclFloat32, q, s->comm, s->s_comm));
+      GS_NCCL(ncclSend(s->sym_S + (size_t)q * bytes, cnt, dt, q, s->comm, s->s_comm));
+      GS_NCCL(ncclRecv(s->sym_R + (size_t)q * bytes, cnt, dt, q, s->comm, s->s_comm));
     }
     GS_NCCL(ncclGroupEnd());
   }
@@ -221,12 +227,13 @@ int ensure_sym(gs_stepper* s) {
   if (s->L.mode != GS_MODE_SYM || s->sym_Pi) return 0;
   if (gs_sym_geometry(s->L.n_pad, &s->sym_NC, &s->sym_H, &s->sym_L, &s->sym_S_n)) return -1;
   const size_t nl = (size_t)s->L.n_local, rows = (size_t)s->sym_NC / s->cfg.nranks;
-  GS_HIP(hipMalloc(&s->sym_Pi, rows * s->sym_S_n * 3 * gs::kSymC * sizeof(float)));
-  GS_HIP(hipMalloc(&s->sym_Pj, rows * s->sym_H * 3 * gs::kSymC * sizeof(float)));
-  GS_HIP(hipMalloc(&s->sym_Pd, rows * 3 * gs::kSymC * sizeof(float)));
-  GS_HIP(hipMalloc(&s->sym_S, (size_t)gs::kSymGroups * 3 * nl * sizeof(float)));
+  const size_t e = s->esz;
+  GS_HIP(hipMalloc(&s->sym_Pi, rows * s->sym_S_n * 3 * gs::kSymC * e));
+  GS_HIP(hipMalloc(&s->sym_Pj, rows * s->sym_H * 3 * gs::kSymC * e));
+  GS_HIP(hipMalloc(&s->sym_Pd, rows * 3 * gs::kSymC * e));
+  GS_HIP(hipMalloc(&s->sym_S, (size_t)gs::kSymGroups * 3 * nl * e));
   if (s->cfg.nranks > 1)
-    GS_HIP(hipMalloc(&s->sym_R, (size_t)gs::kSymGroups * 3 * nl * sizeof(float)));
+    GS_HIP(hipMalloc(&s->sym_R, (size_t)gs::kSymGroups * 3 * nl * e));
   else
     s->sym_R = s->sym_S;
   return 0;
@@ -395,14 +402,12 @@ int enqueue_step(gs_stepper* s, bool capturing, bool gathered_externally) {
   const bool timed = s->timed && !capturing;
   if (timed) GS_HIP(hipEventRecord(s->ev_t0, s->s_comp));
   const bool need_gather = (s->have_comm || s->virt) && !s->full[cur];
-  if constexpr (sizeof(T) == 4) {
-    if (use_sym(s)) {
-      if (enqueue_sym(s, cur, need_gather, gathered_externally, 3, timed)) return -1;
-      if (timed) GS_HIP(hipEventRecord(s->ev_end, s->s_comp));
-      s->full[cur ^ 1] = !(s->have_comm || s->virt);
-      s->k += 1;
-      return 0;
-    }
+  if (use_sym(s)) {
+    if (enqueue_sym(s, cur, need_gather, gathered_externally, 3, timed)) return -1;
+    if (timed) GS_HIP(hipEventRecord(s->ev_end, s->s_comp));
+    s->full[cur ^ 1] = !(s->have_comm || s->virt);
+    s->k += 1;
+    return 0;
   }
   const bool ring = s->cfg.strategy == GS_STRATEGY_RING;
   if (need_gather && ring && (s->emulate || !gathered_externally)) {
@@ -565,21 +570,21 @@ int accel_impl(gs_stepper* s, double* acc4, bool step_path) {
   }
   if (gather(s, cur)) return -1;
   if (s->have_comm) GS_HIP(hipStreamWaitEvent(s->s_comp, s->ev_gathered, 0));
-  if constexpr (sizeof(T) == 4) {
+  {
     if (step_path && use_sym(s)) {
       if (s->virt && s->cfg.nranks > 1) {
         gs_set_error("accel: the sym step path of a virtual-rank shard needs the group");
         return -1;
       }
       gs::SymArgs sa = sym_args(s, cur);
-      sa.acc_out = static_cast<float*>(s->acc);
+      sa.acc_out = s->acc;
       GS_HIP(gs::launch_force_sym(sa, s->s_comp));
       GS_HIP(gs::launch_sym_group_reduce(sa, s->s_comp));
       if (s->have_comm && sym_exchange_rccl(s)) return -1;
       GS_HIP(gs::launch_sym_finalize(sa, s->s_comp));
       GS_HIP(hipStreamSynchronize(s->s_comp));
-      std::vector<float> A((size_t)s->L.n_local * 4);
-      GS_HIP(hipMemcpy(A.data(), s->acc, A.size() * sizeof(float), hipMemcpyDeviceToHost));
+      std::vector<T> A((size_t)s->L.n_local * 4);
+      GS_HIP(hipMemcpy(A.data(), s->acc, A.size() * sizeof(T), hipMemcpyDeviceToHost));
       for (size_t i = 0; i < A.size(); ++i) acc4[i] = (double)A[i];
       return 0;
     }
@@ -763,8 +768,6 @@ int gs_stepper_get_state(gs_stepper* s, double* pos, double* vel, double* mass) 
 
 int gs_stepper_step(gs_stepper* s, int32_t nsteps) {
   GS_HIP(hipSetDevice(s->cfg.device));
-  // A sym layout whose masses resolved to the exact-cutoff path runs the split schedule.
-  if (s->L.mode == GS_MODE_SYM && s->exact && ensure_partial(s)) return -1;
   if (s->cfg.nranks > 1 && !s->have_comm && !s->emulate) {
     gs_set_error("step: nranks > 1 but no RCCL communicator (call gs_stepper_comm_init)");
     return -1;
@@ -976,7 +979,7 @@ int gs_group_step(gs_stepper** sh, int32_t P, int32_t nsteps) {
     if (use_sym(sh[0]) && P > 1) {
       // Symmetric schedule: force + group reduce on every shard, then the group-sum
       // exchange as device copies (shard r's block for q -> shard q's slot r), then finalize.
-      const size_t cnt = (size_t)(gs::kSymGroups / P) * 3 * sh[0]->L.n_local;
+      const size_t cnt = (size_t)(gs::kSymGroups / P) * 3 * sh[0]->L.n_local * sh[0]->esz;
       for (int r = 0; r < P; ++r)
         if (enqueue_sym(sh[r], cur, need, true, 1, false)) return -1;
       for (int r = 0; r < P; ++r) GS_HIP(hipEventRecord(sh[r]->ev_ready, sh[r]->s_comp));
@@ -984,7 +987,7 @@ int gs_group_step(gs_stepper** sh, int32_t P, int32_t nsteps) {
       for (int q = 0; q < P; ++q)
         for (int r = 0; r < P; ++r)
           GS_HIP(hipMemcpyAsync(sh[q]->sym_R + (size_t)r * cnt, sh[r]->sym_S + (size_t)q * cnt,
-                                cnt * sizeof(float), hipMemcpyDeviceToDevice, gsm));
+                                cnt, hipMemcpyDeviceToDevice, gsm));
       GS_HIP(hipEventRecord(sh[0]->ev_sym, gsm));
       for (int r = 0; r < P; ++r) {
         GS_HIP(hipStreamWaitEvent(sh[r]->s_comp, sh[0]->ev_sym, 0));
@@ -1016,8 +1019,7 @@ int gs_stepper_comm_init(gs_stepper* s, const void* id128, int32_t rank, int32_t
   GS_HIP(hipSetDevice(s->cfg.device));
   ncclUniqueId id;
   memcpy(&id, id128, sizeof(id));
-  // The one-sided multi-rank schedule is always split (the sym layout falls back to it only
-  // when its masses resolve to the exact-cutoff path, see gs_stepper_step).
+  // The one-sided multi-rank schedule is always split (the sym schedule has its own slots).
   if (s->L.mode != GS_MODE_SYM && ensure_partial(s)) return -1;
   GS_NCCL(ncclCommInitRank(&s->comm, nranks, id, rank));
   // GRAVSIM_FORCE_COMM keeps a 1-rank communicator live so the full multi-rank schedule

@@ -35,7 +35,7 @@ inline int split_span(const KArgs<T>& a) {
   return (a.c_end - a.c_begin) - (se - sb);
 }
 
-// ---- Newton-3 symmetric schedule (fp32, fast cutoff; nbody_sym.hip) -------------------
+// ---- Newton-3 symmetric schedule (fp32/fp64, fast cutoff; nbody_sym.hip) -------------
 // Canonical decomposition, a function of the padded body count only (so every rank count
 // P | 8 produces the same bits): chunks of kSymC = 2048 bodies, NC = n_pad / 2048 of them,
 // G = 8 row groups of NC / 8 chunks. Chunk A pairs with the next h(A) chunks cyclically
@@ -49,24 +49,27 @@ constexpr int kSymC = 2048;
 constexpr int kSymGroups = 8;
 
 struct SymArgs {
-  const float* X;      // [n_pad * 4] gathered positions (x, y, z, mu)
-  float* Pi;           // [rows][S][3][kSymC] i-side partials
-  float* Pj;           // [rows][H][3][kSymC] j-side partials, H = NC / 2
-  float* Pd;           // [rows][3][kSymC] diagonal-chunk partials
-  float* Sbuf;         // [P][G/P][3][n_local] group sums by destination rank
-  const float* Rbuf;   // [P][G/P][3][n_local] group sums received, by source rank
-  float* X_next;       // [n_pad * 4]
-  float* vel;          // [n_local * 4]
-  float* acc_out;      // optional [n_local * 4]: emit accelerations instead of integrating
+  // Arrays are float (fp32 run) or double (fp64 run); the launchers pick the instantiation.
+  const void* X;       // [n_pad * 4] gathered positions (x, y, z, mu)
+  void* Pi;            // [rows][S][3][kSymC] i-side partials
+  void* Pj;            // [rows][H][3][kSymC] j-side partials, H = NC / 2
+  void* Pd;            // [rows][3][kSymC] diagonal-chunk partials
+  void* Sbuf;          // [P][G/P][3][n_local] group sums by destination rank
+  const void* Rbuf;    // [P][G/P][3][n_local] group sums received, by source rank
+  void* X_next;        // [n_pad * 4]
+  void* vel;           // [n_local * 4]
+  void* acc_out;       // optional [n_local * 4]: emit accelerations instead of integrating
   int64_t n_real, n_local, i_begin;
   int32_t NC, a0, rows, S, L, H, P, real_chunks;
-  float dt, eps2;
+  int32_t fp64;        // element type of every array above
+  int32_t exact;       // reference hard cutoff (select at cut2) instead of the fast core
+  double dt, eps2, cut2;
 };
 
 hipError_t launch_force_sym(const SymArgs& a, hipStream_t s);
 hipError_t launch_sym_group_reduce(const SymArgs& a, hipStream_t s);
 hipError_t launch_sym_finalize(const SymArgs& a, hipStream_t s);
-int sym_occupancy();
+int sym_occupancy(int fp64);
 
 template <typename T>
 hipError_t launch_force_split(const KArgs<T>& a, int kernel, int ipl, int groups, hipStream_t s);

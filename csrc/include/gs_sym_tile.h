@@ -26,6 +26,9 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <stdint.h>
+
+#include <type_traits>
 #include <utility>
 
 namespace gs {
@@ -71,11 +74,33 @@ __device__ __forceinline__ float wave_from_minus16(float v, int addr) {
                             __builtin_amdgcn_ds_bpermute(addr, __builtin_bit_cast(int, v)));
 }
 
-template <int I>
-struct ISet {
-  float x[I], y[I], z[I], mu[I];
-  float ax[I], ay[I], az[I];
+// fp64 counterparts of the cross-lane moves: one DPP / bpermute per 32-bit half.
+template <int O>
+__device__ __forceinline__ double row_from(double v) {
+  if constexpr (O % 16 == 0) {
+    return v;
+  } else {
+    const uint64_t u = __builtin_bit_cast(uint64_t, v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)u, 0x120 + O, 0xf, 0xf, true);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(u >> 32), 0x120 + O, 0xf, 0xf, true);
+    return __builtin_bit_cast(double, ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+  }
+}
+
+__device__ __forceinline__ double wave_from_minus16(double v, int addr) {
+  const uint64_t u = __builtin_bit_cast(uint64_t, v);
+  const int lo = __builtin_amdgcn_ds_bpermute(addr, (int)(uint32_t)u);
+  const int hi = __builtin_amdgcn_ds_bpermute(addr, (int)(uint32_t)(u >> 32));
+  return __builtin_bit_cast(double, ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+
+template <typename T, int I>
+struct ISetT {
+  T x[I], y[I], z[I], mu[I];
+  T ax[I], ay[I], az[I];
 };
+template <int I>
+using ISet = ISetT<float, I>;
 
 template <int J>
 struct JSet {
@@ -103,9 +128,11 @@ __device__ __forceinline__ f2 pk_fma(f2 a, f2 b, f2 c) { return __builtin_elemen
 #endif
 // All I i-bodies of the lane against one j-body (xj, yj, zj, mj): i-side accumulators updated;
 // with SYM the j side's sum over the lane's i-bodies is returned as t (two packed halves).
-template <int I, bool SYM>
+// EXACT: the reference hard cutoff (cuda.cu:39, mpi.c:64), r^-3 := 0 when r^2 < cut2, so
+// the pair contributes to neither side (also removes the self term of diagonal tiles).
+template <int I, bool SYM, bool EXACT = false>
 __device__ __forceinline__ void meet_j(ISet<I>& a, float xj, float yj, float zj, float mj,
-                                       float eps2, f2& tx, f2& ty, f2& tz) {
+                                       float eps2, f2& tx, f2& ty, f2& tz, float cut2 = 0.f) {
   static_assert(I % 2 == 0, "i-bodies are processed in pairs");
   // U i-pairs go through each stage together (stage-major source order), so consecutive
   // instructions are independent and the packed-result read hazard needs no s_nop.
@@ -135,6 +162,13 @@ __device__ __forceinline__ void meet_j(ISet<I>& a, float xj, float yj, float zj,
     for (int u = 0; u < U; ++u) y3[u] = y[u] * y[u];
 #pragma unroll
     for (int u = 0; u < U; ++u) y3[u] = y3[u] * y[u];
+    if constexpr (EXACT) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        y3[u].x = r2[u].x >= cut2 ? y3[u].x : 0.f;
+        y3[u].y = r2[u].y >= cut2 ? y3[u].y : 0.f;
+      }
+    }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int i = i0 + 2 * u;
@@ -227,49 +261,111 @@ __device__ __forceinline__ void tile(ISet<I>& a, JSet<J>& b, float eps2) {
 // lane 16 R + c meets lane 16 ((R - p) & 3) + ((c - k - 1) & 15) (DPP row_ror:n reads lane
 // l - n of the row; verified on gfx950), which sits at entry 16 - c + k in [1, 31]: a
 // per-phase base address plus the immediate offset k.
-template <int J>
-struct CSet {
-  float cx[J], cy[J], cz[J];
+template <typename T, int J>
+struct CSetT {
+  T cx[J], cy[J], cz[J];
 };
+template <int J>
+using CSet = CSetT<float, J>;
 
-constexpr int kStagedRows = 128;  // float4 rows per j-slot in the staged layout
+template <typename T>
+using Vec4 = typename std::conditional<sizeof(T) == 4, float4, double4>::type;
+
+constexpr int kStagedRows = 128;  // V4 rows per j-slot in the staged layout
 
 __device__ __forceinline__ int staged_entry(int lane_src, int copy) {
   const int g = lane_src >> 4, c = lane_src & 15;
   return g * 32 + (copy ? 31 - c : 15 - c);
 }
 
-template <int I, int J, bool SYM, int K>
-__device__ __forceinline__ void lds_step(ISet<I>& a, CSet<J>& c, const float4* base, float eps2) {
+// fp64 pair arithmetic (no packed f64 VALU on gfx950): the integrator's own fp64 formula
+// (nbody_kernels.hip interact, step path): y0 = v_rsq_f64(r^2), e = 1 - r^2 y0^2,
+// r^-3 = y0^3 (1 + 3/2 e + 15/8 e^2) with |e| <= 1.1e-7, i.e. double-precision r^-3;
+// w = r^-3 then feeds both sides: 20 f64 ops + 1 v_rsq_f64 per pair (two interactions)
+// against 2 x (16 + 1) one-sided.
+template <int I, bool SYM, bool EXACT = false>
+__device__ __forceinline__ void meet_j(ISetT<double, I>& a, double xj, double yj, double zj,
+                                       double mj, double eps2, double& tx, double& ty,
+                                       double& tz, double cut2 = 0.0) {
+  // Opaque constants (loop-invariant, eps2 finite): kept in VGPRs instead of being
+  // re-materialised per pair (1.5 and 1.875 are not inline f64 constants).
+  const double c15 = 1.5 + eps2 * 0.0, c1875 = 1.875 + eps2 * 0.0;
 #pragma unroll
-  for (int j = 0; j < J; ++j) {
-    const float4 q = base[j * kStagedRows + K];
-    f2 tx, ty, tz;
-    meet_j<I, SYM>(a, q.x, q.y, q.z, q.w, eps2, tx, ty, tz);
+  for (int i = 0; i < I; ++i) {
+    const double dx = xj - a.x[i], dy = yj - a.y[i], dz = zj - a.z[i];
+    const double r2 = __builtin_fma(dz, dz, __builtin_fma(dy, dy, __builtin_fma(dx, dx, eps2)));
+    // EXACT (reference hard cutoff): the pair's r^-3 is 0 below the cutoff; the rsq input is
+    // replaced so no inf/NaN is formed on the way.
+    const bool ok = !EXACT || r2 >= cut2;
+    const double rr = EXACT ? (ok ? r2 : 1.0) : r2;
+    const double y0 = __builtin_amdgcn_rsq(rr);
+    const double y2 = y0 * y0;
+    const double e = __builtin_fma(-rr, y2, 1.0);
+    const double corr = __builtin_fma(e, __builtin_fma(e, c1875, c15), 1.0);
+    double w = (y2 * y0) * corr;
+    if constexpr (EXACT) w = ok ? w : 0.0;
+    const double si = mj * w;
+    a.ax[i] = __builtin_fma(si, dx, a.ax[i]);
+    a.ay[i] = __builtin_fma(si, dy, a.ay[i]);
+    a.az[i] = __builtin_fma(si, dz, a.az[i]);
     if constexpr (SYM) {
-      c.cx[j] = row_from<1>(c.cx[j]) - (tx.x + tx.y);
-      c.cy[j] = row_from<1>(c.cy[j]) - (ty.x + ty.y);
-      c.cz[j] = row_from<1>(c.cz[j]) - (tz.x + tz.y);
+      const double sj = a.mu[i] * w;
+      if (i == 0) {
+        tx = sj * dx; ty = sj * dy; tz = sj * dz;
+      } else {
+        tx = __builtin_fma(sj, dx, tx);
+        ty = __builtin_fma(sj, dy, ty);
+        tz = __builtin_fma(sj, dz, tz);
+      }
     }
   }
 }
 
-template <int I, int J, bool SYM, int... Ks>
-__device__ __forceinline__ void lds_row_pass(ISet<I>& a, CSet<J>& c, const float4* base,
-                                             float eps2, std::integer_sequence<int, Ks...>) {
-  (lds_step<I, J, SYM, Ks>(a, c, base, eps2), ...);
+template <typename T, int I, int J, bool SYM, bool EXACT, int K>
+__device__ __forceinline__ void lds_step(ISetT<T, I>& a, CSetT<T, J>& c, const Vec4<T>* base,
+                                         T eps2, T cut2) {
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    const Vec4<T> q = base[j * kStagedRows + K];
+    if constexpr (sizeof(T) == 4) {
+      f2 tx, ty, tz;
+      meet_j<I, SYM, EXACT>(a, q.x, q.y, q.z, q.w, eps2, tx, ty, tz, cut2);
+      if constexpr (SYM) {
+        c.cx[j] = row_from<1>(c.cx[j]) - (tx.x + tx.y);
+        c.cy[j] = row_from<1>(c.cy[j]) - (ty.x + ty.y);
+        c.cz[j] = row_from<1>(c.cz[j]) - (tz.x + tz.y);
+      }
+    } else {
+      double tx, ty, tz;
+      meet_j<I, SYM, EXACT>(a, q.x, q.y, q.z, q.w, eps2, tx, ty, tz, cut2);
+      if constexpr (SYM) {
+        c.cx[j] = row_from<1>(c.cx[j]) - tx;
+        c.cy[j] = row_from<1>(c.cy[j]) - ty;
+        c.cz[j] = row_from<1>(c.cz[j]) - tz;
+      }
+    }
+  }
+}
+
+template <typename T, int I, int J, bool SYM, bool EXACT, int... Ks>
+__device__ __forceinline__ void lds_row_pass(ISetT<T, I>& a, CSetT<T, J>& c,
+                                             const Vec4<T>* base, T eps2, T cut2,
+                                             std::integer_sequence<int, Ks...>) {
+  (lds_step<T, I, J, SYM, EXACT, Ks>(a, c, base, eps2, cut2), ...);
 }
 
 // All (64 I) x (64 J) pairs against the staged j-tile `tile` (LDS). Carriers return home.
-template <int I, int J, bool SYM>
-__device__ __forceinline__ void tile_lds(ISet<I>& a, CSet<J>& c, const float4* tile, float eps2) {
+template <typename T, int I, int J, bool SYM, bool EXACT>
+__device__ __forceinline__ void tile_lds(ISetT<T, I>& a, CSetT<T, J>& c, const Vec4<T>* tile,
+                                         T eps2, T cut2) {
   const int lane = static_cast<int>(__lane_id());
   const int R = lane >> 4, col = lane & 15;
   const int addr = ((lane + 48) & 63) << 2;
 #pragma unroll 1
   for (int p = 0; p < 4; ++p) {
-    const float4* base = tile + ((R - p) & 3) * 32 + (16 - col);
-    lds_row_pass<I, J, SYM>(a, c, base, eps2, std::make_integer_sequence<int, 16>{});
+    const Vec4<T>* base = tile + ((R - p) & 3) * 32 + (16 - col);
+    lds_row_pass<T, I, J, SYM, EXACT>(a, c, base, eps2, cut2,
+                                      std::make_integer_sequence<int, 16>{});
     if constexpr (SYM) {
 #pragma unroll
       for (int j = 0; j < J; ++j) {

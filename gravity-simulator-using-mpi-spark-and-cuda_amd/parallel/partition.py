@@ -75,22 +75,22 @@ def sym_geometry(n_pad: int) -> dict:
     return {"NC": nc, "H": h, "L": seg, "S": -(-h // seg)}
 
 
-def sym_bytes(n_pad: int, nranks: int) -> int:
+def sym_bytes(n_pad: int, nranks: int, esz: int = 4) -> int:
     g = sym_geometry(n_pad)
     n_local = n_pad // nranks
-    return n_local * 12 * (g["S"] + g["H"] + 1) + 2 * n_local * SYM_GROUPS * 12
+    return n_local * 3 * esz * (g["S"] + g["H"] + 1) + 2 * n_local * SYM_GROUPS * 3 * esz
 
 
 def sym_auto(n: int, nranks: int, chunk: int = 0, dtype: str = "fp32",
              cutoff_mode: str = "auto") -> bool:
     """Whether mode=auto picks the sym schedule (mirror of gs_layout_compute)."""
     c = chunk or auto_chunk(n)
-    if dtype != "fp32" or cutoff_mode == "exact" or 8 % nranks or n < 262144:
+    if cutoff_mode == "exact" or 8 % nranks or n < 262144:
         return False
     sp = sym_pad(n, c)
     if sp * 20 > round_up(n, nranks * c) * 21:
         return False
-    return sym_bytes(sp, nranks) <= 96 << 30
+    return sym_bytes(sp, nranks, 8 if dtype == "fp64" else 4) <= 160 << 30
 
 
 def layout(n: int, rank: int = 0, nranks: int = 1, chunk: int = 0, sym: bool = False) -> Layout:
