@@ -95,10 +95,14 @@ def main() -> int:
 
     if a.md:
         with open(a.md, "w") as f:
-            f.write("| config | GPUs | how | ms/step | body-updates/s |\n|---|---|---|---|---|\n")
+            from gravsim.ops._native import MODE_NAMES
+
+            f.write("| config | GPUs | how | schedule | ms/step | body-updates/s |\n"
+                    "|---|---|---|---|---|---|\n")
             for r in rows:
-                f.write(f"| {r['config']} | {r['gpus']} | {r['how']} | {r['ms_per_step']:.3f} | "
-                        f"{r['body_updates_per_s']:.4g} |\n")
+                mode = MODE_NAMES.get(r.get("layout", {}).get("mode"), "cpu")
+                f.write(f"| {r['config']} | {r['gpus']} | {r['how']} | {mode} | "
+                        f"{r['ms_per_step']:.3f} | {r['body_updates_per_s']:.4g} |\n")
     return 0
 
 

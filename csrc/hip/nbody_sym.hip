@@ -28,7 +28,7 @@ namespace {
 // Workgroup shape per precision: W waves, I i-bodies and J j-bodies per lane; one workgroup
 // holds one 2048-body chunk on its i side (W * 64 * I == kSymC).
 //   fp32: GS_SYM_SHAPE 1 (default) = (4 waves, I 8, J 2); 0 = (8 waves, I 4, J 4).
-//   fp64: (8 waves, I 4, J 2): 14 VGPRs per i-body leave no room for I 8.
+//   fp64: (8 waves, I 4, J GS_SYM_J64 = 1): 14 VGPRs per i-body leave no room for I 8.
 #ifndef GS_SYM_SHAPE
 #define GS_SYM_SHAPE 1
 #endif
@@ -39,17 +39,26 @@ struct Shape<float> {
   static constexpr int W = GS_SYM_SHAPE == 1 ? 4 : 8, I = GS_SYM_SHAPE == 1 ? 8 : 4,
                        J = GS_SYM_SHAPE == 1 ? 2 : 4;
 };
+#ifndef GS_SYM_J64
+#define GS_SYM_J64 1
+#endif
 template <>
 struct Shape<double> {
-  static constexpr int W = 8, I = 4, J = 2;
+  static constexpr int W = 8, I = 4, J = GS_SYM_J64;
 };
 
-// Occupancy floor (waves per SIMD) as an A/B knob.
+// Occupancy floor (waves per SIMD), per precision. fp64 at 4 waves/SIMD (2 workgroups of
+// 8 waves) with a few spills beats 2 waves/SIMD at 130 VGPRs: 512K fp64 124.7 -> 119.6 ms
+// with J 1 (profiles/r1_sym_ab.jsonl). fp32 gains nothing from it (170.8 vs 170.1 ms).
 #ifdef GS_SYM_WAVES_PER_EU
-#define GS_SYM_WPE __attribute__((amdgpu_waves_per_eu(GS_SYM_WAVES_PER_EU)))
+#define GS_SYM_WPE32 __attribute__((amdgpu_waves_per_eu(GS_SYM_WAVES_PER_EU)))
 #else
-#define GS_SYM_WPE
+#define GS_SYM_WPE32
 #endif
+#ifndef GS_SYM_WAVES_PER_EU64
+#define GS_SYM_WAVES_PER_EU64 4
+#endif
+#define GS_SYM_WPE64 __attribute__((amdgpu_waves_per_eu(GS_SYM_WAVES_PER_EU64)))
 
 #ifndef GS_SYM_JLDS
 #define GS_SYM_JLDS 1
@@ -184,7 +193,7 @@ __device__ __forceinline__ void run_tiles(const SymArgs& a, sym::ISetT<T, Geo<T>
 
 // One workgroup per unit (row a, segment s); s == S is the row's diagonal chunk.
 template <typename T, bool EXACT>
-__global__ __launch_bounds__(Geo<T>::kThreads) GS_SYM_WPE void force_sym_kernel(SymArgs a) {
+__device__ __forceinline__ void force_sym_body(const SymArgs& a) {
   using G = Geo<T>;
   using V4 = sym::Vec4<T>;
   __shared__ Smem<T> sm;
@@ -225,6 +234,15 @@ __global__ __launch_bounds__(Geo<T>::kThreads) GS_SYM_WPE void force_sym_kernel(
     out[kSymC + b] = is.ay[i];
     out[2 * kSymC + b] = is.az[i];
   }
+}
+
+template <bool EXACT>
+__global__ __launch_bounds__(Geo<float>::kThreads) GS_SYM_WPE32 void force_sym_kernel_f32(SymArgs a) {
+  force_sym_body<float, EXACT>(a);
+}
+template <bool EXACT>
+__global__ __launch_bounds__(Geo<double>::kThreads) GS_SYM_WPE64 void force_sym_kernel_f64(SymArgs a) {
+  force_sym_body<double, EXACT>(a);
 }
 
 // S_g(x) for this rank's groups and every body x of a real chunk: rows A of group g in
@@ -318,12 +336,14 @@ template <typename T>
 hipError_t launch_force_sym_t(const SymArgs& a, hipStream_t s) {
   const int units = a.rows * (a.S + 1);
   if (units <= 0) return hipSuccess;
-  if (a.exact)
-    hipLaunchKernelGGL((force_sym_kernel<T, true>), dim3(units), dim3(Geo<T>::kThreads), 0, s,
-                       a);
-  else
-    hipLaunchKernelGGL((force_sym_kernel<T, false>), dim3(units), dim3(Geo<T>::kThreads), 0,
-                       s, a);
+  const dim3 grid(units), block(Geo<T>::kThreads);
+  if constexpr (sizeof(T) == 8) {
+    if (a.exact) hipLaunchKernelGGL(force_sym_kernel_f64<true>, grid, block, 0, s, a);
+    else hipLaunchKernelGGL(force_sym_kernel_f64<false>, grid, block, 0, s, a);
+  } else {
+    if (a.exact) hipLaunchKernelGGL(force_sym_kernel_f32<true>, grid, block, 0, s, a);
+    else hipLaunchKernelGGL(force_sym_kernel_f32<false>, grid, block, 0, s, a);
+  }
   return hipGetLastError();
 }
 
@@ -351,9 +371,9 @@ hipError_t launch_sym_finalize(const SymArgs& a, hipStream_t s) {
 int sym_occupancy(int fp64) {
   int n = 0;
   const hipError_t e =
-      fp64 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, force_sym_kernel<double, false>,
+      fp64 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, force_sym_kernel_f64<false>,
                                                           Geo<double>::kThreads, 0)
-           : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, force_sym_kernel<float, false>,
+           : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, force_sym_kernel_f32<false>,
                                                           Geo<float>::kThreads, 0);
   return e == hipSuccess ? n : 0;
 }
