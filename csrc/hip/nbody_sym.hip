@@ -198,7 +198,17 @@ __device__ __forceinline__ void force_sym_body(const SymArgs& a) {
   using V4 = sym::Vec4<T>;
   __shared__ Smem<T> sm;
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int ar = blockIdx.x / (a.S + 1), s = blockIdx.x % (a.S + 1);
+  int ar, s;
+  if (a.units == 1) {
+    ar = blockIdx.x;
+    s = a.S;
+  } else if (a.units == 2) {
+    ar = blockIdx.x / a.S;
+    s = blockIdx.x % a.S;
+  } else {
+    ar = blockIdx.x / (a.S + 1);
+    s = blockIdx.x % (a.S + 1);
+  }
   const int A = a.a0 + ar;
   if ((int64_t)A * kSymC >= a.n_real) return;  // all-ghost row: never read
   const V4* X4 = static_cast<const V4*>(a.X);
@@ -334,7 +344,7 @@ __global__ __launch_bounds__(256) void sym_finalize_kernel(SymArgs a) {
 
 template <typename T>
 hipError_t launch_force_sym_t(const SymArgs& a, hipStream_t s) {
-  const int units = a.rows * (a.S + 1);
+  const int units = a.units == 1 ? a.rows : a.rows * (a.units == 2 ? a.S : a.S + 1);
   if (units <= 0) return hipSuccess;
   const dim3 grid(units), block(Geo<T>::kThreads);
   if constexpr (sizeof(T) == 8) {

@@ -378,11 +378,18 @@ int enqueue_sym(gs_stepper* s, int cur, bool need_gather, bool gathered_external
   if (s->emulate) a.Rbuf = s->sym_S;  // timing emulation: no exchange, stale sums
   if (part & 1) {
     if (need_gather) {
+      // The diagonal chunks need only this rank's own rows: they run while the all-gather
+      // of the other ranks' rows is in flight; the shell chunks wait for it.
       if (gathered_externally) s->full[cur] = true;
       else if (gather(s, cur)) return -1;
+      gs::SymArgs d = a;
+      d.units = 1;
+      GS_HIP(gs::launch_force_sym(d, s->s_comp));
       GS_HIP(hipStreamWaitEvent(s->s_comp, s->ev_gathered, 0));
+      a.units = 2;
     }
     GS_HIP(gs::launch_force_sym(a, s->s_comp));
+    a.units = 0;
     if (timed) GS_HIP(hipEventRecord(s->ev_local, s->s_comp));
     GS_HIP(gs::launch_sym_group_reduce(a, s->s_comp));
     if (s->have_comm && sym_exchange_rccl(s)) return -1;

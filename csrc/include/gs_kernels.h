@@ -63,6 +63,8 @@ struct SymArgs {
   int32_t NC, a0, rows, S, L, H, P, real_chunks;
   int32_t fp64;        // element type of every array above
   int32_t exact;       // reference hard cutoff (select at cut2) instead of the fast core
+  int32_t units;       // which units a force launch covers: 0 all, 1 diagonal chunks only
+                       // (need only the own rows), 2 shell chunks only
   double dt, eps2, cut2;
 };
 
