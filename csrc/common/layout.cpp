@@ -39,16 +39,17 @@ extern "C" int gs_layout_compute(const gs_config* cfg, gs_layout* out) {
   out->n_pad = gs::round_up(cfg->n, (int64_t)cfg->nranks * chunk);
   // Newton-3 symmetric schedule (fp32, fast cutoff, P | 8). Its chunk/row/group structure
   // must not depend on P, so the padding is the one an 8-rank run would use.
-  const bool sym_ok = cfg->cutoff_mode != 1 && 8 % cfg->nranks == 0 &&
-                      cfg->kernel != GS_KERNEL_MFMA;
+  const bool sym_ok = 8 % cfg->nranks == 0 && cfg->kernel != GS_KERNEL_MFMA;
   if (cfg->mode == GS_MODE_SYM && !sym_ok) {
-    gs_set_error("layout: the sym schedule needs the fast cutoff and nranks dividing 8");
+    gs_set_error("layout: the sym schedule needs nranks dividing 8 (and not the mfma kernel)");
     return -1;
   }
   const int64_t sym_unit = 8 * (int64_t)(chunk % 2048 == 0 ? chunk : 2 * chunk);
   const int64_t sym_pad = gs::round_up(cfg->n, sym_unit);
   bool sym = cfg->mode == GS_MODE_SYM;
-  if (cfg->mode == GS_MODE_AUTO && sym_ok && cfg->n >= 262144 && sym_pad * 20 <= out->n_pad * 21) {
+  // From 64K bodies the sym schedule beats the one-sided split (65536: 1.053 vs 1.082 ms,
+  // 131072: 3.05 vs 3.80, 262144: 11.0 vs 16.4; profiles/r1_sym_sizes.jsonl).
+  if (cfg->mode == GS_MODE_AUTO && sym_ok && cfg->n >= 65536 && sym_pad * 20 <= out->n_pad * 21) {
     // Partial buffers: n_local * (S + H) * 3 elements (gs_sym_bytes); keep them well
     // inside the 288 GB of HBM.
     sym = gs_sym_bytes(sym_pad, cfg->nranks, cfg->dtype == GS_FP64 ? 8 : 4) <= ((int64_t)160 << 30);
@@ -109,26 +110,39 @@ extern "C" int gs_layout_compute(const gs_config* cfg, gs_layout* out) {
   return 0;
 }
 
-// Symmetric-schedule geometry (gs_kernels.h SymArgs): NC chunks of 2048, shell H = NC / 2,
-// segment length L = max(1, NC / 512) chunks, S = ceil(H / L) segments per row.
-extern "C" int gs_sym_geometry(int64_t n_pad, int32_t* NC, int32_t* H, int32_t* L, int32_t* S) {
+// Symmetric-schedule geometry (gs_kernels.h SymArgs), a function of n_pad only:
+//   NC chunks of 2048 bodies; shell H = NC / 2 chunks;
+//   L = segment length in quanta of 128 bodies (16 per chunk): 16 * (NC / 512) from
+//       NC = 512 up, else the largest power of two <= max(1, NC / 32), so a row has
+//       about 256 segments at every size (enough workgroups for one rank of eight);
+//   S = ceil(16 H / L) segments per row; D = max(1, 16 / L) parts of the diagonal chunk.
+extern "C" int gs_sym_geometry(int64_t n_pad, int32_t* NC, int32_t* H, int32_t* L, int32_t* S,
+                               int32_t* D) {
   if (n_pad % (8 * 2048) != 0) { gs_set_error("sym: n_pad must be a multiple of 16384"); return -1; }
   const int32_t nc = (int32_t)(n_pad / 2048);
   const int32_t h = nc / 2;
-  const int32_t l = nc / 512 > 1 ? nc / 512 : 1;
+  int32_t l;
+  if (nc >= 512) {
+    l = 16 * (nc / 512);
+  } else {
+    const int32_t want = nc / 32 > 1 ? nc / 32 : 1;
+    l = 1;
+    while (l * 2 <= want) l *= 2;
+  }
   if (NC) *NC = nc;
   if (H) *H = h;
   if (L) *L = l;
-  if (S) *S = (h + l - 1) / l;
+  if (S) *S = (16 * h + l - 1) / l;
+  if (D) *D = l < 16 ? 16 / l : 1;
   return 0;
 }
 
 extern "C" int64_t gs_sym_bytes(int64_t n_pad, int32_t nranks, int32_t esz) {
-  int32_t nc, h, l, sg;
-  if (gs_sym_geometry(n_pad, &nc, &h, &l, &sg)) return -1;
+  int32_t nc, h, l, sg, dp;
+  if (gs_sym_geometry(n_pad, &nc, &h, &l, &sg, &dp)) return -1;
   const int64_t n_local = n_pad / nranks;
   // Pi + Pj + Pd (3 elements per body per slot) + two group-sum buffers (8 groups x 3)
-  return n_local * 3 * esz * ((int64_t)sg + h + 1) + 2 * n_local * 8 * 3 * esz;
+  return n_local * 3 * esz * ((int64_t)sg + h + dp) + 2 * n_local * 8 * 3 * esz;
 }
 
 extern "C" void gs_ic_fill_host(int32_t ic, uint64_t seed, int64_t n, int64_t begin, int64_t end,

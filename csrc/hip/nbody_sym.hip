@@ -27,17 +27,14 @@ namespace {
 
 // Workgroup shape per precision: W waves, I i-bodies and J j-bodies per lane; one workgroup
 // holds one 2048-body chunk on its i side (W * 64 * I == kSymC).
-//   fp32: GS_SYM_SHAPE 1 (default) = (4 waves, I 8, J 2); 0 = (8 waves, I 4, J 4).
+//   fp32: (4 waves, I 8, J 2). (8 waves, I 4, J 4) measured 7 % slower: the per-step j
+//         overhead is amortised over fewer i (profiles/r1_sym_ab.jsonl).
 //   fp64: (8 waves, I 4, J GS_SYM_J64 = 1): 14 VGPRs per i-body leave no room for I 8.
-#ifndef GS_SYM_SHAPE
-#define GS_SYM_SHAPE 1
-#endif
 template <typename T>
 struct Shape;
 template <>
 struct Shape<float> {
-  static constexpr int W = GS_SYM_SHAPE == 1 ? 4 : 8, I = GS_SYM_SHAPE == 1 ? 8 : 4,
-                       J = GS_SYM_SHAPE == 1 ? 2 : 4;
+  static constexpr int W = 4, I = 8, J = 2;
 };
 #ifndef GS_SYM_J64
 #define GS_SYM_J64 1
@@ -75,32 +72,34 @@ struct Geo {
   static constexpr int kTileJ = 64 * J;  // j bodies per tile
   static constexpr int kThreads = 64 * W;
   static constexpr int kTilesPerChunk = kSymC / kTileJ;
+  static constexpr int kTilesPerQuantum = 128 / kTileJ;  // segments count 128-body quanta
   static_assert(W * kTileI == kSymC, "one workgroup holds one chunk on its i side");
+  static_assert(kTileJ <= 128 && 128 % kTileJ == 0, "a j-tile must not straddle quanta");
 };
 
 __device__ __forceinline__ int shell_len(int A, int NC) { return A < NC / 2 ? NC / 2 : NC / 2 - 1; }
 
-// Unit (row a, segment s) -> the sequence of j-tiles it visits, in order, skipping all-ghost
-// column chunks (mu = 0 there, and their rows are never read). s == S is the diagonal chunk.
+// A unit's j-tiles, in order: shell tile u of row A is tile u % T of chunk A + 1 + u / T
+// (T tiles per chunk); a diagonal unit's tile u is tile u of chunk A. All-ghost column chunks
+// are skipped (mu = 0 there, and their rows are never read).
 template <typename T>
 struct TileSeq {
-  int A, NC, real_chunks, d1, d, t;
+  int A, NC, real_chunks, u, u1;
   bool diag;
-  __device__ __forceinline__ int valid(int dd) const {
-    while (dd <= d1 && (A + dd) % NC >= real_chunks) ++dd;
-    return dd;
+  static constexpr int kT = Geo<T>::kTilesPerChunk;
+  __device__ __forceinline__ int d() const { return diag ? 0 : 1 + u / kT; }
+  __device__ __forceinline__ int t() const { return u % kT; }
+  __device__ __forceinline__ int valid(int uu) const {
+    if (!diag)
+      while (uu < u1 && (A + 1 + uu / kT) % NC >= real_chunks) uu = (uu / kT + 1) * kT;
+    return uu;
   }
-  __device__ __forceinline__ bool done() const { return d > d1; }
+  __device__ __forceinline__ bool done() const { return u >= u1; }
   __device__ __forceinline__ int64_t row0() const {
-    const int B = diag ? A : (A + d) % NC;
-    return (int64_t)B * kSymC + t * Geo<T>::kTileJ;
+    const int B = diag ? A : (A + d()) % NC;
+    return (int64_t)B * kSymC + t() * Geo<T>::kTileJ;
   }
-  __device__ __forceinline__ void next() {
-    if (++t == Geo<T>::kTilesPerChunk) {
-      t = 0;
-      d = diag ? d1 + 1 : valid(d + 1);
-    }
-  }
+  __device__ __forceinline__ void next() { u = valid(u + 1); }
 };
 
 // Stage body b of a j-tile into the tile_lds layout (each body stored twice).
@@ -138,7 +137,7 @@ __device__ __forceinline__ void run_tiles(const SymArgs& a, sym::ISetT<T, Geo<T>
   while (!seq.done()) {
     TileSeq<T> nx = seq;
     nx.next();
-    const int d = seq.d, t = seq.t;
+    const int d = seq.d(), t = seq.t();
     V4 q_next;
     const bool stage_next = kJlds<T> && !nx.done() && threadIdx.x < G::kTileJ;
     if (stage_next) q_next = X4[nx.row0() + threadIdx.x];  // lands during the arithmetic
@@ -198,19 +197,34 @@ __device__ __forceinline__ void force_sym_body(const SymArgs& a) {
   using V4 = sym::Vec4<T>;
   __shared__ Smem<T> sm;
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  // Units per row: S shell segments, then D parts of the diagonal chunk.
   int ar, s;
   if (a.units == 1) {
-    ar = blockIdx.x;
-    s = a.S;
+    ar = blockIdx.x / a.D;
+    s = a.S + blockIdx.x % a.D;
   } else if (a.units == 2) {
     ar = blockIdx.x / a.S;
     s = blockIdx.x % a.S;
   } else {
-    ar = blockIdx.x / (a.S + 1);
-    s = blockIdx.x % (a.S + 1);
+    ar = blockIdx.x / (a.S + a.D);
+    s = blockIdx.x % (a.S + a.D);
   }
   const int A = a.a0 + ar;
   if ((int64_t)A * kSymC >= a.n_real) return;  // all-ghost row: never read
+  const bool diag = s >= a.S;
+  const int seg_tiles = a.L * G::kTilesPerQuantum;
+  TileSeq<T> seq{A, a.NC, a.real_chunks, 0, 0, diag};
+  if (diag) {
+    const int q = s - a.S;
+    seq.u = q * seg_tiles;
+    seq.u1 = a.D > 1 ? seq.u + seg_tiles : G::kTilesPerChunk;
+  } else {
+    const int h_tiles = shell_len(A, a.NC) * G::kTilesPerChunk;
+    const int u0 = s * seg_tiles;
+    if (u0 >= h_tiles) return;  // past this row's shell: never read
+    seq.u1 = min(u0 + seg_tiles, h_tiles);
+    seq.u = seq.valid(u0);
+  }
   const V4* X4 = static_cast<const V4*>(a.X);
   sym::ISetT<T, G::I> is;
   const int64_t i_row0 = (int64_t)A * kSymC + w * G::kTileI;
@@ -220,20 +234,13 @@ __device__ __forceinline__ void force_sym_body(const SymArgs& a) {
     is.x[i] = q.x; is.y[i] = q.y; is.z[i] = q.z; is.mu[i] = q.w;
     is.ax[i] = is.ay[i] = is.az[i] = T(0);
   }
-  const bool diag = s == a.S;
-  TileSeq<T> seq{A, a.NC, a.real_chunks, 0, 0, 0, diag};
   T* out;
   if (diag) {
-    // One pseudo-shell step: the 2048-body diagonal chunk (self term 0 through the core, or
+    // Part of the 2048-body diagonal chunk, one-sided (self term 0 through the core, or
     // through the cutoff select in the exact path).
     run_tiles<T, false, EXACT>(a, is, seq, ar, sm);
-    out = static_cast<T*>(a.Pd) + (int64_t)ar * 3 * kSymC;
+    out = static_cast<T*>(a.Pd) + ((int64_t)ar * a.D + (s - a.S)) * 3 * kSymC;
   } else {
-    const int h = shell_len(A, a.NC);
-    const int d0 = s * a.L + 1;
-    if (d0 > h) return;
-    seq.d1 = min(d0 + a.L - 1, h);
-    seq.d = seq.valid(d0);
     run_tiles<T, true, EXACT>(a, is, seq, ar, sm);
     out = static_cast<T*>(a.Pi) + ((int64_t)ar * a.S + s) * 3 * kSymC;
   }
@@ -306,10 +313,15 @@ __global__ __launch_bounds__(256) void sym_finalize_kernel(SymArgs a) {
   }
   const int A = (int)(gi / kSymC), c = (int)(gi % kSymC);
   const int ar = A - a.a0;
-  const T* pd = static_cast<const T*>(a.Pd) + (int64_t)ar * 3 * kSymC + c;
+  const T* pd = static_cast<const T*>(a.Pd) + (int64_t)ar * a.D * 3 * kSymC + c;
   T ax = pd[0], ay = pd[kSymC], az = pd[2 * kSymC];
+  for (int q = 1; q < a.D; ++q) {
+    ax += pd[q * 3 * kSymC];
+    ay += pd[q * 3 * kSymC + kSymC];
+    az += pd[q * 3 * kSymC + 2 * kSymC];
+  }
   const int h = shell_len(A, a.NC);
-  const int segs = (h + a.L - 1) / a.L;
+  const int segs = (16 * h + a.L - 1) / a.L;  // shell length in 128-body quanta / L
   for (int s = 0; s < segs; ++s) {
     const T* p = static_cast<const T*>(a.Pi) + ((int64_t)ar * a.S + s) * 3 * kSymC + c;
     ax += p[0];
@@ -344,7 +356,7 @@ __global__ __launch_bounds__(256) void sym_finalize_kernel(SymArgs a) {
 
 template <typename T>
 hipError_t launch_force_sym_t(const SymArgs& a, hipStream_t s) {
-  const int units = a.units == 1 ? a.rows : a.rows * (a.units == 2 ? a.S : a.S + 1);
+  const int units = a.rows * (a.units == 1 ? a.D : a.units == 2 ? a.S : a.S + a.D);
   if (units <= 0) return hipSuccess;
   const dim3 grid(units), block(Geo<T>::kThreads);
   if constexpr (sizeof(T) == 8) {

@@ -100,7 +100,7 @@ struct gs_stepper {
   char* sym_Pd = nullptr;
   char* sym_S = nullptr;  // group sums by destination rank
   char* sym_R = nullptr;  // group sums by source rank (== sym_S with one rank)
-  int32_t sym_NC = 0, sym_H = 0, sym_L = 0, sym_S_n = 0;
+  int32_t sym_NC = 0, sym_H = 0, sym_L = 0, sym_S_n = 0, sym_D = 1;
   hipEvent_t ev_sym = nullptr;
 };
 
@@ -189,6 +189,7 @@ gs::SymArgs sym_args(gs_stepper* s, int cur) {
   a.a0 = s->cfg.rank * a.rows;
   a.S = s->sym_S_n;
   a.L = s->sym_L;
+  a.D = s->sym_D;
   a.H = s->sym_H;
   a.real_chunks = (int32_t)((s->L.n + gs::kSymC - 1) / gs::kSymC);
   a.dt = s->cfg.dt;
@@ -225,12 +226,13 @@ int sym_exchange_rccl(gs_stepper* s) {
 
 int ensure_sym(gs_stepper* s) {
   if (s->L.mode != GS_MODE_SYM || s->sym_Pi) return 0;
-  if (gs_sym_geometry(s->L.n_pad, &s->sym_NC, &s->sym_H, &s->sym_L, &s->sym_S_n)) return -1;
+  if (gs_sym_geometry(s->L.n_pad, &s->sym_NC, &s->sym_H, &s->sym_L, &s->sym_S_n, &s->sym_D))
+    return -1;
   const size_t nl = (size_t)s->L.n_local, rows = (size_t)s->sym_NC / s->cfg.nranks;
   const size_t e = s->esz;
   GS_HIP(hipMalloc(&s->sym_Pi, rows * s->sym_S_n * 3 * gs::kSymC * e));
   GS_HIP(hipMalloc(&s->sym_Pj, rows * s->sym_H * 3 * gs::kSymC * e));
-  GS_HIP(hipMalloc(&s->sym_Pd, rows * 3 * gs::kSymC * e));
+  GS_HIP(hipMalloc(&s->sym_Pd, rows * s->sym_D * 3 * gs::kSymC * e));
   GS_HIP(hipMalloc(&s->sym_S, (size_t)gs::kSymGroups * 3 * nl * e));
   if (s->cfg.nranks > 1)
     GS_HIP(hipMalloc(&s->sym_R, (size_t)gs::kSymGroups * 3 * nl * e));

@@ -90,7 +90,8 @@ int gs_layout_compute(const gs_config* cfg, gs_layout* out);
 int32_t gs_auto_chunk(int64_t n);
 // Symmetric (Newton-3) schedule geometry for a padded body count, and its partial-buffer
 // bytes per rank (GS_MODE_SYM).
-int gs_sym_geometry(int64_t n_pad, int32_t* NC, int32_t* H, int32_t* L, int32_t* S);
+int gs_sym_geometry(int64_t n_pad, int32_t* NC, int32_t* H, int32_t* L, int32_t* S,
+                    int32_t* D);
 int64_t gs_sym_bytes(int64_t n_pad, int32_t nranks, int32_t esz);
 
 // ---------------------------------------------------------------- counter-based RNG / ICs (host)

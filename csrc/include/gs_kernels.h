@@ -40,20 +40,21 @@ inline int split_span(const KArgs<T>& a) {
 // P | 8 produces the same bits): chunks of kSymC = 2048 bodies, NC = n_pad / 2048 of them,
 // G = 8 row groups of NC / 8 chunks. Chunk A pairs with the next h(A) chunks cyclically
 // (h = NC/2 for A < NC/2, NC/2 - 1 above: every unordered chunk pair exactly once) and with
-// itself (one-sided). Row A's shell is cut into segments of L chunks; one workgroup per
-// (row, segment) unit writes an i-side partial Pi[row][segment] and, per shell chunk, a
-// j-side partial Pj[row][d-1]. Group reduce: S_g(x) = sum over rows A of group g (A
-// ascending) of Pj[A][x - A]. Final: a = Pd + sum_s Pi[s] (s ascending) + sum_g S_g
-// (g ascending), then the KD integrate.
+// itself (one-sided). Row A's shell is cut into segments of L quanta (128 bodies; see
+// gs_sym_geometry), its diagonal chunk into D parts; one workgroup per unit writes an i-side
+// partial (Pi[row][segment] or Pd[row][part]) and, for every shell tile it visits, the
+// j-side partial of its 2048 i-bodies into Pj[row][d-1]. Group reduce: S_g(x) = sum over
+// rows A of group g (A ascending) of Pj[A][x - A]. Final: a = sum_q Pd[q] + sum_s Pi[s]
+// + sum_g S_g (each ascending), then the KD integrate.
 constexpr int kSymC = 2048;
 constexpr int kSymGroups = 8;
 
 struct SymArgs {
   // Arrays are float (fp32 run) or double (fp64 run); the launchers pick the instantiation.
   const void* X;       // [n_pad * 4] gathered positions (x, y, z, mu)
-  void* Pi;            // [rows][S][3][kSymC] i-side partials
+  void* Pi;            // [rows][S][3][kSymC] i-side partials (segment = L quanta of 128)
   void* Pj;            // [rows][H][3][kSymC] j-side partials, H = NC / 2
-  void* Pd;            // [rows][3][kSymC] diagonal-chunk partials
+  void* Pd;            // [rows][D][3][kSymC] diagonal-chunk partials
   void* Sbuf;          // [P][G/P][3][n_local] group sums by destination rank
   const void* Rbuf;    // [P][G/P][3][n_local] group sums received, by source rank
   void* X_next;        // [n_pad * 4]
@@ -61,6 +62,7 @@ struct SymArgs {
   void* acc_out;       // optional [n_local * 4]: emit accelerations instead of integrating
   int64_t n_real, n_local, i_begin;
   int32_t NC, a0, rows, S, L, H, P, real_chunks;
+  int32_t D;           // parts of the diagonal chunk (L < 16 quanta: 16 / L)
   int32_t fp64;        // element type of every array above
   int32_t exact;       // reference hard cutoff (select at cut2) instead of the fast core
   int32_t units;       // which units a force launch covers: 0 all, 1 diagonal chunks only

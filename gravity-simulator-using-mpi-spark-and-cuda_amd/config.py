@@ -81,8 +81,8 @@ class SimConfig:
         if self.kernel == "mfma" and (self.dtype != "fp32" or self.ipl > 1 or
                                       self.mode == "fused"):
             raise ValueError("kernel mfma is fp32, ipl 0/1, split schedule only")
-        if self.mode == "sym" and (self.cutoff_mode == "exact" or self.kernel == "mfma"):
-            raise ValueError("mode sym needs the fast cutoff path (Newton-3 pairs)")
+        if self.mode == "sym" and self.kernel == "mfma":
+            raise ValueError("mode sym has its own kernels (not --kernel mfma)")
         if self.ipl not in (0, 1, 2, 4, 8) or (self.ipl == 8 and self.dtype != "fp32"):
             raise ValueError("ipl must be 0, 1, 2, 4 (or 8 for fp32)")
         if self.chunk and self.chunk % 1024:

@@ -66,26 +66,32 @@ def sym_pad(n: int, chunk: int) -> int:
 
 
 def sym_geometry(n_pad: int) -> dict:
-    """NC chunks, shell H = NC/2, segment length L, segments S (layout.cpp gs_sym_geometry)."""
+    """NC chunks, shell H = NC/2, segment length L (quanta of 128 bodies), S segments per row,
+    D diagonal parts (layout.cpp gs_sym_geometry)."""
     if n_pad % (SYM_GROUPS * SYM_CHUNK):
         raise ValueError("sym n_pad must be a multiple of 16384")
     nc = n_pad // SYM_CHUNK
     h = nc // 2
-    seg = max(1, nc // 512)
-    return {"NC": nc, "H": h, "L": seg, "S": -(-h // seg)}
+    if nc >= 512:
+        seg = 16 * (nc // 512)
+    else:
+        want = max(1, nc // 32)
+        seg = 1
+        while seg * 2 <= want:
+            seg *= 2
+    return {"NC": nc, "H": h, "L": seg, "S": -(-16 * h // seg), "D": 16 // seg if seg < 16 else 1}
 
 
 def sym_bytes(n_pad: int, nranks: int, esz: int = 4) -> int:
     g = sym_geometry(n_pad)
     n_local = n_pad // nranks
-    return n_local * 3 * esz * (g["S"] + g["H"] + 1) + 2 * n_local * SYM_GROUPS * 3 * esz
+    return n_local * 3 * esz * (g["S"] + g["H"] + g["D"]) + 2 * n_local * SYM_GROUPS * 3 * esz
 
 
-def sym_auto(n: int, nranks: int, chunk: int = 0, dtype: str = "fp32",
-             cutoff_mode: str = "auto") -> bool:
+def sym_auto(n: int, nranks: int, chunk: int = 0, dtype: str = "fp32") -> bool:
     """Whether mode=auto picks the sym schedule (mirror of gs_layout_compute)."""
     c = chunk or auto_chunk(n)
-    if cutoff_mode == "exact" or 8 % nranks or n < 262144:
+    if 8 % nranks or n < 65536:
         return False
     sp = sym_pad(n, c)
     if sp * 20 > round_up(n, nranks * c) * 21:

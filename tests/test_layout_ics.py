@@ -131,7 +131,7 @@ def test_sym_layout_independent_of_world_size(n, P):
 
 def test_sym_layout_rejects_unsupported():
     lib = _native.cpu_lib()
-    for kw in (dict(nranks=3, rank=0), dict(cutoff_mode=1), dict(kernel=3)):
+    for kw in (dict(nranks=3, rank=0), dict(kernel=3)):
         base = dict(n=50000, dtype=0, rank=0, nranks=1, device=0, mode=_native.MODE_IDS["sym"])
         base.update(kw)
         L = _native.GsLayout()
