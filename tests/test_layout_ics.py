@@ -126,7 +126,18 @@ def test_sym_layout_independent_of_world_size(n, P):
     assert (L.n_pad, L.n_local, L.local_begin) == (p.n_pad, p.n_local, p.local_begin)
     assert p.n_pad == partition.layout(n, 0, 1, sym=True).n_pad
     g = partition.sym_geometry(p.n_pad)
-    assert g["NC"] % (partition.SYM_GROUPS) == 0 and g["S"] * g["L"] >= g["H"]
+    assert g["NC"] % (partition.SYM_GROUPS) == 0
+    # segments of L quanta (128 bodies, 16 per chunk) cover the H-chunk shell; the diagonal
+    # chunk is cut into D parts of the same length when L < 16
+    assert g["S"] * g["L"] >= 16 * g["H"] > (g["S"] - 1) * g["L"]
+    assert g["D"] * min(g["L"], 16) == 16
+    nc, h, seg, S, D = (ctypes.c_int32() for _ in range(5))
+    assert lib.gs_sym_geometry(ctypes.c_int64(p.n_pad), ctypes.byref(nc), ctypes.byref(h),
+                               ctypes.byref(seg), ctypes.byref(S), ctypes.byref(D)) == 0
+    assert (nc.value, h.value, seg.value, S.value, D.value) == \
+        (g["NC"], g["H"], g["L"], g["S"], g["D"])
+    for esz in (4, 8):
+        assert lib.gs_sym_bytes(p.n_pad, P, esz) == partition.sym_bytes(p.n_pad, P, esz)
 
 
 def test_sym_layout_rejects_unsupported():
