@@ -37,6 +37,8 @@ HIP_LIB = OUT / "libgravsim_hip.so"
 TOOL_BIN = OUT / "gravsim_bench"
 MICRO_SRC = CSRC / "tools" / "microbench.hip"
 MICRO_BIN = OUT / "microbench"
+PROBE_SRC = CSRC / "tools" / "sym_probe.hip"
+PROBE_BIN = OUT / "sym_probe"
 
 
 def _stale(target: Path, deps: list[Path]) -> bool:
@@ -107,17 +109,30 @@ def build_microbench(force: bool = False) -> Path:
     return MICRO_BIN
 
 
+def build_sym_probe(force: bool = False) -> Path:
+    """DPP issue-cost / sym register-tile probe (csrc/tools/sym_probe.hip)."""
+    OUT.mkdir(parents=True, exist_ok=True)
+    deps = [PROBE_SRC, *HEADERS]
+    if PROBE_SRC.exists() and (force or _stale(PROBE_BIN, deps)):
+        tmp = PROBE_BIN.with_suffix(".tmp")
+        _run([hipcc(), "-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fno-slp-vectorize",
+              f"-I{CSRC / 'include'}", str(PROBE_SRC), "-o", str(tmp)])
+        os.replace(tmp, PROBE_BIN)
+    return PROBE_BIN
+
+
 def build_all(force: bool = False) -> None:
     build_cpu(force)
     build_hip(force)
     build_tool(force)
     build_microbench(force)
+    build_sym_probe(force)
 
 
 def main(argv: list[str] | None = None) -> int:
     ap = argparse.ArgumentParser(description=__doc__)
     ap.add_argument("--force", action="store_true")
-    ap.add_argument("--only", choices=["cpu", "hip", "tool", "microbench"])
+    ap.add_argument("--only", choices=["cpu", "hip", "tool", "microbench", "sym_probe"])
     a = ap.parse_args(argv)
     if a.only == "cpu":
         build_cpu(a.force)
@@ -127,6 +142,8 @@ def main(argv: list[str] | None = None) -> int:
         build_tool(a.force)
     elif a.only == "microbench":
         build_microbench(a.force)
+    elif a.only == "sym_probe":
+        build_sym_probe(a.force)
     else:
         build_all(a.force)
     return 0
