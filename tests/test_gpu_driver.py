@@ -26,10 +26,12 @@ def test_cli_gpu_fp32_mpi_log(hip, tmp_path, capsys):
     assert text.count("Particle ") == 4096 and "Simulation completed successfully" in text
 
 
-@pytest.mark.parametrize("dtype", ["fp32", "fp64"])
-def test_gpu_resume_bit_exact(hip, tmp_path, dtype):
+@pytest.mark.parametrize("dtype,mode,integrator", [("fp32", "auto", "kd"), ("fp64", "auto", "kd"),
+                                                   ("fp32", "sym", "kd"), ("fp64", "sym", "kd"),
+                                                   ("fp32", "sym", "leapfrog")])
+def test_gpu_resume_bit_exact(hip, tmp_path, dtype, mode, integrator):
     cfg = SimConfig(n=3000, steps=9, dtype=dtype, device="gpu", checkpoint_dir=str(tmp_path),
-                    checkpoint_every=5)
+                    checkpoint_every=5, mode=mode, integrator=integrator)
     sim = Simulation(cfg)
     sim.run()
     full = sim.global_state()
@@ -41,11 +43,14 @@ def test_gpu_resume_bit_exact(hip, tmp_path, dtype):
     assert np.array_equal(got.pos, full.pos) and np.array_equal(got.vel, full.vel)
 
 
-def test_gpu_matches_cpu_engine_steps_fp64(hip):
-    """The GPU Stepper and the native CPU engine integrate the same fp64 trajectory."""
+@pytest.mark.parametrize("mode", ["auto", "sym"])
+def test_gpu_matches_cpu_engine_steps_fp64(hip, mode):
+    """The GPU Stepper (one-sided or Newton-3 schedule) and the native CPU engine integrate
+    the same fp64 trajectory."""
     out = {}
     for dev in ("cpu", "gpu"):
-        sim = Simulation(SimConfig(n=1500, steps=10, dtype="fp64", device=dev))
+        sim = Simulation(SimConfig(n=1500, steps=10, dtype="fp64", device=dev,
+                                   mode=mode if dev == "gpu" else "auto"))
         sim.run()
         out[dev] = sim.global_state()
         sim.close()
@@ -92,10 +97,12 @@ def test_plummer_model_on_gpu_energy(hip):
     assert abs(energy(b1.pos, b1.vel, b1.mass) - e0) / abs(e0) < 1e-3
 
 
-def test_gpu_leapfrog_matches_oracle_kdk(hip):
+@pytest.mark.parametrize("mode", ["auto", "sym"])
+def test_gpu_leapfrog_matches_oracle_kdk(hip, mode):
     from gravsim.ops import oracle
 
-    cfg = SimConfig(n=800, steps=10, dtype="fp64", device="gpu", integrator="leapfrog")
+    cfg = SimConfig(n=800, steps=10, dtype="fp64", device="gpu", integrator="leapfrog",
+                    mode=mode)
     sim = Simulation(cfg)
     b0 = ic.solar_random(800, cfg.seed)
     sim.run()
