@@ -1,28 +1,32 @@
-// Newton-3 (symmetric) register tile for the fp32 direct sum on gfx950.
+// Newton-3 (symmetric) register tile for the direct sum on gfx950 (fp32 and fp64).
 //
 // The reference's cuda.cu:53-60 visits each unordered pair once (j > i) and scatters the
 // equal-and-opposite force into both bodies (cuda.cu:43-49), but does it with racy
 // non-atomic global read-modify-writes. This tile keeps the "one pair,
-// two interactions" saving without any scatter: each wave holds an i-set of 64*I bodies and
-// a j-set of 64*J bodies in registers and visits all (64 I) x (64 J) pairs, accumulating
-//   * the i side in per-lane registers (as the asymmetric kernel does), and
+// two interactions" saving without any scatter: each wave holds an i-set of 64*I bodies in
+// registers, meets a j-tile of 64*J bodies and visits all (64 I) x (64 J) pairs, accumulating
+//   * the i side in per-lane registers (as the one-sided kernels do), and
 //   * the j side in per-lane "carrier" registers that travel with the j-bodies.
 //
-// Data movement is all DPP. Within a 16-lane row, step k (k = 0..15) reads the j positions
-// of lane l-(k+1) with `v_mov_b32_dpp row_ror:(k+1)`. The carriers advance one lane per step with
-// a single `v_sub_f32_dpp row_ror:1` that also adds the step's contribution, so the carrier
-// of a j-body always sits in the lane that is currently interacting with it. After 16 steps
-// the carriers are home; the j positions and carriers then move one row (16 lanes) with
-// ds_bpermute, and after 4 such phases every lane has met every j of the wave.
+// Within a 16-lane row, at step k (k = 0..15) every lane meets the j-body of lane l-(k+1)
+// (DPP row_ror:n reads lane l - n of the row; checked on gfx950). The carriers advance one
+// lane per step with a single `v_sub_f32_dpp row_ror:1` that also subtracts the step's
+// contribution, so the carrier of a j-body always sits in the lane currently meeting it.
+// After 16 steps the carriers are home; they then move one row (16 lanes) with ds_bpermute,
+// and after 4 such phases every lane has met every j of the tile. The j positions come
+// either from an LDS-staged copy of the tile (`tile_lds`, the production path: one
+// ds_read_b128 per j and step on the LDS pipe) or from registers rotated like the carriers
+// (`tile`, `v_mov_b32_dpp row_ror:(k+1)`, fp32 only, kept as the GS_SYM_JLDS=0 A/B path).
 //
-// Cost per pair (two interactions): 3 sub + 3 FMA (r^2) + v_rsq_f32 + 2 mul (r^-3)
+// Cost per pair (two interactions), fp32: 3 sub + 3 FMA (r^2) + v_rsq_f32 + 2 mul (r^-3)
 // + 2 mul (s_i, s_j) + 6 FMA/mul (both accumulators), all packed two pairs per v_pk_*
 // instruction: 4 v_pk + 0.5 v_rsq per interaction, against 6 v_pk + 1 v_rsq for the
-// one-sided loop (nbody_kernels.hip interact_pk).
+// one-sided loop (nbody_kernels.hip interact_pk). fp64: 20 f64 ops + 1 v_rsq_f64 per pair.
 //
-// Numerics: the pair term uses the fast-cutoff core (r^2 + eps2, nbody_kernels.hip FM_FAST),
-// and r^-3 = (y*y)*y with y = rsq(r^2 + eps2). The j-side term of a pair is the exact
-// negation of what body j would compute for body i (x_i - x_j = -(x_j - x_i) in IEEE).
+// Numerics: the pair term uses the fast-cutoff core (r^2 + eps2, nbody_kernels.hip FM_FAST)
+// or, with EXACT, the reference hard cutoff as a select; r^-3 = (y*y)*y with y = rsq(r^2 +
+// eps2) (fp64: the refined r^-3 of the one-sided fp64 path). The j-side term of a pair is the
+// exact negation of what body j would compute for body i (x_i - x_j = -(x_j - x_i) in IEEE).
 #pragma once
 #include <hip/hip_runtime.h>
 
