@@ -20,6 +20,16 @@
 // is a single fused launch (KD integrate in its epilogue) or split + reduce; the loop is
 // captured once into a hipGraph (two steps = one ping-pong period) and replayed. With
 // use_graph >= 2 the multi-rank step, collective included, is captured too.
+//
+// Newton-3 sym schedule (GS_MODE_SYM, the default from 64K bodies; nbody_sym.hip):
+//   s_comm : ncclAllGather in place (as above)
+//   s_comp : diagonal-chunk units (own rows only, beside the gather) -> wait(gathered)
+//            -> shell units (both sides of every pair) -> group reduce
+//   s_comm : group-sum exchange: ncclSend/ncclRecv to every peer (one group call)
+//   s_comp : wait(exchange) -> finalize (fixed-order sum + KD integrate) -> own slice of
+//            X[(k+1)&1]
+// The partial slots and summation order depend on N only, so every P dividing 8 gives the
+// same bits.
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <math.h>
