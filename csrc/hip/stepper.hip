@@ -581,7 +581,9 @@ int download_state(gs_stepper* s, double* pos, double* vel, double* mass) {
 
 template <typename T>
 int accel_impl(gs_stepper* s, double* acc4, bool step_path) {
-  if (ensure_partial(s)) return -1;
+  // The one-sided split partials (n_chunks x n_local rows; 8.6 GB per rank at 16M / 8) are
+  // allocated only when the query runs the split kernels, not for the sym step path.
+  if (!(step_path && use_sym(s)) && ensure_partial(s)) return -1;
   const int cur = (int)(s->k & 1);
   if (s->virt && !s->full[cur]) {
     gs_set_error("accel: virtual-rank shard is not gathered (use the group API)");

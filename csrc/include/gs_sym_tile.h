@@ -159,8 +159,12 @@ __device__ __forceinline__ void meet_j(ISet<I>& a, float xj, float yj, float zj,
     for (int u = 0; u < U; ++u) r2[u] = pk_fma(dz[u], dz[u], r2[u]);
 #pragma unroll
     for (int u = 0; u < U; ++u) {
+#ifdef GS_SYM_PROBE_NO_RSQ  // timing probe only: what the transcendental costs in this loop
+      y[u] = r2[u] * f2(0.5f);
+#else
       y[u].x = __builtin_amdgcn_rsqf(r2[u].x);
       y[u].y = __builtin_amdgcn_rsqf(r2[u].y);
+#endif
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) y3[u] = y[u] * y[u];

@@ -79,6 +79,62 @@ __global__ __launch_bounds__(256) void dpp_chain_kernel(float* out, int iters, f
   out[blockIdx.x * 256 + threadIdx.x] = s;
 }
 
+// Does v_rsq_f32 overlap packed VALU work? Per iteration: MODE 0 = 16 v_pk_fma_f32 (8
+// independent 2-vector chains), MODE 1 = 4 v_rsq_f32 (4 independent chains), MODE 2 = both,
+// interleaved (rsq results consumed only in the next iteration). If MODE 2 ~ max(0, 1) the
+// transcendental runs beside the VALU; if ~ 0 + 1 it serialises.
+template <int MODE>
+__global__ __launch_bounds__(256) void trans_overlap_kernel(float* out, int iters, float c) {
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  f2 v[8];
+  float r[4];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) v[u] = f2{1.0f + 0.001f * (threadIdx.x + u), 1.5f};
+#pragma unroll
+  for (int u = 0; u < 4; ++u) r[u] = 1.0f + 0.01f * (threadIdx.x + u);
+  const f2 cc = f2{c, c}, dd = f2{0.5f, 0.5f};
+  for (int it = 0; it < iters; ++it) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      if constexpr (MODE != 1) {
+        v[u] = __builtin_elementwise_fma(v[u], cc, dd);
+        v[u] = __builtin_elementwise_fma(v[u], cc, dd);
+      }
+      if constexpr (MODE != 0) {
+        if ((u & 1) == 0) r[u >> 1] = __builtin_amdgcn_rsqf(r[u >> 1]) + 1.0f;
+      }
+    }
+  }
+  float s = 0;
+#pragma unroll
+  for (int u = 0; u < 8; ++u) s += v[u].x + v[u].y;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) s += r[u];
+  out[blockIdx.x * 256 + threadIdx.x] = s;
+}
+
+template <int MODE>
+static void run_trans_overlap() {
+  float* d;
+  const int blocks = 256 * 8, iters = 2048;
+  CK(hipMalloc(&d, (size_t)blocks * 256 * 4));
+  trans_overlap_kernel<MODE><<<blocks, 256>>>(d, 16, 0.999f);
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+  CK(hipEventRecord(e0));
+  trans_overlap_kernel<MODE><<<blocks, 256>>>(d, iters, 0.999f);
+  CK(hipEventRecord(e1));
+  CK(hipEventSynchronize(e1));
+  float ms = 0;
+  CK(hipEventElapsedTime(&ms, e0, e1));
+  const double wave_iters = (double)blocks * 4 * iters / 1024.0;  // per SIMD
+  printf("{\"probe\": \"trans_overlap\", \"mode\": \"%s\", \"ns_per_iter_per_simd\": %.3f}\n",
+         MODE == 0 ? "16 v_pk_fma" : MODE == 1 ? "4 v_rsq" : "16 v_pk_fma + 4 v_rsq",
+         ms * 1e6 / wave_iters);
+  fflush(stdout);
+  CK(hipFree(d));
+}
+
 template <int MODE>
 static void run_dpp_chain() {
   float* d;
@@ -186,6 +242,10 @@ int main(int argc, char** argv) {
   const int reps = argc > 2 ? atoi(argv[2]) : 40;
   run_dpp_chain<0>();
   run_dpp_chain<1>();
+  run_trans_overlap<0>();
+  run_trans_overlap<1>();
+  run_trans_overlap<2>();
+  if (argc > 3) return 0;  // overlap probes only
   run<4, 4, true>(waves, reps);
   run<4, 2, true>(waves, reps);
   run<8, 1, true>(waves, reps / 2);
