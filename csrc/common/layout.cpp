@@ -50,9 +50,9 @@ extern "C" int gs_layout_compute(const gs_config* cfg, gs_layout* out) {
   // From 64K bodies the sym schedule beats the one-sided split (65536: 1.053 vs 1.082 ms,
   // 131072: 3.05 vs 3.80, 262144: 11.0 vs 16.4; profiles/r1_sym_sizes.jsonl).
   if (cfg->mode == GS_MODE_AUTO && sym_ok && cfg->n >= 65536 && sym_pad * 20 <= out->n_pad * 21) {
-    // Partial buffers: n_local * (S + H) * 3 elements (gs_sym_bytes); keep them well
-    // inside the 288 GB of HBM.
-    sym = gs_sym_bytes(sym_pad, cfg->nranks, cfg->dtype == GS_FP64 ? 8 : 4) <= ((int64_t)160 << 30);
+    // The partial slots are processed in bands of bounded size (stepper.hip ensure_sym),
+    // so memory does not limit the choice.
+    sym = true;
   }
   if (sym) out->n_pad = sym_pad;
   out->n_local = out->n_pad / cfg->nranks;
@@ -137,6 +137,7 @@ extern "C" int gs_sym_geometry(int64_t n_pad, int32_t* NC, int32_t* H, int32_t* 
   return 0;
 }
 
+// Partial-slot bytes per rank if all of the rank's rows were held at once (one band).
 extern "C" int64_t gs_sym_bytes(int64_t n_pad, int32_t nranks, int32_t esz) {
   int32_t nc, h, l, sg, dp;
   if (gs_sym_geometry(n_pad, &nc, &h, &l, &sg, &dp)) return -1;

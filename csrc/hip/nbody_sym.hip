@@ -120,7 +120,7 @@ struct Smem {
 // runs with SYM = false: every ordered pair once on the i side).
 template <typename T, bool SYM, bool EXACT>
 __device__ __forceinline__ void run_tiles(const SymArgs& a, sym::ISetT<T, Geo<T>::I>& is,
-                                          TileSeq<T> seq, int ar, Smem<T>& sm) {
+                                          TileSeq<T> seq, int br, Smem<T>& sm) {
   static_assert(kJlds<T> || !EXACT, "the DPP-position tile has no exact-cutoff variant");
   using G = Geo<T>;
   using V4 = sym::Vec4<T>;
@@ -175,7 +175,7 @@ __device__ __forceinline__ void run_tiles(const SymArgs& a, sym::ISetT<T, Geo<T>
     if (kJlds<T> || SYM) __syncthreads();
     if constexpr (SYM) {
       // Sum the waves' carriers in wave order (fixed) and store the tile's j-side partial.
-      T* pj = static_cast<T*>(a.Pj) + ((int64_t)ar * a.H + (d - 1)) * 3 * kSymC;
+      T* pj = static_cast<T*>(a.Pj) + ((int64_t)br * a.H + (d - 1)) * 3 * kSymC;
       for (int v = threadIdx.x; v < 3 * G::kTileJ; v += G::kThreads) {
         const int c = v / G::kTileJ, b = v % G::kTileJ;
         T acc = sm.slot[buf][0][c][b];
@@ -198,18 +198,19 @@ __device__ __forceinline__ void force_sym_body(const SymArgs& a) {
   __shared__ Smem<T> sm;
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   // Units per row: S shell segments, then D parts of the diagonal chunk.
-  int ar, s;
+  // br: row within the band (index into Pi/Pj/Pd); the rank's row is band0 + br.
+  int br, s;
   if (a.units == 1) {
-    ar = blockIdx.x / a.D;
+    br = blockIdx.x / a.D;
     s = a.S + blockIdx.x % a.D;
   } else if (a.units == 2) {
-    ar = blockIdx.x / a.S;
+    br = blockIdx.x / a.S;
     s = blockIdx.x % a.S;
   } else {
-    ar = blockIdx.x / (a.S + a.D);
+    br = blockIdx.x / (a.S + a.D);
     s = blockIdx.x % (a.S + a.D);
   }
-  const int A = a.a0 + ar;
+  const int A = a.a0 + a.band0 + br;
   if ((int64_t)A * kSymC >= a.n_real) return;  // all-ghost row: never read
   const bool diag = s >= a.S;
   const int seg_tiles = a.L * G::kTilesPerQuantum;
@@ -238,11 +239,11 @@ __device__ __forceinline__ void force_sym_body(const SymArgs& a) {
   if (diag) {
     // Part of the 2048-body diagonal chunk, one-sided (self term 0 through the core, or
     // through the cutoff select in the exact path).
-    run_tiles<T, false, EXACT>(a, is, seq, ar, sm);
-    out = static_cast<T*>(a.Pd) + ((int64_t)ar * a.D + (s - a.S)) * 3 * kSymC;
+    run_tiles<T, false, EXACT>(a, is, seq, br, sm);
+    out = static_cast<T*>(a.Pd) + ((int64_t)br * a.D + (s - a.S)) * 3 * kSymC;
   } else {
-    run_tiles<T, true, EXACT>(a, is, seq, ar, sm);
-    out = static_cast<T*>(a.Pi) + ((int64_t)ar * a.S + s) * 3 * kSymC;
+    run_tiles<T, true, EXACT>(a, is, seq, br, sm);
+    out = static_cast<T*>(a.Pi) + ((int64_t)br * a.S + s) * 3 * kSymC;
   }
 #pragma unroll
   for (int i = 0; i < G::I; ++i) {
@@ -274,25 +275,59 @@ __global__ __launch_bounds__(256) void sym_group_reduce_kernel(SymArgs a) {
   const int R = a.NC / kSymGroups;
   const int g = (a.a0 / R) + gl;
   const int X = (int)(x / kSymC), c = (int)(x % kSymC);
+  // Rows of group g inside the current band; Sbuf was zeroed at step start, so continuing
+  // it band by band adds in the same order as one pass over the group.
+  const int lo = max(g * R, a.a0 + a.band0);
+  const int hi = min(min((g + 1) * R, a.a0 + a.band0 + a.band_rows), a.real_chunks);
+  if (lo >= hi) return;
+  const int q = (int)(x / a.n_local);
+  const int64_t xl = x % a.n_local;
+  T* o = static_cast<T*>(a.Sbuf) + ((int64_t)q * gpr + gl) * 3 * a.n_local + xl;
   const T* Pj = static_cast<const T*>(a.Pj);
-  T sx = T(0), sy = T(0), sz = T(0);
-  for (int A = g * R; A < (g + 1) * R && A < a.real_chunks; ++A) {
+  T sx = o[0], sy = o[a.n_local], sz = o[2 * a.n_local];
+  for (int A = lo; A < hi; ++A) {
     const int d = (X - A + a.NC) % a.NC;
     if (d == 0 || d > shell_len(A, a.NC)) continue;
-    const T* p = Pj + ((int64_t)(A - a.a0) * a.H + (d - 1)) * 3 * kSymC + c;
+    const T* p = Pj + ((int64_t)(A - a.a0 - a.band0) * a.H + (d - 1)) * 3 * kSymC + c;
     sx += p[0];
     sy += p[kSymC];
     sz += p[2 * kSymC];
   }
-  const int q = (int)(x / a.n_local);
-  const int64_t xl = x % a.n_local;
-  T* o = static_cast<T*>(a.Sbuf) + ((int64_t)q * gpr + gl) * 3 * a.n_local + xl;
   o[0] = sx;
   o[a.n_local] = sy;
   o[2 * a.n_local] = sz;
 }
 
-// a = Pd + sum_s Pi[s] + sum_g S_g, then kick-drift (cuda.cu:73-76, mpi.c:207-215) exactly as
+// Ti = sum_q Pd[q] + sum_s Pi[s] (each ascending) for the bodies of the band's rows.
+template <typename T>
+__global__ __launch_bounds__(256) void sym_row_reduce_kernel(SymArgs a) {
+  const int64_t b = (int64_t)blockIdx.x * 256 + threadIdx.x;  // body within the band
+  if (b >= (int64_t)a.band_rows * kSymC) return;
+  const int br = (int)(b / kSymC), c = (int)(b % kSymC);
+  const int A = a.a0 + a.band0 + br;
+  if ((int64_t)A * kSymC >= a.n_real) return;  // all-ghost row
+  const T* pd = static_cast<const T*>(a.Pd) + (int64_t)br * a.D * 3 * kSymC + c;
+  T ax = pd[0], ay = pd[kSymC], az = pd[2 * kSymC];
+  for (int q = 1; q < a.D; ++q) {
+    ax += pd[q * 3 * kSymC];
+    ay += pd[q * 3 * kSymC + kSymC];
+    az += pd[q * 3 * kSymC + 2 * kSymC];
+  }
+  const int h = shell_len(A, a.NC);
+  const int segs = (16 * h + a.L - 1) / a.L;  // shell length in 128-body quanta / L
+  for (int s = 0; s < segs; ++s) {
+    const T* p = static_cast<const T*>(a.Pi) + ((int64_t)br * a.S + s) * 3 * kSymC + c;
+    ax += p[0];
+    ay += p[kSymC];
+    az += p[2 * kSymC];
+  }
+  T* ti = static_cast<T*>(a.Ti) + (int64_t)(a.band0 + br) * kSymC + c;
+  ti[0] = ax;
+  ti[a.n_local] = ay;
+  ti[2 * a.n_local] = az;
+}
+
+// a = Ti + sum_g S_g, then kick-drift (cuda.cu:73-76, mpi.c:207-215) exactly as
 // the one-sided kernels' epilogue (nbody_kernels.hip integrate_store); ghost rows are zeroed.
 template <typename T>
 __global__ __launch_bounds__(256) void sym_finalize_kernel(SymArgs a) {
@@ -311,23 +346,8 @@ __global__ __launch_bounds__(256) void sym_finalize_kernel(SymArgs a) {
     }
     return;
   }
-  const int A = (int)(gi / kSymC), c = (int)(gi % kSymC);
-  const int ar = A - a.a0;
-  const T* pd = static_cast<const T*>(a.Pd) + (int64_t)ar * a.D * 3 * kSymC + c;
-  T ax = pd[0], ay = pd[kSymC], az = pd[2 * kSymC];
-  for (int q = 1; q < a.D; ++q) {
-    ax += pd[q * 3 * kSymC];
-    ay += pd[q * 3 * kSymC + kSymC];
-    az += pd[q * 3 * kSymC + 2 * kSymC];
-  }
-  const int h = shell_len(A, a.NC);
-  const int segs = (16 * h + a.L - 1) / a.L;  // shell length in 128-body quanta / L
-  for (int s = 0; s < segs; ++s) {
-    const T* p = static_cast<const T*>(a.Pi) + ((int64_t)ar * a.S + s) * 3 * kSymC + c;
-    ax += p[0];
-    ay += p[kSymC];
-    az += p[2 * kSymC];
-  }
+  const T* ti = static_cast<const T*>(a.Ti) + li;
+  T ax = ti[0], ay = ti[a.n_local], az = ti[2 * a.n_local];
   // Rbuf[source rank][its local group] in global group order g = 0..7.
   for (int gg = 0; gg < kSymGroups; ++gg) {
     const T* p = static_cast<const T*>(a.Rbuf) + (int64_t)gg * 3 * a.n_local + li;
@@ -356,7 +376,7 @@ __global__ __launch_bounds__(256) void sym_finalize_kernel(SymArgs a) {
 
 template <typename T>
 hipError_t launch_force_sym_t(const SymArgs& a, hipStream_t s) {
-  const int units = a.rows * (a.units == 1 ? a.D : a.units == 2 ? a.S : a.S + a.D);
+  const int units = a.band_rows * (a.units == 1 ? a.D : a.units == 2 ? a.S : a.S + a.D);
   if (units <= 0) return hipSuccess;
   const dim3 grid(units), block(Geo<T>::kThreads);
   if constexpr (sizeof(T) == 8) {
@@ -380,6 +400,14 @@ hipError_t launch_sym_group_reduce(const SymArgs& a, hipStream_t s) {
   const dim3 grid((unsigned)((bodies + 255) / 256), kSymGroups / a.P);
   if (a.fp64) hipLaunchKernelGGL(sym_group_reduce_kernel<double>, grid, dim3(256), 0, s, a);
   else hipLaunchKernelGGL(sym_group_reduce_kernel<float>, grid, dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_sym_row_reduce(const SymArgs& a, hipStream_t s) {
+  const int64_t bodies = (int64_t)a.band_rows * kSymC;
+  const dim3 grid((unsigned)((bodies + 255) / 256));
+  if (a.fp64) hipLaunchKernelGGL(sym_row_reduce_kernel<double>, grid, dim3(256), 0, s, a);
+  else hipLaunchKernelGGL(sym_row_reduce_kernel<float>, grid, dim3(256), 0, s, a);
   return hipGetLastError();
 }
 

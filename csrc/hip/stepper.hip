@@ -110,7 +110,9 @@ struct gs_stepper {
   char* sym_Pd = nullptr;
   char* sym_S = nullptr;  // group sums by destination rank
   char* sym_R = nullptr;  // group sums by source rank (== sym_S with one rank)
+  char* sym_Ti = nullptr;  // per-body i-side totals [3][n_local]
   int32_t sym_NC = 0, sym_H = 0, sym_L = 0, sym_S_n = 0, sym_D = 1;
+  int32_t sym_band = 0;  // rows per band (Pi/Pj/Pd hold one band)
   hipEvent_t ev_sym = nullptr;
 };
 
@@ -190,6 +192,7 @@ gs::SymArgs sym_args(gs_stepper* s, int cur) {
   a.Pd = s->sym_Pd;
   a.Sbuf = s->sym_S;
   a.Rbuf = s->sym_R;
+  a.Ti = s->sym_Ti;
   a.n_real = s->L.n;
   a.n_local = s->L.n_local;
   a.i_begin = s->L.local_begin;
@@ -206,6 +209,8 @@ gs::SymArgs sym_args(gs_stepper* s, int cur) {
   a.eps2 = s->eps2;
   a.exact = s->exact ? 1 : 0;
   a.cut2 = s->cfg.cutoff * s->cfg.cutoff;
+  a.band0 = 0;
+  a.band_rows = a.rows;
   return a;
 }
 
@@ -240,9 +245,20 @@ int ensure_sym(gs_stepper* s) {
     return -1;
   const size_t nl = (size_t)s->L.n_local, rows = (size_t)s->sym_NC / s->cfg.nranks;
   const size_t e = s->esz;
-  GS_HIP(hipMalloc(&s->sym_Pi, rows * s->sym_S_n * 3 * gs::kSymC * e));
-  GS_HIP(hipMalloc(&s->sym_Pj, rows * s->sym_H * 3 * gs::kSymC * e));
-  GS_HIP(hipMalloc(&s->sym_Pd, rows * s->sym_D * 3 * gs::kSymC * e));
+  // Rows per band: the partial slots of one band stay within the budget (default 32 GiB,
+  // GRAVSIM_SYM_BAND_MB overrides; tests use a tiny budget to force many bands). 1M bodies
+  // need 6.4 GB for all rows (one band); 16M on 8 ranks would need 109 GB per rank.
+  const size_t per_row = (size_t)(s->sym_S_n + s->sym_H + s->sym_D) * 3 * gs::kSymC * e;
+  size_t budget = (size_t)32 << 30;
+  if (const char* mb = getenv("GRAVSIM_SYM_BAND_MB")) budget = (size_t)atoll(mb) << 20;
+  size_t band = budget / per_row;
+  if (band < 1) band = 1;
+  if (band > rows) band = rows;
+  s->sym_band = (int32_t)band;
+  GS_HIP(hipMalloc(&s->sym_Pi, band * s->sym_S_n * 3 * gs::kSymC * e));
+  GS_HIP(hipMalloc(&s->sym_Pj, band * s->sym_H * 3 * gs::kSymC * e));
+  GS_HIP(hipMalloc(&s->sym_Pd, band * s->sym_D * 3 * gs::kSymC * e));
+  GS_HIP(hipMalloc(&s->sym_Ti, 3 * nl * e));
   GS_HIP(hipMalloc(&s->sym_S, (size_t)gs::kSymGroups * 3 * nl * e));
   if (s->cfg.nranks > 1)
     GS_HIP(hipMalloc(&s->sym_R, (size_t)gs::kSymGroups * 3 * nl * e));
@@ -384,26 +400,44 @@ int ring_finish(gs_stepper* s, const gs::KArgs<T>& a) {
 // Symmetric schedule, parts: 1 = force + group reduce (+ RCCL group-sum exchange),
 // 2 = finalize (sum + integrate), 3 = both. Virtual-rank groups run part 1 on every shard,
 // exchange by device copies, then part 2 (gs_group_step).
+// Force + reductions over the rank's rows, band by band: zero the group sums, then per band
+// the force units, the group reduce (continuing S_g) and the row reduce (Ti). With one band
+// and a pending all-gather, the diagonal-chunk units (own rows only) run beside the gather
+// and the shell units wait for it.
+int sym_force(gs_stepper* s, gs::SymArgs a, bool overlap_gather) {
+  GS_HIP(hipMemsetAsync(s->sym_S, 0, (size_t)gs::kSymGroups * 3 * s->L.n_local * s->esz,
+                        s->s_comp));
+  for (int b0 = 0; b0 < a.rows; b0 += s->sym_band) {
+    a.band0 = b0;
+    a.band_rows = s->sym_band < a.rows - b0 ? s->sym_band : a.rows - b0;
+    a.units = 0;
+    if (overlap_gather && b0 == 0) {
+      if (a.band_rows == a.rows) {
+        gs::SymArgs d = a;
+        d.units = 1;
+        GS_HIP(gs::launch_force_sym(d, s->s_comp));
+        a.units = 2;
+      }
+      GS_HIP(hipStreamWaitEvent(s->s_comp, s->ev_gathered, 0));
+    }
+    GS_HIP(gs::launch_force_sym(a, s->s_comp));
+    GS_HIP(gs::launch_sym_group_reduce(a, s->s_comp));
+    GS_HIP(gs::launch_sym_row_reduce(a, s->s_comp));
+  }
+  return 0;
+}
+
 int enqueue_sym(gs_stepper* s, int cur, bool need_gather, bool gathered_externally, int part,
                 bool timed) {
   gs::SymArgs a = sym_args(s, cur);
   if (s->emulate) a.Rbuf = s->sym_S;  // timing emulation: no exchange, stale sums
   if (part & 1) {
     if (need_gather) {
-      // The diagonal chunks need only this rank's own rows: they run while the all-gather
-      // of the other ranks' rows is in flight; the shell chunks wait for it.
       if (gathered_externally) s->full[cur] = true;
       else if (gather(s, cur)) return -1;
-      gs::SymArgs d = a;
-      d.units = 1;
-      GS_HIP(gs::launch_force_sym(d, s->s_comp));
-      GS_HIP(hipStreamWaitEvent(s->s_comp, s->ev_gathered, 0));
-      a.units = 2;
     }
-    GS_HIP(gs::launch_force_sym(a, s->s_comp));
-    a.units = 0;
+    if (sym_force(s, a, need_gather)) return -1;
     if (timed) GS_HIP(hipEventRecord(s->ev_local, s->s_comp));
-    GS_HIP(gs::launch_sym_group_reduce(a, s->s_comp));
     if (s->have_comm && sym_exchange_rccl(s)) return -1;
   }
   if (part & 2) GS_HIP(gs::launch_sym_finalize(a, s->s_comp));
@@ -599,8 +633,7 @@ int accel_impl(gs_stepper* s, double* acc4, bool step_path) {
       }
       gs::SymArgs sa = sym_args(s, cur);
       sa.acc_out = s->acc;
-      GS_HIP(gs::launch_force_sym(sa, s->s_comp));
-      GS_HIP(gs::launch_sym_group_reduce(sa, s->s_comp));
+      if (sym_force(s, sa, false)) return -1;
       if (s->have_comm && sym_exchange_rccl(s)) return -1;
       GS_HIP(gs::launch_sym_finalize(sa, s->s_comp));
       GS_HIP(hipStreamSynchronize(s->s_comp));
@@ -729,7 +762,7 @@ int gs_stepper_destroy(gs_stepper* s) {
   if (s->sym_R == s->sym_S) s->sym_R = nullptr;
   for (void* p : {s->X[0], s->X[1], s->vel, s->partial, s->acc, (void*)s->mass_dev,
                   (void*)s->nonfinite, (void*)s->sym_Pi, (void*)s->sym_Pj, (void*)s->sym_Pd,
-                  (void*)s->sym_S, (void*)s->sym_R})
+                  (void*)s->sym_S, (void*)s->sym_R, (void*)s->sym_Ti})
     if (p) (void)hipFree(p);
   for (hipEvent_t e : {s->ev_ready, s->ev_gathered, s->ev_t0, s->ev_local, s->ev_end,
                        s->ev_remote, s->ev_fork, s->ev_rem2, s->ev_sym})

@@ -43,9 +43,11 @@ inline int split_span(const KArgs<T>& a) {
 // itself (one-sided). Row A's shell is cut into segments of L quanta (128 bodies; see
 // gs_sym_geometry), its diagonal chunk into D parts; one workgroup per unit writes an i-side
 // partial (Pi[row][segment] or Pd[row][part]) and, for every shell tile it visits, the
-// j-side partial of its 2048 i-bodies into Pj[row][d-1]. Group reduce: S_g(x) = sum over
-// rows A of group g (A ascending) of Pj[A][x - A]. Final: a = sum_q Pd[q] + sum_s Pi[s]
-// + sum_g S_g (each ascending), then the KD integrate.
+// j-side partial of its 2048 i-bodies into Pj[row][d-1]. Rows are processed in bands (all of
+// a rank's rows unless the partial buffers would exceed the band budget); per band the group
+// reduce continues S_g(x) (rows A of group g ascending, S zeroed at step start) and the row
+// reduce forms Ti = sum_q Pd[q] + sum_s Pi[s]. Final: a = Ti + sum_g S_g (g ascending), then
+// the KD integrate. Every sum runs in the same order for any band size and any P | 8.
 constexpr int kSymC = 2048;
 constexpr int kSymGroups = 8;
 
@@ -55,6 +57,7 @@ struct SymArgs {
   void* Pi;            // [rows][S][3][kSymC] i-side partials (segment = L quanta of 128)
   void* Pj;            // [rows][H][3][kSymC] j-side partials, H = NC / 2
   void* Pd;            // [rows][D][3][kSymC] diagonal-chunk partials
+  void* Ti;            // [3][n_local] per-body i-side total: sum_q Pd[q] + sum_s Pi[s]
   void* Sbuf;          // [P][G/P][3][n_local] group sums by destination rank
   const void* Rbuf;    // [P][G/P][3][n_local] group sums received, by source rank
   void* X_next;        // [n_pad * 4]
@@ -63,6 +66,8 @@ struct SymArgs {
   int64_t n_real, n_local, i_begin;
   int32_t NC, a0, rows, S, L, H, P, real_chunks;
   int32_t D;           // parts of the diagonal chunk (L < 16 quanta: 16 / L)
+  int32_t band0, band_rows;  // rows [band0, band0 + band_rows) of this rank (rank-relative)
+                             // are in the Pi/Pj/Pd buffers (row index - band0)
   int32_t fp64;        // element type of every array above
   int32_t exact;       // reference hard cutoff (select at cut2) instead of the fast core
   int32_t units;       // which units a force launch covers: 0 all, 1 diagonal chunks only
@@ -71,7 +76,8 @@ struct SymArgs {
 };
 
 hipError_t launch_force_sym(const SymArgs& a, hipStream_t s);
-hipError_t launch_sym_group_reduce(const SymArgs& a, hipStream_t s);
+hipError_t launch_sym_group_reduce(const SymArgs& a, hipStream_t s);  // accumulates into Sbuf
+hipError_t launch_sym_row_reduce(const SymArgs& a, hipStream_t s);    // the band's rows -> Ti
 hipError_t launch_sym_finalize(const SymArgs& a, hipStream_t s);
 int sym_occupancy(int fp64);
 

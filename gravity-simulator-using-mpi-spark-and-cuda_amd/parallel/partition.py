@@ -83,6 +83,7 @@ def sym_geometry(n_pad: int) -> dict:
 
 
 def sym_bytes(n_pad: int, nranks: int, esz: int = 4) -> int:
+    """Partial-slot bytes per rank if all of the rank's rows were held at once (one band)."""
     g = sym_geometry(n_pad)
     n_local = n_pad // nranks
     return n_local * 3 * esz * (g["S"] + g["H"] + g["D"]) + 2 * n_local * SYM_GROUPS * 3 * esz
@@ -93,10 +94,8 @@ def sym_auto(n: int, nranks: int, chunk: int = 0, dtype: str = "fp32") -> bool:
     c = chunk or auto_chunk(n)
     if 8 % nranks or n < 65536:
         return False
-    sp = sym_pad(n, c)
-    if sp * 20 > round_up(n, nranks * c) * 21:
-        return False
-    return sym_bytes(sp, nranks, 8 if dtype == "fp64" else 4) <= 160 << 30
+    # the partial slots are processed in bounded bands, so memory does not limit the choice
+    return sym_pad(n, c) * 20 <= round_up(n, nranks * c) * 21
 
 
 def layout(n: int, rank: int = 0, nranks: int = 1, chunk: int = 0, sym: bool = False) -> Layout:

@@ -180,3 +180,25 @@ def test_sym_fp64_close_to_split(hip):
         e.close()
     rel = np.abs(outs["sym"] - outs["split"]).max() / np.abs(outs["split"]).max()
     assert rel < 1e-13
+
+
+@pytest.mark.parametrize("P,dtype", [(1, "fp32"), (2, "fp32"), (1, "fp64")])
+def test_sym_bands_bitwise(hip, monkeypatch, P, dtype):
+    """Processing the rows in many small bands (bounded partial memory) gives the same bits
+    as one band: every sum continues in the same order."""
+    from gravsim.runtime.engines import VirtualGroup
+
+    cfg = SimConfig(n=40000, dtype=dtype, device="gpu", mode="sym")
+    out = []
+    for band_mb in (None, "1"):
+        if band_mb:
+            monkeypatch.setenv("GRAVSIM_SYM_BAND_MB", band_mb)  # one 2048-body row per band
+        else:
+            monkeypatch.delenv("GRAVSIM_SYM_BAND_MB", raising=False)
+        g = VirtualGroup(cfg, P)
+        g.init_ics("solar+random", 17)
+        g.step(3)
+        out.append(g.state())
+        g.close()
+    assert np.array_equal(out[0].pos, out[1].pos)
+    assert np.array_equal(out[0].vel, out[1].vel)
