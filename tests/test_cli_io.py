@@ -149,6 +149,17 @@ def test_config_validation():
         SimConfig(dtype="bf16").validate()
     with pytest.raises(ValueError):
         SimConfig(chunk=1000).validate()
+    # the Newton-3 schedule: both precisions and both cutoff paths; not with the MFMA kernel
+    for kw in (dict(dtype="fp32"), dict(dtype="fp64"), dict(cutoff_mode="exact")):
+        SimConfig(mode="sym", **kw).validate()
+    with pytest.raises(ValueError):
+        SimConfig(mode="sym", kernel="mfma").validate()
+
+
+def test_cli_accepts_sym_mode(capsys):
+    """--mode sym parses (the CPU engine ignores the GPU schedule)."""
+    assert main(["--n", "64", "--steps", "2", "--device", "cpu", "--mode", "sym",
+                 "--log-format", "none"]) == 0
 
 
 @pytest.mark.parametrize("fam", ["plummer", "cold", "random"])
