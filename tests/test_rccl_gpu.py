@@ -1,8 +1,11 @@
-"""Real RCCL path (in-place all-gather + overlapped local chunks) with 2 processes.
+"""Real RCCL path (in-place all-gather + overlapped local chunks, ring pass, the sym
+schedule's group-sum send/recv) with 2 and 4 processes.
 
-The GPU box exposes one MI355X, so both ranks share device 0. If RCCL refuses two ranks on
-one device the test is skipped with RCCL's message; the same schedule is covered on one GPU
-by the virtual-rank tests (device-copy all-gather) and on CPU by the gloo tests.
+The GPU box exposes one MI355X, so every rank shares device 0. RCCL refuses two ranks of one
+host on one device ("Duplicate GPU detected"), so each rank gets its own NCCL_HOSTID: RCCL
+then treats the ranks as separate hosts and moves data through its socket transport over
+loopback instead of xGMI. The collectives, peer calls, stream/event ordering and buffer
+offsets of the multi-rank schedule are the production ones; only the transport differs.
 """
 import os
 import socket
@@ -22,9 +25,16 @@ def _port():
     return p
 
 
-def _worker(rank, world, port, out_dir, n, steps, strategy="allgather"):
+def _rccl_env(rank):
+    # one "host" per rank (see the module docstring); loopback sockets, no IB probing
+    return dict(NCCL_HOSTID=f"gravsim-test-rank{rank}", NCCL_SOCKET_IFNAME="lo",
+                NCCL_IB_DISABLE="1")
+
+
+def _worker(rank, world, port, out_dir, n, steps, strategy="allgather", mode="auto",
+            dtype="fp32"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
-                      WORLD_SIZE=str(world), LOCAL_RANK="0")
+                      WORLD_SIZE=str(world), LOCAL_RANK="0", **_rccl_env(rank))
     import gravsim  # noqa: F401
     from gravsim.config import SimConfig
     from gravsim.parallel import comm
@@ -33,8 +43,8 @@ def _worker(rank, world, port, out_dir, n, steps, strategy="allgather"):
     dist = comm.init(timeout_s=120)
     status = "ok"
     try:
-        cfg = SimConfig(n=n, dtype="fp32", device="gpu", chunk=1024, step_timeout_s=120,
-                        strategy=strategy)
+        cfg = SimConfig(n=n, dtype=dtype, device="gpu", chunk=1024, step_timeout_s=120,
+                        strategy=strategy, mode=mode)
         eng = HipEngine(cfg, rank, world, device=0, dist=dist)
         uid = HipEngine.unique_id() if rank == 0 else None
         uid = comm.broadcast_bytes(dist, uid)
@@ -48,8 +58,12 @@ def _worker(rank, world, port, out_dir, n, steps, strategy="allgather"):
             eng.step(steps)
             eng.sync(timeout_s=120)
             b = eng.state()
+            own = eng.layout.real_local  # velocities are rank-local (positions are gathered)
+            np.save(os.path.join(out_dir, f"vel{rank}.npy"), b.vel[own.start:own.stop])
             if rank == 0:
                 np.save(os.path.join(out_dir, "pos.npy"), b.pos)
+                with open(os.path.join(out_dir, "mode.txt"), "w") as f:
+                    f.write(str(eng.native_layout["mode"]))
         eng.close()
     finally:
         if rank == 0:
@@ -58,23 +72,37 @@ def _worker(rank, world, port, out_dir, n, steps, strategy="allgather"):
         comm.shutdown(dist)
 
 
-@pytest.mark.parametrize("strategy", ["allgather", "ring"])
-def test_rccl_two_ranks_match_single_rank(hip, tmp_path, strategy):
-    n, steps = 5000, 6
-    mp.start_processes(_worker, args=(2, _port(), str(tmp_path), n, steps, strategy), nprocs=2,
-                       start_method="spawn", join=True)
+@pytest.mark.parametrize("world,strategy,mode,dtype,n", [
+    (2, "allgather", "auto", "fp32", 5000),
+    (2, "ring", "auto", "fp32", 5000),
+    (2, "allgather", "sym", "fp32", 20000),
+    (4, "allgather", "sym", "fp32", 20000),
+    (2, "allgather", "sym", "fp64", 20000),
+    (4, "ring", "split", "fp32", 9000),
+])
+def test_rccl_multi_rank_match_single_rank(hip, tmp_path, world, strategy, mode, dtype, n):
+    """P real RCCL ranks (one process each) give the same bits as one rank without a
+    communicator (the canonical decomposition makes the result P-independent)."""
+    steps = 5
+    mp.start_processes(_worker, args=(world, _port(), str(tmp_path), n, steps, strategy, mode,
+                                      dtype),
+                       nprocs=world, start_method="spawn", join=True)
     status = open(tmp_path / "status.txt").read()
-    if status != "ok":
-        pytest.skip(f"RCCL with 2 ranks on one device: {status[:300]}")
+    assert status == "ok", f"RCCL with {world} ranks: {status[:300]}"
     from gravsim.config import SimConfig
     from gravsim.runtime.engines import HipEngine
 
-    eng = HipEngine(SimConfig(n=n, dtype="fp32", device="gpu", chunk=1024))
+    eng = HipEngine(SimConfig(n=n, dtype=dtype, device="gpu", chunk=1024, mode=mode))
     eng.init_ics("solar+random", 5)
     eng.step(steps)
-    ref = eng.state().pos
+    ref = eng.state()
+    ref_mode = eng.native_layout["mode"]
     eng.close()
-    assert np.array_equal(np.load(tmp_path / "pos.npy"), ref)
+    if mode == "sym":  # (the one-sided multi-rank schedule is split; one rank may fuse)
+        assert open(tmp_path / "mode.txt").read() == str(ref_mode)
+    assert np.array_equal(np.load(tmp_path / "pos.npy"), ref.pos)
+    vel = np.concatenate([np.load(tmp_path / f"vel{r}.npy") for r in range(world)])
+    assert np.array_equal(vel, ref.vel)
 
 
 @pytest.mark.parametrize("graph,strategy", [(1, "allgather"), (2, "allgather"), (1, "ring"),
