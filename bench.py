@@ -33,7 +33,9 @@ def main() -> int:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--n", type=int, default=1 << 20)
+    # (under torch.distributed.run spell it --num-bodies: torchrun's parser takes --n as an
+    # ambiguous prefix of its own --nnodes/--nproc-per-node even after the script name)
+    ap.add_argument("--n", "--num-bodies", dest="n", type=int, default=1 << 20)
     ap.add_argument("--dtype", choices=["fp32", "fp64"], default="fp32")
     ap.add_argument("--kernel", default="auto", choices=["auto", "lds", "smem", "mfma"])
     ap.add_argument("--mode", default="auto", choices=["auto", "fused", "split", "sym"])

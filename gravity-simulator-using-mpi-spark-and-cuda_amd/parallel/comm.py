@@ -38,11 +38,24 @@ def env_info() -> DistInfo:
                     local_rank=int(os.environ.get("LOCAL_RANK", os.environ.get("RANK", "0"))))
 
 
+def rccl_rank_hosts(rank: int) -> None:
+    """Rehearsal knob (GRAVSIM_RCCL_RANK_HOSTS=1): give every rank its own NCCL_HOSTID so that
+    RCCL accepts several ranks on ONE GPU (it refuses two ranks of one host on one device) and
+    connects them through its socket transport over loopback. Lets a 1-GPU box run the real
+    multi-rank RCCL schedule (tests/test_rccl_gpu.py, scripts/gpu_torchrun.sh); never set on
+    a multi-GPU node, where the ranks must share a host to use xGMI."""
+    os.environ["NCCL_HOSTID"] = f"gravsim-rank{rank}"
+    os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+    os.environ.setdefault("NCCL_IB_DISABLE", "1")
+
+
 def init(timeout_s: float = 600.0) -> DistInfo:
     """Initialise the gloo control group when WORLD_SIZE > 1 (no-op for a single process)."""
     info = env_info()
     if info.world <= 1:
         return info
+    if os.environ.get("GRAVSIM_RCCL_RANK_HOSTS") == "1":
+        rccl_rank_hosts(info.rank)
     import torch.distributed as dist
 
     if not dist.is_initialized():

@@ -1,0 +1,33 @@
+#!/bin/bash
+# Multi-rank rehearsal on a ONE-GPU box: every rank runs on device 0 and RCCL connects the
+# ranks through its socket transport (GRAVSIM_RCCL_RANK_HOSTS=1 gives each rank its own
+# NCCL_HOSTID, gravsim/parallel/comm.py). Checks the torchrun launch contract of bench.py
+# (one JSON line, max over ranks) and the CLI (--nproc, dumps, checkpoints, resume across
+# rank counts). Throughput here is meaningless (loopback sockets, one shared GPU).
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+mkdir -p gpurun_out/tr
+export TMPDIR=/tmp GRAVSIM_RCCL_RANK_HOSTS=1
+out=gpurun_out/tr
+run="python -m torch.distributed.run --nnodes=1 --master-addr 127.0.0.1"
+timeout -k 10 240 $run --nproc-per-node 2 --master-port 29611 bench.py --gpus 2 --steps 3 \
+  --warmup 1 --num-bodies 65536 > $out/bench2.log 2>&1 || { tail -30 $out/bench2.log; exit 1; }
+grep '^{' $out/bench2.log
+timeout -k 10 240 $run --nproc-per-node 4 --master-port 29612 bench.py --gpus 4 --steps 2 \
+  --warmup 1 --num-bodies 131072 > $out/bench4.log 2>&1 || { tail -30 $out/bench4.log; exit 1; }
+grep '^{' $out/bench4.log
+timeout -k 10 240 $run --nproc-per-node 2 --master-port 29613 bench.py --gpus 2 --steps 2 \
+  --warmup 1 --num-bodies 65536 --strategy ring --mode split > $out/bench2_ring.log 2>&1 \
+  || { tail -30 $out/bench2_ring.log; exit 1; }
+grep '^{' $out/bench2_ring.log
+# CLI: 2 ranks (sym, checkpoint every 3) vs 1 rank, then a 1-rank resume of the 2-rank
+# checkpoint; the three final dumps must be identical text.
+common="--n 40000 --device gpu --mode sym --log-format none --quiet"
+timeout -k 10 240 python -m gravsim $common --steps 6 --nproc 2 --dump $out/p2.txt \
+  --checkpoint-dir $out/ck --checkpoint-every 3 > $out/cli2.log 2>&1 || { tail -30 $out/cli2.log; exit 1; }
+timeout -k 10 240 python -m gravsim $common --steps 6 --dump $out/p1.txt \
+  > $out/cli1.log 2>&1 || { tail -30 $out/cli1.log; exit 1; }
+ck3=$(ls $out/ck/*00000003* | head -1)
+timeout -k 10 240 python -m gravsim $common --steps 3 --resume "$ck3" --dump $out/pr.txt \
+  > $out/clir.log 2>&1 || { tail -30 $out/clir.log; exit 1; }
+cmp $out/p1.txt $out/p2.txt && cmp $out/p1.txt $out/pr.txt && echo "CLI dumps identical (P=2, P=1, P=2 ckpt -> P=1 resume)"

@@ -25,16 +25,11 @@ def _port():
     return p
 
 
-def _rccl_env(rank):
-    # one "host" per rank (see the module docstring); loopback sockets, no IB probing
-    return dict(NCCL_HOSTID=f"gravsim-test-rank{rank}", NCCL_SOCKET_IFNAME="lo",
-                NCCL_IB_DISABLE="1")
-
-
 def _worker(rank, world, port, out_dir, n, steps, strategy="allgather", mode="auto",
             dtype="fp32"):
+    # one "host" per rank (see the module docstring): gravsim.parallel.comm.rccl_rank_hosts
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
-                      WORLD_SIZE=str(world), LOCAL_RANK="0", **_rccl_env(rank))
+                      WORLD_SIZE=str(world), LOCAL_RANK="0", GRAVSIM_RCCL_RANK_HOSTS="1")
     import gravsim  # noqa: F401
     from gravsim.config import SimConfig
     from gravsim.parallel import comm
