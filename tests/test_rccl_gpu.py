@@ -72,6 +72,7 @@ def _worker(rank, world, port, out_dir, n, steps, strategy="allgather", mode="au
     (2, "ring", "auto", "fp32", 5000),
     (2, "allgather", "sym", "fp32", 20000),
     (4, "allgather", "sym", "fp32", 20000),
+    (8, "allgather", "sym", "fp32", 20000),  # the 8-GPU shape: one group per destination
     (2, "allgather", "sym", "fp64", 20000),
     (4, "ring", "split", "fp32", 9000),
 ])
