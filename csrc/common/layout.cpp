@@ -6,6 +6,7 @@
 // equal contiguous slice (RCCL all-gather needs equal counts) and the j-chunk boundaries,
 // hence the floating-point summation order, do not depend on P.
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "gravsim.h"
@@ -113,8 +114,10 @@ extern "C" int gs_layout_compute(const gs_config* cfg, gs_layout* out) {
 // Symmetric-schedule geometry (gs_kernels.h SymArgs), a function of n_pad only:
 //   NC chunks of 2048 bodies; shell H = NC / 2 chunks;
 //   L = segment length in quanta of 128 bodies (16 per chunk): 16 * (NC / 512) from
-//       NC = 512 up, else the largest power of two <= max(1, NC / 32), so a row has
-//       about 256 segments at every size (enough workgroups for one rank of eight);
+//       NC = 512 up (a row has about 256 segments: enough workgroups for one rank of
+//       eight), else the largest power of two <= max(1, NC / 16) (about 128 segments: half
+//       the i-side partial traffic; 1 GPU, profiles/r1_sym_seglen.jsonl: 65K 0.768 vs
+//       0.788 ms at NC / 32, 131K 2.836 vs 2.850, 256K 11.04 vs 11.09, 512K 43.56 vs 43.65);
 //   S = ceil(16 H / L) segments per row; D = max(1, 16 / L) parts of the diagonal chunk.
 extern "C" int gs_sym_geometry(int64_t n_pad, int32_t* NC, int32_t* H, int32_t* L, int32_t* S,
                                int32_t* D) {
@@ -125,9 +128,15 @@ extern "C" int gs_sym_geometry(int64_t n_pad, int32_t* NC, int32_t* H, int32_t* 
   if (nc >= 512) {
     l = 16 * (nc / 512);
   } else {
-    const int32_t want = nc / 32 > 1 ? nc / 32 : 1;
+    const int32_t want = nc / 16 > 1 ? nc / 16 : 1;
     l = 1;
     while (l * 2 <= want) l *= 2;
+  }
+  // Tuning override (A/B sweeps only; changes the summation order, hence the bits):
+  // a power of two up to 16, or a multiple of 16.
+  if (const char* e = getenv("GRAVSIM_SYM_L")) {
+    const int32_t v = atoi(e);
+    if (v >= 1 && ((v <= 16 && (v & (v - 1)) == 0) || v % 16 == 0)) l = v;
   }
   if (NC) *NC = nc;
   if (H) *H = h;

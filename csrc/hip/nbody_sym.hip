@@ -275,16 +275,24 @@ __global__ __launch_bounds__(256) void sym_group_reduce_kernel(SymArgs a) {
   const int R = a.NC / kSymGroups;
   const int g = (a.a0 / R) + gl;
   const int X = (int)(x / kSymC), c = (int)(x % kSymC);
-  // Rows of group g inside the current band; Sbuf was zeroed at step start, so continuing
-  // it band by band adds in the same order as one pass over the group.
+  // Rows of group g inside the current band. The first band starts the sums at 0 (it writes
+  // every entry, so Sbuf needs no clearing); later bands continue them, which adds in the
+  // same order as one pass over the group. Entries of bodies past the real chunks are never
+  // read (finalize zeroes ghost bodies without reading Rbuf).
   const int lo = max(g * R, a.a0 + a.band0);
   const int hi = min(min((g + 1) * R, a.a0 + a.band0 + a.band_rows), a.real_chunks);
-  if (lo >= hi) return;
+  const bool first = a.band0 == 0;
+  if (lo >= hi && !first) return;
   const int q = (int)(x / a.n_local);
   const int64_t xl = x % a.n_local;
   T* o = static_cast<T*>(a.Sbuf) + ((int64_t)q * gpr + gl) * 3 * a.n_local + xl;
   const T* Pj = static_cast<const T*>(a.Pj);
-  T sx = o[0], sy = o[a.n_local], sz = o[2 * a.n_local];
+  T sx = T(0), sy = T(0), sz = T(0);
+  if (!first) {
+    sx = o[0];
+    sy = o[a.n_local];
+    sz = o[2 * a.n_local];
+  }
   for (int A = lo; A < hi; ++A) {
     const int d = (X - A + a.NC) % a.NC;
     if (d == 0 || d > shell_len(A, a.NC)) continue;
@@ -299,32 +307,36 @@ __global__ __launch_bounds__(256) void sym_group_reduce_kernel(SymArgs a) {
 }
 
 // Ti = sum_q Pd[q] + sum_s Pi[s] (each ascending) for the bodies of the band's rows.
+// Grid: (bodies / 256, 3 components). A pure streaming sum with a serial add chain per
+// thread: one component per thread triples the loads in flight, and the loads of 8 segments
+// are issued ahead of their (ordered) adds.
 template <typename T>
 __global__ __launch_bounds__(256) void sym_row_reduce_kernel(SymArgs a) {
   const int64_t b = (int64_t)blockIdx.x * 256 + threadIdx.x;  // body within the band
   if (b >= (int64_t)a.band_rows * kSymC) return;
   const int br = (int)(b / kSymC), c = (int)(b % kSymC);
+  const int k = blockIdx.y;  // component
   const int A = a.a0 + a.band0 + br;
   if ((int64_t)A * kSymC >= a.n_real) return;  // all-ghost row
-  const T* pd = static_cast<const T*>(a.Pd) + (int64_t)br * a.D * 3 * kSymC + c;
-  T ax = pd[0], ay = pd[kSymC], az = pd[2 * kSymC];
-  for (int q = 1; q < a.D; ++q) {
-    ax += pd[q * 3 * kSymC];
-    ay += pd[q * 3 * kSymC + kSymC];
-    az += pd[q * 3 * kSymC + 2 * kSymC];
-  }
+  const T* __restrict__ pd = static_cast<const T*>(a.Pd) + (int64_t)br * a.D * 3 * kSymC +
+                             k * kSymC + c;
+  T acc = pd[0];
+  for (int q = 1; q < a.D; ++q) acc += pd[q * 3 * kSymC];
   const int h = shell_len(A, a.NC);
   const int segs = (16 * h + a.L - 1) / a.L;  // shell length in 128-body quanta / L
-  for (int s = 0; s < segs; ++s) {
-    const T* p = static_cast<const T*>(a.Pi) + ((int64_t)br * a.S + s) * 3 * kSymC + c;
-    ax += p[0];
-    ay += p[kSymC];
-    az += p[2 * kSymC];
+  const T* __restrict__ p = static_cast<const T*>(a.Pi) + (int64_t)br * a.S * 3 * kSymC +
+                            k * kSymC + c;
+  constexpr int U = 8;
+  int s = 0;
+  for (; s + U <= segs; s += U) {
+    T v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = __builtin_nontemporal_load(p + (int64_t)(s + u) * 3 * kSymC);
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc += v[u];
   }
-  T* ti = static_cast<T*>(a.Ti) + (int64_t)(a.band0 + br) * kSymC + c;
-  ti[0] = ax;
-  ti[a.n_local] = ay;
-  ti[2 * a.n_local] = az;
+  for (; s < segs; ++s) acc += __builtin_nontemporal_load(p + (int64_t)s * 3 * kSymC);
+  static_cast<T*>(a.Ti)[(int64_t)k * a.n_local + (int64_t)(a.band0 + br) * kSymC + c] = acc;
 }
 
 // a = Ti + sum_g S_g, then kick-drift (cuda.cu:73-76, mpi.c:207-215) exactly as
@@ -405,7 +417,7 @@ hipError_t launch_sym_group_reduce(const SymArgs& a, hipStream_t s) {
 
 hipError_t launch_sym_row_reduce(const SymArgs& a, hipStream_t s) {
   const int64_t bodies = (int64_t)a.band_rows * kSymC;
-  const dim3 grid((unsigned)((bodies + 255) / 256));
+  const dim3 grid((unsigned)((bodies + 255) / 256), 3);
   if (a.fp64) hipLaunchKernelGGL(sym_row_reduce_kernel<double>, grid, dim3(256), 0, s, a);
   else hipLaunchKernelGGL(sym_row_reduce_kernel<float>, grid, dim3(256), 0, s, a);
   return hipGetLastError();

@@ -400,13 +400,11 @@ int ring_finish(gs_stepper* s, const gs::KArgs<T>& a) {
 // Symmetric schedule, parts: 1 = force + group reduce (+ RCCL group-sum exchange),
 // 2 = finalize (sum + integrate), 3 = both. Virtual-rank groups run part 1 on every shard,
 // exchange by device copies, then part 2 (gs_group_step).
-// Force + reductions over the rank's rows, band by band: zero the group sums, then per band
-// the force units, the group reduce (continuing S_g) and the row reduce (Ti). With one band
+// Force + reductions over the rank's rows, band by band: the force units, the group reduce
+// (the first band starts S_g, later ones continue it) and the row reduce (Ti). With one band
 // and a pending all-gather, the diagonal-chunk units (own rows only) run beside the gather
 // and the shell units wait for it.
 int sym_force(gs_stepper* s, gs::SymArgs a, bool overlap_gather) {
-  GS_HIP(hipMemsetAsync(s->sym_S, 0, (size_t)gs::kSymGroups * 3 * s->L.n_local * s->esz,
-                        s->s_comp));
   for (int b0 = 0; b0 < a.rows; b0 += s->sym_band) {
     a.band0 = b0;
     a.band_rows = s->sym_band < a.rows - b0 ? s->sym_band : a.rows - b0;

@@ -13,6 +13,7 @@ order fixed, so instead:
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 
 
@@ -75,10 +76,13 @@ def sym_geometry(n_pad: int) -> dict:
     if nc >= 512:
         seg = 16 * (nc // 512)
     else:
-        want = max(1, nc // 32)
+        want = max(1, nc // 16)
         seg = 1
         while seg * 2 <= want:
             seg *= 2
+    v = int(os.environ.get("GRAVSIM_SYM_L", "0") or 0)  # tuning override (layout.cpp)
+    if v >= 1 and ((v <= 16 and v & (v - 1) == 0) or v % 16 == 0):
+        seg = v
     return {"NC": nc, "H": h, "L": seg, "S": -(-16 * h // seg), "D": 16 // seg if seg < 16 else 1}
 
 
