@@ -28,13 +28,18 @@ namespace {
 // Workgroup shape per precision: W waves, I i-bodies and J j-bodies per lane; one workgroup
 // holds one 2048-body chunk on its i side (W * 64 * I == kSymC).
 //   fp32: (4 waves, I 8, J 2). (8 waves, I 4, J 4) measured 7 % slower: the per-step j
-//         overhead is amortised over fewer i (profiles/r1_sym_ab.jsonl).
+//         overhead is amortised over fewer i (profiles/r1_sym_ab.jsonl). I 16 (2 waves,
+//         GS_SYM_I32=16) would halve that overhead but needs 256 VGPRs + 94 AGPRs and spills
+//         to scratch (131 VGPRs at I 8).
 //   fp64: (8 waves, I 4, J GS_SYM_J64 = 1): 14 VGPRs per i-body leave no room for I 8.
 template <typename T>
 struct Shape;
+#ifndef GS_SYM_I32
+#define GS_SYM_I32 8
+#endif
 template <>
 struct Shape<float> {
-  static constexpr int W = 4, I = 8, J = 2;
+  static constexpr int I = GS_SYM_I32, W = kSymC / (64 * I), J = 2;
 };
 #ifndef GS_SYM_J64
 #define GS_SYM_J64 1
