@@ -70,6 +70,13 @@ struct Shape<double> {
 template <typename T>
 constexpr bool kJlds = sizeof(T) == 8 || GS_SYM_JLDS;  // (the exact-cutoff kernels need 1)
 
+// fp32 tile packing: j-pairs (1, gs_sym_tile.h tile_lds_jp) or i-pairs (0, tile_lds).
+#ifndef GS_SYM_JPACK
+#define GS_SYM_JPACK 1
+#endif
+template <typename T>
+constexpr bool kJpack = sizeof(T) == 4 && GS_SYM_JPACK && GS_SYM_JLDS && Shape<T>::J == 2;
+
 template <typename T>
 struct Geo {
   static constexpr int W = Shape<T>::W, I = Shape<T>::I, J = Shape<T>::J;
@@ -115,6 +122,37 @@ __device__ __forceinline__ void stage_store(V* dst, int b, const V& q) {
   dst[j * sym::kStagedRows + sym::staged_entry(l, 1)] = q;
 }
 
+// i-set of a lane: i-pair packed accumulators, or j-pair packed ones (kJpack).
+template <typename T>
+using ISetK = typename std::conditional<kJpack<T>, sym::ISetP<Geo<T>::I>,
+                                        sym::ISetT<T, Geo<T>::I>>::type;
+
+// One staging thread's share of a j-tile: one body (thread b < kTileJ), or with kJpack the
+// bodies l and 64 + l (thread l < 64) interleaved into the pair layout of tile_lds_jp.
+template <typename T>
+struct StageQ {
+  static constexpr int kN = kJpack<T> ? 2 : 1;
+  static constexpr int kThreads = kJpack<T> ? 64 : Geo<T>::kTileJ;
+  sym::Vec4<T> q[kN];
+  __device__ __forceinline__ void load(const sym::Vec4<T>* X4, int64_t row0, int t) {
+#pragma unroll
+    for (int k = 0; k < kN; ++k) q[k] = X4[row0 + k * 64 + t];
+  }
+  __device__ __forceinline__ void store(sym::Vec4<T>* dst, int t) const {
+    if constexpr (kJpack<T>) {
+      const float4 p0 = {q[0].x, q[1].x, q[0].y, q[1].y}, p1 = {q[0].z, q[1].z, q[0].w, q[1].w};
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const int e = sym::staged_entry(t, c);
+        dst[2 * e] = p0;
+        dst[2 * e + 1] = p1;
+      }
+    } else {
+      stage_store(dst, t, q[0]);
+    }
+  }
+};
+
 template <typename T>
 struct Smem {
   T slot[2][Geo<T>::W][3][Geo<T>::kTileJ];  // j-side carriers of each wave, double-buffered
@@ -124,8 +162,8 @@ struct Smem {
 // Visit the unit's j-tiles. SYM: pairs both ways, j-side partials to Pj (the diagonal chunk
 // runs with SYM = false: every ordered pair once on the i side).
 template <typename T, bool SYM, bool EXACT>
-__device__ __forceinline__ void run_tiles(const SymArgs& a, sym::ISetT<T, Geo<T>::I>& is,
-                                          TileSeq<T> seq, int br, Smem<T>& sm) {
+__device__ __forceinline__ void run_tiles(const SymArgs& a, ISetK<T>& is, TileSeq<T> seq,
+                                          int br, Smem<T>& sm) {
   static_assert(kJlds<T> || !EXACT, "the DPP-position tile has no exact-cutoff variant");
   using G = Geo<T>;
   using V4 = sym::Vec4<T>;
@@ -134,20 +172,31 @@ __device__ __forceinline__ void run_tiles(const SymArgs& a, sym::ISetT<T, Geo<T>
   const V4* X4 = static_cast<const V4*>(a.X);
   const T eps2 = (T)a.eps2, cut2 = (T)a.cut2;
   int buf = 0, cur = 0;
+  const bool stager = threadIdx.x < StageQ<T>::kThreads;
   if constexpr (kJlds<T>) {
-    if (!seq.done() && threadIdx.x < G::kTileJ)
-      stage_store(sm.jt[0], threadIdx.x, X4[seq.row0() + threadIdx.x]);
+    if (!seq.done() && stager) {
+      StageQ<T> sq;
+      sq.load(X4, seq.row0(), threadIdx.x);
+      sq.store(sm.jt[0], threadIdx.x);
+    }
     __syncthreads();
   }
   while (!seq.done()) {
     TileSeq<T> nx = seq;
     nx.next();
     const int d = seq.d(), t = seq.t();
-    V4 q_next;
-    const bool stage_next = kJlds<T> && !nx.done() && threadIdx.x < G::kTileJ;
-    if (stage_next) q_next = X4[nx.row0() + threadIdx.x];  // lands during the arithmetic
+    StageQ<T> q_next;
+    const bool stage_next = kJlds<T> && !nx.done() && stager;
+    if (stage_next) q_next.load(X4, nx.row0(), threadIdx.x);  // lands during the arithmetic
     T cx[J], cy[J], cz[J];
-    if constexpr (kJlds<T>) {
+    if constexpr (kJpack<T>) {
+      sym::CSetT<T, J> cs;
+#pragma unroll
+      for (int j = 0; j < J; ++j) cs.cx[j] = cs.cy[j] = cs.cz[j] = T(0);
+      sym::tile_lds_jp<G::I, SYM, EXACT>(is, cs, sm.jt[cur], eps2, cut2);
+#pragma unroll
+      for (int j = 0; j < J; ++j) { cx[j] = cs.cx[j]; cy[j] = cs.cy[j]; cz[j] = cs.cz[j]; }
+    } else if constexpr (kJlds<T>) {
       sym::CSetT<T, J> cs;
 #pragma unroll
       for (int j = 0; j < J; ++j) cs.cx[j] = cs.cy[j] = cs.cz[j] = T(0);
@@ -176,7 +225,7 @@ __device__ __forceinline__ void run_tiles(const SymArgs& a, sym::ISetT<T, Geo<T>
       }
     }
     // jt[cur ^ 1] was last read in the previous tile, before the previous barrier.
-    if (stage_next) stage_store(sm.jt[cur ^ 1], threadIdx.x, q_next);
+    if (stage_next) q_next.store(sm.jt[cur ^ 1], threadIdx.x);
     if (kJlds<T> || SYM) __syncthreads();
     if constexpr (SYM) {
       // Sum the waves' carriers in wave order (fixed) and store the tile's j-side partial.
@@ -232,13 +281,13 @@ __device__ __forceinline__ void force_sym_body(const SymArgs& a) {
     seq.u = seq.valid(u0);
   }
   const V4* X4 = static_cast<const V4*>(a.X);
-  sym::ISetT<T, G::I> is;
+  ISetK<T> is;
   const int64_t i_row0 = (int64_t)A * kSymC + w * G::kTileI;
 #pragma unroll
   for (int i = 0; i < G::I; ++i) {
     const V4 q = X4[i_row0 + i * 64 + lane];
     is.x[i] = q.x; is.y[i] = q.y; is.z[i] = q.z; is.mu[i] = q.w;
-    is.ax[i] = is.ay[i] = is.az[i] = T(0);
+    is.ax[i] = is.ay[i] = is.az[i] = std::remove_reference_t<decltype(is.ax[i])>(0);
   }
   T* out;
   if (diag) {
@@ -253,9 +302,15 @@ __device__ __forceinline__ void force_sym_body(const SymArgs& a) {
 #pragma unroll
   for (int i = 0; i < G::I; ++i) {
     const int b = w * G::kTileI + i * 64 + lane;
-    out[b] = is.ax[i];
-    out[kSymC + b] = is.ay[i];
-    out[2 * kSymC + b] = is.az[i];
+    if constexpr (kJpack<T>) {  // slot-0 half + slot-1 half
+      out[b] = is.ax[i].x + is.ax[i].y;
+      out[kSymC + b] = is.ay[i].x + is.ay[i].y;
+      out[2 * kSymC + b] = is.az[i].x + is.az[i].y;
+    } else {
+      out[b] = is.ax[i];
+      out[kSymC + b] = is.ay[i];
+      out[2 * kSymC + b] = is.az[i];
+    }
   }
 }
 

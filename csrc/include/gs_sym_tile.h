@@ -22,6 +22,8 @@
 // + 2 mul (s_i, s_j) + 6 FMA/mul (both accumulators), all packed two pairs per v_pk_*
 // instruction: 4 v_pk + 0.5 v_rsq per interaction, against 6 v_pk + 1 v_rsq for the
 // one-sided loop (nbody_kernels.hip interact_pk). fp64: 20 f64 ops + 1 v_rsq_f64 per pair.
+// fp32 ships the j-pair packed form (tile_lds_jp, below): the pair is the lane's two j-slots
+// against one i-body, so the carriers need no fold of packed halves.
 //
 // Numerics: the pair term uses the fast-cutoff core (r^2 + eps2, nbody_kernels.hip FM_FAST)
 // or, with EXACT, the reference hard cutoff as a select; r^-3 = (y*y)*y with y = rsq(r^2 +
@@ -350,6 +352,131 @@ __device__ __forceinline__ void lds_step(ISetT<T, I>& a, CSetT<T, J>& c, const V
         c.cx[j] = row_from<1>(c.cx[j]) - tx;
         c.cy[j] = row_from<1>(c.cy[j]) - ty;
         c.cz[j] = row_from<1>(c.cz[j]) - tz;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// j-pair packed fp32 variant (J = 2): the two j-slots of a step form the packed pair and the
+// lane's i-bodies are splat operands, instead of packing two i-bodies against one j. The
+// pair arithmetic is the same 16 v_pk + 2 v_rsq per pair-pair, but the j-side sum of a step
+// comes out as one packed value whose halves ARE the two carriers' increments: per step
+// 6 v_sub_f32_dpp move the carriers, against 6 v_add (folding i-pair halves) + 6 v_sub_dpp.
+// The i side accumulates packed (slot-0 and slot-1 halves) and is folded once per unit.
+// Staged layout per entry (same entries as above): two float4, (x0, x1, y0, y1) and
+// (z0, z1, mu0, mu1), so each ds_read_b128 lands packed pairs in register pairs.
+template <int I>
+struct ISetP {
+  float x[I], y[I], z[I], mu[I];
+  f2 ax[I], ay[I], az[I];
+};
+
+#ifndef GS_SYM_UP
+#define GS_SYM_UP 2
+#endif
+template <int I, bool SYM, bool EXACT>
+__device__ __forceinline__ void meet_jp(ISetP<I>& a, f2 xj, f2 yj, f2 zj, f2 mj, float eps2,
+                                        f2& tx, f2& ty, f2& tz, float cut2) {
+  constexpr int U = I % GS_SYM_UP == 0 ? GS_SYM_UP : 1;
+#pragma unroll
+  for (int i0 = 0; i0 < I; i0 += U) {
+    f2 dx[U], dy[U], dz[U], r2[U], y[U], y3[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      dx[u] = xj - f2(a.x[i0 + u]);
+      dy[u] = yj - f2(a.y[i0 + u]);
+      dz[u] = zj - f2(a.z[i0 + u]);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) r2[u] = pk_fma(dx[u], dx[u], f2(eps2));
+#pragma unroll
+    for (int u = 0; u < U; ++u) r2[u] = pk_fma(dy[u], dy[u], r2[u]);
+#pragma unroll
+    for (int u = 0; u < U; ++u) r2[u] = pk_fma(dz[u], dz[u], r2[u]);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      y[u].x = __builtin_amdgcn_rsqf(r2[u].x);
+      y[u].y = __builtin_amdgcn_rsqf(r2[u].y);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) y3[u] = y[u] * y[u];
+#pragma unroll
+    for (int u = 0; u < U; ++u) y3[u] = y3[u] * y[u];
+    if constexpr (EXACT) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        y3[u].x = r2[u].x >= cut2 ? y3[u].x : 0.f;
+        y3[u].y = r2[u].y >= cut2 ? y3[u].y : 0.f;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = i0 + u;
+      const f2 si = mj * y3[u];
+      a.ax[i] = pk_fma(si, dx[u], a.ax[i]);
+      a.ay[i] = pk_fma(si, dy[u], a.ay[i]);
+      a.az[i] = pk_fma(si, dz[u], a.az[i]);
+    }
+    if constexpr (SYM) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int i = i0 + u;
+        const f2 sj = f2(a.mu[i]) * y3[u];
+        if (i == 0) {
+          tx = sj * dx[u]; ty = sj * dy[u]; tz = sj * dz[u];
+        } else {
+          tx = pk_fma(sj, dx[u], tx);
+          ty = pk_fma(sj, dy[u], ty);
+          tz = pk_fma(sj, dz[u], tz);
+        }
+      }
+    }
+  }
+}
+
+template <int I, bool SYM, bool EXACT, int K>
+__device__ __forceinline__ void lds_step_jp(ISetP<I>& a, CSetT<float, 2>& c, const float4* base,
+                                            float eps2, float cut2) {
+  const float4 p = base[2 * K], q = base[2 * K + 1];
+  f2 tx, ty, tz;
+  meet_jp<I, SYM, EXACT>(a, f2{p.x, p.y}, f2{p.z, p.w}, f2{q.x, q.y}, f2{q.z, q.w}, eps2, tx,
+                         ty, tz, cut2);
+  if constexpr (SYM) {
+    c.cx[0] = row_from<1>(c.cx[0]) - tx.x;
+    c.cx[1] = row_from<1>(c.cx[1]) - tx.y;
+    c.cy[0] = row_from<1>(c.cy[0]) - ty.x;
+    c.cy[1] = row_from<1>(c.cy[1]) - ty.y;
+    c.cz[0] = row_from<1>(c.cz[0]) - tz.x;
+    c.cz[1] = row_from<1>(c.cz[1]) - tz.y;
+  }
+}
+
+template <int I, bool SYM, bool EXACT, int... Ks>
+__device__ __forceinline__ void lds_row_pass_jp(ISetP<I>& a, CSetT<float, 2>& c,
+                                                const float4* base, float eps2, float cut2,
+                                                std::integer_sequence<int, Ks...>) {
+  (lds_step_jp<I, SYM, EXACT, Ks>(a, c, base, eps2, cut2), ...);
+}
+
+// All (64 I) x 128 pairs against the pair-staged j-tile (LDS). Carriers return home.
+template <int I, bool SYM, bool EXACT>
+__device__ __forceinline__ void tile_lds_jp(ISetP<I>& a, CSetT<float, 2>& c, const float4* tile,
+                                            float eps2, float cut2) {
+  const int lane = static_cast<int>(__lane_id());
+  const int R = lane >> 4, col = lane & 15;
+  const int addr = ((lane + 48) & 63) << 2;
+#pragma unroll 1
+  for (int p = 0; p < 4; ++p) {
+    const float4* base = tile + 2 * (((R - p) & 3) * 32 + (16 - col));
+    lds_row_pass_jp<I, SYM, EXACT>(a, c, base, eps2, cut2,
+                                   std::make_integer_sequence<int, 16>{});
+    if constexpr (SYM) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        c.cx[j] = wave_from_minus16(c.cx[j], addr);
+        c.cy[j] = wave_from_minus16(c.cy[j], addr);
+        c.cz[j] = wave_from_minus16(c.cz[j], addr);
       }
     }
   }
