@@ -372,8 +372,11 @@ struct ISetP {
   f2 ax[I], ay[I], az[I];
 };
 
+// i-bodies per stage group: each group's rsq burst is followed by an s_nop (trans-use
+// hazard); 4 halves the groups. 1M: U 4 169.42 ms, U 2 170.6, U 8 170.2 (alternating runs,
+// profiles/r1_sym_ab_jpack.jsonl).
 #ifndef GS_SYM_UP
-#define GS_SYM_UP 2
+#define GS_SYM_UP 4
 #endif
 template <int I, bool SYM, bool EXACT>
 __device__ __forceinline__ void meet_jp(ISetP<I>& a, f2 xj, f2 yj, f2 zj, f2 mj, float eps2,
