@@ -96,10 +96,11 @@ def main() -> int:
     if rank == 0:
         value = cfg.n * a.steps / wall
         mode = _native.MODE_NAMES.get(lay["mode"])
-        sym = mode == "sym" and not fmode["exact"]
-        if sym:
+        if mode == "sym":
             # Newton-3 schedule: each unordered pair once, both sides (nbody_sym.hip).
-            kernel_info = {"kernel": "sym: DPP/LDS register tile, 8 i x 2 j per lane, "
+            tile = ("8 i x 2 j per lane, j-pair packed fp32" if a.dtype == "fp32"
+                    else "4 i x 1 j per lane, fp64")
+            kernel_info = {"kernel": f"sym: register tile (LDS-staged j, DPP carriers), {tile}, "
                                      "cyclic half-shell of 2048-body chunks",
                            "n_pad": lay["n_pad"]}
             exch = "all-gather + group-sum send/recv"

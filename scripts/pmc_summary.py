@@ -19,3 +19,13 @@ for path in glob.glob(sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc_*/**
 for k, v in sorted(rows.items()):
     print(f"{k:32s} {v:.6g}")
 print("kernels:", dict(kern))
+# fp32 tiles issue one v_rsq_f32 per pair-evaluation (per wave: 64 of them), so wave-level
+# VALU instructions per trans instruction = VALU issue per pair, rsq included.
+trans = rows.get("SQ_INSTS_VALU_TRANS_F32", 0.0)
+if trans and rows.get("SQ_INSTS_VALU"):
+    print(f"{'VALU instructions per rsq':32s} {rows['SQ_INSTS_VALU'] / trans:.3f}")
+if rows.get("SQ_INSTS_LDS") and trans:
+    print(f"{'LDS instructions per rsq':32s} {rows['SQ_INSTS_LDS'] / trans:.3f}")
+if rows.get("SQ_ACTIVE_INST_VALU") and rows.get("SQ_BUSY_CYCLES"):
+    print(f"{'VALU-active / busy cycles':32s} "
+          f"{rows['SQ_ACTIVE_INST_VALU'] / rows['SQ_BUSY_CYCLES']:.3f}")
