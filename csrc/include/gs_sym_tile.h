@@ -365,7 +365,10 @@ __device__ __forceinline__ void lds_step(ISetT<T, I>& a, CSetT<T, J>& c, const V
 // 6 v_sub_f32_dpp move the carriers, against 6 v_add (folding i-pair halves) + 6 v_sub_dpp.
 // The i side accumulates packed (slot-0 and slot-1 halves) and is folded once per unit.
 // Staged layout per entry (same entries as above): two float4, (x0, x1, y0, y1) and
-// (z0, z1, mu0, mu1), so each ds_read_b128 lands packed pairs in register pairs.
+// (z0, z1, mu0, mu1), so each ds_read_b128 lands packed pairs in register pairs. The 32-byte
+// lane stride costs LDS bank conflicts (1.3e10 conflict cycles in 3 steps at 1M) but the LDS
+// pipe has slack: two 16-byte planes remove them and measured 0.4 % slower (167.75 vs
+// 167.07 ms, alternating runs, profiles/r1_sym_ab_jpack.jsonl).
 template <int I>
 struct ISetP {
   float x[I], y[I], z[I], mu[I];

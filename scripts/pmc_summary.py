@@ -26,6 +26,6 @@ if trans and rows.get("SQ_INSTS_VALU"):
     print(f"{'VALU instructions per rsq':32s} {rows['SQ_INSTS_VALU'] / trans:.3f}")
 if rows.get("SQ_INSTS_LDS") and trans:
     print(f"{'LDS instructions per rsq':32s} {rows['SQ_INSTS_LDS'] / trans:.3f}")
-if rows.get("SQ_ACTIVE_INST_VALU") and rows.get("SQ_BUSY_CYCLES"):
-    print(f"{'VALU-active / busy cycles':32s} "
-          f"{rows['SQ_ACTIVE_INST_VALU'] / rows['SQ_BUSY_CYCLES']:.3f}")
+if rows.get("SQ_LDS_BANK_CONFLICT") is not None and rows.get("SQ_LDS_IDX_ACTIVE"):
+    print(f"{'LDS bank-conflict / active cycles':32s} "
+          f"{rows['SQ_LDS_BANK_CONFLICT'] / rows['SQ_LDS_IDX_ACTIVE']:.3f}")
