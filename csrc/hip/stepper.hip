@@ -216,7 +216,9 @@ gs::SymArgs sym_args(gs_stepper* s, int cur) {
 
 // Group-sum exchange of the symmetric schedule: rank r sends S_g(x) of its groups for the
 // bodies of rank q to q (ncclSend/ncclRecv pairs, one group call) and keeps its own block.
-int sym_exchange_rccl(gs_stepper* s) {
+// With join = false the compute stream does not wait for it yet (the caller joins with
+// hipStreamWaitEvent(s_comp, ev_sym) after work that does not read Rbuf).
+int sym_exchange_rccl(gs_stepper* s, bool join = true) {
   const int P = s->cfg.nranks, r = s->cfg.rank;
   const size_t cnt = (size_t)(gs::kSymGroups / P) * 3 * s->L.n_local;  // elements
   const size_t bytes = cnt * s->esz;
@@ -235,7 +237,7 @@ int sym_exchange_rccl(gs_stepper* s) {
     GS_NCCL(ncclGroupEnd());
   }
   GS_HIP(hipEventRecord(s->ev_sym, s->s_comm));
-  GS_HIP(hipStreamWaitEvent(s->s_comp, s->ev_sym, 0));
+  if (join) GS_HIP(hipStreamWaitEvent(s->s_comp, s->ev_sym, 0));
   return 0;
 }
 
@@ -403,8 +405,10 @@ int ring_finish(gs_stepper* s, const gs::KArgs<T>& a) {
 // Force + reductions over the rank's rows, band by band: the force units, the group reduce
 // (the first band starts S_g, later ones continue it) and the row reduce (Ti). With one band
 // and a pending all-gather, the diagonal-chunk units (own rows only) run beside the gather
-// and the shell units wait for it.
-int sym_force(gs_stepper* s, gs::SymArgs a, bool overlap_gather) {
+// and the shell units wait for it. With `exchange` the RCCL group-sum exchange starts right
+// after the last group reduce and runs beside the last row reduce; the compute stream joins
+// it afterwards.
+int sym_force(gs_stepper* s, gs::SymArgs a, bool overlap_gather, bool exchange = false) {
   for (int b0 = 0; b0 < a.rows; b0 += s->sym_band) {
     a.band0 = b0;
     a.band_rows = s->sym_band < a.rows - b0 ? s->sym_band : a.rows - b0;
@@ -420,7 +424,10 @@ int sym_force(gs_stepper* s, gs::SymArgs a, bool overlap_gather) {
     }
     GS_HIP(gs::launch_force_sym(a, s->s_comp));
     GS_HIP(gs::launch_sym_group_reduce(a, s->s_comp));
+    const bool last = b0 + a.band_rows >= a.rows;
+    if (exchange && last && sym_exchange_rccl(s, false)) return -1;
     GS_HIP(gs::launch_sym_row_reduce(a, s->s_comp));
+    if (exchange && last) GS_HIP(hipStreamWaitEvent(s->s_comp, s->ev_sym, 0));
   }
   return 0;
 }
@@ -434,9 +441,8 @@ int enqueue_sym(gs_stepper* s, int cur, bool need_gather, bool gathered_external
       if (gathered_externally) s->full[cur] = true;
       else if (gather(s, cur)) return -1;
     }
-    if (sym_force(s, a, need_gather)) return -1;
+    if (sym_force(s, a, need_gather, s->have_comm)) return -1;
     if (timed) GS_HIP(hipEventRecord(s->ev_local, s->s_comp));
-    if (s->have_comm && sym_exchange_rccl(s)) return -1;
   }
   if (part & 2) GS_HIP(gs::launch_sym_finalize(a, s->s_comp));
   return 0;
