@@ -257,10 +257,10 @@ __device__ __forceinline__ void force_sym_body(const SymArgs& a) {
   if (a.units == 1) {
     br = blockIdx.x / a.D;
     s = a.S + blockIdx.x % a.D;
-  } else if (a.units == 2) {
+  } else if (a.units == 2 || a.units == 4) {  // shell units: all (2) or the non-local ones (4)
     br = blockIdx.x / a.S;
     s = blockIdx.x % a.S;
-  } else {
+  } else {  // every unit (0), or the diagonal ones + the rank-local shell ones (5)
     br = blockIdx.x / (a.S + a.D);
     s = blockIdx.x % (a.S + a.D);
   }
@@ -278,6 +278,12 @@ __device__ __forceinline__ void force_sym_body(const SymArgs& a) {
     const int u0 = s * seg_tiles;
     if (u0 >= h_tiles) return;  // past this row's shell: never read
     seq.u1 = min(u0 + seg_tiles, h_tiles);
+    if (a.units >= 4) {
+      // Rank-local: every j-chunk of the segment is one of the rank's own rows, so it needs
+      // no gathered positions (chunks A+1 .. < a0 + rows: no wrap below NC).
+      const bool local = A + 1 + (seq.u1 - 1) / G::kTilesPerChunk < a.a0 + a.rows;
+      if (local != (a.units == 5)) return;
+    }
     seq.u = seq.valid(u0);
   }
   const V4* X4 = static_cast<const V4*>(a.X);
@@ -448,7 +454,8 @@ __global__ __launch_bounds__(256) void sym_finalize_kernel(SymArgs a) {
 
 template <typename T>
 hipError_t launch_force_sym_t(const SymArgs& a, hipStream_t s) {
-  const int units = a.band_rows * (a.units == 1 ? a.D : a.units == 2 ? a.S : a.S + a.D);
+  const int units = a.band_rows * (a.units == 1 ? a.D : (a.units == 2 || a.units == 4) ? a.S
+                                                                                      : a.S + a.D);
   if (units <= 0) return hipSuccess;
   const dim3 grid(units), block(Geo<T>::kThreads);
   if constexpr (sizeof(T) == 8) {

@@ -23,11 +23,13 @@
 //
 // Newton-3 sym schedule (GS_MODE_SYM, the default from 64K bodies; nbody_sym.hip):
 //   s_comm : ncclAllGather in place (as above)
-//   s_comp : diagonal-chunk units (own rows only, beside the gather) -> wait(gathered)
-//            -> shell units (both sides of every pair) -> group reduce
-//   s_comm : group-sum exchange: ncclSend/ncclRecv to every peer (one group call)
+//   s_comp : wait(gathered) -> every unit in one launch (diagonal chunks one-sided, shell
+//            chunks both sides of every pair) -> group reduce
+//   s_comm : group-sum exchange: ncclSend/ncclRecv to every peer (one group call), beside
+//            the row reduce on s_comp
 //   s_comp : wait(exchange) -> finalize (fixed-order sum + KD integrate) -> own slice of
 //            X[(k+1)&1]
+// (work beside the gather: see sym_force; a launch boundary costs more than the gather.)
 // The partial slots and summation order depend on N only, so every P dividing 8 gives the
 // same bits.
 #include <dlfcn.h>
@@ -97,6 +99,10 @@ struct gs_stepper {
   bool have_comm = false;
   bool virt = false;  // member of a virtual-rank group (gather = device copies, gs_group_step)
   bool emulate = false;  // GRAVSIM_EMULATE_RANK: run one rank's launch shapes, no exchange
+  // sym work beside a pending gather (GRAVSIM_SYM_OVERLAP): 0 none (wait, then one launch),
+  // 1 the diagonal units first on the compute stream, 2 diagonal + rank-local shell units
+  // concurrently with the rest on a second stream.
+  int sym_overlap = 0;
   hipGraphExec_t graph = nullptr;
   bool timed = false;  // eager steps record phase events
   int own_c0 = 0, own_c1 = 0;  // this rank's chunks clipped to [0, n_chunks)
@@ -404,8 +410,18 @@ int ring_finish(gs_stepper* s, const gs::KArgs<T>& a) {
 // exchange by device copies, then part 2 (gs_group_step).
 // Force + reductions over the rank's rows, band by band: the force units, the group reduce
 // (the first band starts S_g, later ones continue it) and the row reduce (Ti). With one band
-// and a pending all-gather, the diagonal-chunk units (own rows only) run beside the gather
-// and the shell units wait for it. With `exchange` the RCCL group-sum exchange starts right
+// and a pending all-gather (sym_overlap, GRAVSIM_SYM_OVERLAP):
+//   0 (default): wait for the gather, then one launch of every unit;
+//   1: the diagonal-chunk units (own rows only) run beside the gather, then the shell units
+//     after it;
+//   2: the diagonal units and the shell segments whose j-chunks are all own rows (1M, P = 8:
+//     2080 of 16448 units) run on s_comp beside the gather and the other shell units on
+//     s_rem after it, concurrently.
+// A unit is ~0.6 ms of work at 1M, so every extra launch boundary drains the GPU for about
+// that long, while the gather it would hide is ~0.1 ms (14.7 MB per rank over xGMI).
+// Per-rank emulation of 1M, P = 8 (gather treated as done), alternating runs: 0: 21.0-21.2 ms,
+// 1: 21.4-21.6, 2: 22.4-22.6 (profiles/r1_sym_overlap_ab.txt).
+// With `exchange` the RCCL group-sum exchange starts right
 // after the last group reduce and runs beside the last row reduce; the compute stream joins
 // it afterwards.
 int sym_force(gs_stepper* s, gs::SymArgs a, bool overlap_gather, bool exchange = false) {
@@ -413,16 +429,31 @@ int sym_force(gs_stepper* s, gs::SymArgs a, bool overlap_gather, bool exchange =
     a.band0 = b0;
     a.band_rows = s->sym_band < a.rows - b0 ? s->sym_band : a.rows - b0;
     a.units = 0;
-    if (overlap_gather && b0 == 0) {
-      if (a.band_rows == a.rows) {
-        gs::SymArgs d = a;
-        d.units = 1;
-        GS_HIP(gs::launch_force_sym(d, s->s_comp));
-        a.units = 2;
-      }
+    const bool one_band = a.band_rows == a.rows;
+    const int ov = s->sym_overlap;
+    if (overlap_gather && b0 == 0 && one_band && ov == 1) {
+      gs::SymArgs d = a;
+      d.units = 1;  // diagonal chunks beside the gather
+      GS_HIP(gs::launch_force_sym(d, s->s_comp));
       GS_HIP(hipStreamWaitEvent(s->s_comp, s->ev_gathered, 0));
+      a.units = 2;
+      GS_HIP(gs::launch_force_sym(a, s->s_comp));
+    } else if (overlap_gather && b0 == 0 && one_band && ov == 2) {
+      // fork: s_rem starts after everything already on s_comp (X[cur] written) and the gather
+      GS_HIP(hipEventRecord(s->ev_fork, s->s_comp));
+      GS_HIP(hipStreamWaitEvent(s->s_rem, s->ev_fork, 0));
+      GS_HIP(hipStreamWaitEvent(s->s_rem, s->ev_gathered, 0));
+      gs::SymArgs r = a;
+      r.units = 4;  // shell segments that read gathered rows
+      GS_HIP(gs::launch_force_sym(r, s->s_rem));
+      GS_HIP(hipEventRecord(s->ev_remote, s->s_rem));
+      a.units = 5;  // diagonal + rank-local shell units, beside the gather
+      GS_HIP(gs::launch_force_sym(a, s->s_comp));
+      GS_HIP(hipStreamWaitEvent(s->s_comp, s->ev_remote, 0));  // join
+    } else {
+      if (overlap_gather && b0 == 0) GS_HIP(hipStreamWaitEvent(s->s_comp, s->ev_gathered, 0));
+      GS_HIP(gs::launch_force_sym(a, s->s_comp));
     }
-    GS_HIP(gs::launch_force_sym(a, s->s_comp));
     GS_HIP(gs::launch_sym_group_reduce(a, s->s_comp));
     const bool last = b0 + a.band_rows >= a.rows;
     if (exchange && last && sym_exchange_rccl(s, false)) return -1;
@@ -689,6 +720,7 @@ int gs_stepper_create(const gs_config* cfg, gs_stepper** out) {
   s->esz = cfg->dtype == GS_FP64 ? 8 : 4;
   s->timed = getenv("GRAVSIM_PHASE_TIMING") != nullptr;
   s->emulate = getenv("GRAVSIM_EMULATE_RANK") != nullptr && cfg->nranks > 1;
+  if (const char* ov = getenv("GRAVSIM_SYM_OVERLAP")) s->sym_overlap = atoi(ov);
   const int64_t own_first = s->L.local_begin / s->L.chunk;
   const int64_t own_last = (s->L.local_begin + s->L.n_local) / s->L.chunk;
   s->own_c0 = (int)(own_first < s->L.n_chunks ? own_first : s->L.n_chunks);

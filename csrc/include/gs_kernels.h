@@ -71,7 +71,9 @@ struct SymArgs {
   int32_t fp64;        // element type of every array above
   int32_t exact;       // reference hard cutoff (select at cut2) instead of the fast core
   int32_t units;       // which units a force launch covers: 0 all, 1 diagonal chunks only
-                       // (need only the own rows), 2 shell chunks only
+                       // (need only the own rows), 2 shell segments only, 4 the shell
+                       // segments with a j-chunk outside the own rows, 5 every other unit
+                       // (diagonal + rank-local shell: no gathered positions needed)
   double dt, eps2, cut2;
 };
 
