@@ -136,34 +136,10 @@ def run_one(cfg: SimConfig, dist, log, quiet: bool = False, final: bool = True) 
 
 def _launch(nproc: int, argv: list[str]) -> int:
     """Re-run this CLI as `nproc` ranks under torch.distributed.run in a child process (no
-    exec, nothing has touched the GPU yet); rendezvous on 127.0.0.1."""
-    import os
-    import socket
-    import subprocess
+    exec, nothing has touched the GPU yet); rendezvous on 127.0.0.1 (parallel/launch.py)."""
+    from .parallel import launch
 
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    rest, skip = [], False
-    for x in argv:  # drop --nproc/--gpus N; torchrun's own options make --n ambiguous
-        if skip:
-            skip = False
-            continue
-        if x in ("--nproc", "--gpus"):
-            skip = True
-            continue
-        if x.startswith(("--nproc=", "--gpus=")):
-            continue
-        rest.append("--num-bodies" if x == "--n" else
-                    "--num-bodies=" + x[4:] if x.startswith("--n=") else x)
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = dict(os.environ)
-    env["PYTHONPATH"] = root + (os.pathsep + env["PYTHONPATH"] if env.get("PYTHONPATH") else "")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node",
-           str(nproc), "--master-addr", "127.0.0.1", "--master-port", str(port), "-m",
-           "gravsim", *rest]
-    return subprocess.call(cmd, env=env)
+    return launch.spawn(nproc, ["-m", "gravsim"], argv)
 
 
 def main(argv: Optional[list[str]] = None) -> int:
