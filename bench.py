@@ -7,15 +7,22 @@ the Newton-3 schedule: every unordered pair is evaluated once and applied to bot
 (csrc/hip/nbody_sym.hip). Each rank owns N/P bodies (a block of 2048-body chunk rows), joins
 an in-place RCCL all-gather of positions, evaluates its rows' cyclic half-shell of chunk
 pairs, exchanges the group sums of the far sides with ncclSend/ncclRecv, and integrates its
-own bodies (kick-drift). --mode split runs the one-sided schedule instead.
+own bodies (kick-drift). Single-rank steps replay a hipGraph; multi-rank steps run eagerly
+(--graph-comm captures them, collectives included).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--n BODIES] [--dtype fp32|fp64]
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
-A step is the full simulation step: all-gather + force + integrate (no work skipped).
-Data: synthetic Sun/Earth/Mars + uniform random bodies generated on device (seeded).
-Rank 0 prints ONE JSON line; value is the whole-job body-updates/s = N * K / max_rank(wall).
+Run without a launcher, `--gpus N > 1` starts N ranks itself: a child torch.distributed.run
+on 127.0.0.1 (parallel/launch.py; the reference's `mpirun -np P`, mpi.c:140-144), before
+anything touches the GPU. Under a launcher, WORLD_SIZE must equal --gpus.
+
+A step is the full simulation step: all-gather + force + exchange + integrate (no work
+skipped). Data: synthetic Sun/Earth/Mars + uniform random bodies generated on device
+(seeded). Rank 0 prints ONE JSON line; value is the whole-job body-updates/s =
+N * K / max_rank(wall). Outside the timed region: a sampled accuracy check of the step's own
+accelerations (before the warmup) and a few eager steps with phase events for the comm split.
 """
 from __future__ import annotations
 
@@ -25,10 +32,13 @@ import os
 import sys
 import time
 
-sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "body-updates/sec (whole node) at N=1M direct O(N^2), 1/2/4/8 MI355X"
 
 
-def main() -> int:
+def parse(argv=None) -> argparse.Namespace:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
@@ -41,13 +51,74 @@ def main() -> int:
     ap.add_argument("--mode", default="auto", choices=["auto", "fused", "split", "sym"])
     ap.add_argument("--ipl", type=int, default=0)
     ap.add_argument("--no-graph", dest="graph", action="store_false")
-    ap.add_argument("--graph-comm", action="store_true",
-                    help="capture the multi-rank step incl. the RCCL all-gather in a hipGraph")
+    ap.add_argument("--graph-comm", dest="graph_comm", action="store_true",
+                    help="capture multi-rank steps, RCCL collectives included, in a hipGraph")
+    ap.add_argument("--no-graph-comm", dest="graph_comm", action="store_false",
+                    help=argparse.SUPPRESS)
+    ap.add_argument("--overlap", type=int, default=None, choices=[0, 1, 2, 3],
+                    help="sym work beside the all-gather (default: GRAVSIM_SYM_OVERLAP or 0)")
     ap.add_argument("--dt", type=float, default=3600.0)
     ap.add_argument("--cutoff-mode", default="auto", choices=["auto", "exact", "fast"])
     ap.add_argument("--strategy", default="allgather", choices=["allgather", "ring"],
                     help="multi-rank exchange: in-place all-gather or pipelined ring pass")
-    a = ap.parse_args()
+    ap.add_argument("--check-samples", type=int, default=256,
+                    help="bodies whose step-0 accelerations are checked against an fp64 row "
+                         "sum on the host (0 = skip)")
+    ap.add_argument("--phase-steps", type=int, default=3,
+                    help="eager steps with phase events after the timed loop (comm split)")
+    return ap.parse_args(argv)
+
+
+def sampled_error(eng, cfg, samples: int, seed: int = 7) -> float:
+    """Max over sampled own bodies of |a_gpu - a_ref| / |a_ref|, where a_gpu is the step's own
+    force path (sym kernels, configured cutoff mode) and a_ref an fp64 row sum over all N
+    bodies by the native CPU engine (4 blocks of samples/4 contiguous rows). Collective."""
+    import numpy as np
+
+    from gravsim.ops import _native
+
+    a_gpu = eng.accel(step_path=True)  # (n_local, 4), collective for P > 1
+    st = eng.state()  # full positions (collective)
+    L = eng.layout
+    real = max(0, min(L.n_local, cfg.n - L.local_begin))
+    if samples <= 0 or real == 0:
+        return 0.0
+    rng = np.random.default_rng(seed + eng.rank)
+    blk = max(1, min(samples // 4, real))
+    starts = sorted(set(int(x) for x in rng.integers(0, real - blk + 1, size=4)))
+    mu = cfg.G * st.mass
+    X = np.zeros((L.n_pad, 4))
+    X[:cfg.n, :3] = st.pos
+    X[:cfg.n, 3] = mu
+    lib = _native.cpu_lib()
+    worst = 0.0
+    eps2 = cfg.softening ** 2  # the intended physics: hard cutoff, no core (SURVEY §2.7)
+    for s0 in starts:
+        g0 = L.local_begin + s0
+        out = np.zeros((blk, 4))
+        _native.check(lib, lib.gs_cpu_accel_f64(_native.dptr(X), cfg.n, g0, g0 + blk, L.chunk,
+                                                cfg.cutoff ** 2, eps2, _native.dptr(out)),
+                      "cpu accel")
+        ref = out[:, :3]
+        got = a_gpu[s0:s0 + blk, :3]
+        err = np.linalg.norm(got - ref, axis=1) / np.maximum(np.linalg.norm(ref, axis=1), 1e-300)
+        worst = max(worst, float(err.max()))
+    return worst
+
+
+def main(argv=None) -> int:
+    raw = list(sys.argv[1:] if argv is None else argv)
+    a = parse(raw)
+    world_env = int(os.environ.get("WORLD_SIZE", "0") or 0)
+    if world_env == 0 and a.gpus > 1:
+        # No launcher: start the ranks ourselves (child process; nothing touched the GPU).
+        from gravsim.parallel import launch
+
+        launch.check_device_count(a.gpus)
+        return launch.spawn(a.gpus, [os.path.join(ROOT, "bench.py")], raw, keep_gpus=True)
+    if world_env and world_env != a.gpus:
+        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE {world_env}: run one rank per GPU "
+                         "(torch.distributed.run --nproc-per-node must equal --gpus)")
 
     import torch
 
@@ -59,22 +130,32 @@ def main() -> int:
 
     dist = comm.init()
     world, rank = dist.world, dist.rank
-    if world != a.gpus and world > 1:
-        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE {world}")
+    if world != a.gpus:
+        raise SystemExit(f"--gpus {a.gpus} but the job has {world} rank(s)")
     if not torch.cuda.is_available():
         raise SystemExit("bench.py needs a HIP device (MI355X)")
-    dev = dist.local_rank % torch.cuda.device_count()
+    ndev = torch.cuda.device_count()
+    if world > ndev and os.environ.get("GRAVSIM_RCCL_RANK_HOSTS") != "1":
+        raise SystemExit(f"{world} ranks but {ndev} visible GPU(s)")
+    dev = dist.local_rank % ndev
     torch.cuda.set_device(dev)
 
     cfg = SimConfig(n=a.n, dt=a.dt, dtype=a.dtype, device="gpu", kernel=a.kernel, mode=a.mode,
                     ipl=a.ipl, graph=a.graph, graph_comm=a.graph_comm,
                     cutoff_mode=a.cutoff_mode, strategy=a.strategy).validate()
     eng = HipEngine(cfg, rank, world, device=dev, dist=dist)
+    if a.overlap is not None:
+        eng.set_overlap(a.overlap)
     if world > 1:
         uid = HipEngine.unique_id() if rank == 0 else None
         eng.comm_init(comm.broadcast_bytes(dist, uid))
     eng.init_ics("solar+random", cfg.seed)
     eng.sync()
+
+    # Accuracy of the step's own force path at step 0 (untimed).
+    err = sampled_error(eng, cfg, a.check_samples) if a.check_samples > 0 else None
+    if err is not None:
+        err = comm.allreduce_max(dist, err)
 
     eng.step(a.warmup)
     eng.sync()
@@ -90,6 +171,15 @@ def main() -> int:
     wall = comm.allreduce_max(dist, t1 - t0)
 
     bad = comm.allreduce_sum(dist, eng.nonfinite())
+    # Comm/compute split (untimed): a few eager steps with per-step phase events.
+    phase = None
+    if a.phase_steps > 0:
+        eng.set_timing(True)
+        eng.step(a.phase_steps)
+        phase = eng.phase_stats()
+        eng.set_timing(False)
+        for k in ("step_ms", "comm_ms", "exposed_comm_ms", "gather_ms", "exchange_ms"):
+            phase[k] = comm.allreduce_max(dist, phase[k])
     lay = eng.native_layout
     fmode = eng.force_mode()
     eng.close()
@@ -104,14 +194,16 @@ def main() -> int:
                                      "cyclic half-shell of 2048-body chunks",
                            "n_pad": lay["n_pad"]}
             exch = "all-gather + group-sum send/recv"
+            pairs = cfg.n * (cfg.n - 1) / 2  # unordered pairs, each evaluated once
         else:
             kernel_info = {"kernel": _native.KERNEL_NAMES.get(lay["kernel"]), "ipl": lay["ipl"],
                            "chunk": lay["chunk"]}
             exch = "ring send/recv" if a.strategy == "ring" else "all-gather"
+            pairs = float(cfg.n) * cfg.n  # one-sided: every ordered pair evaluated
         parallelism = (f"body-decomposition x{world} (RCCL {exch})" if world > 1
                        else "single GPU")
         out = {
-            "metric": "body-updates/sec (whole node) at N=1M direct O(N^2), 1/2/4/8 MI355X",
+            "metric": METRIC,
             "value": value,
             "unit": "body-updates/s",
             "n_gpus": world,
@@ -135,12 +227,21 @@ def main() -> int:
                 "cutoff_path": "exact-select" if fmode["exact"] else
                 f"fast (core^2={fmode['eps2']:.3g} m^2; bit-identical to the 1e-10 m hard cutoff "
                 "for separations above ~mm)",
-                # N^2 pair terms per step (the sym schedule evaluates each unordered pair
-                # once and applies it to both bodies: N(N-1)/2 pair evaluations).
-                "interactions_per_s": float(cfg.n) * cfg.n * a.steps / wall,
+                "graph": bool(a.graph and (world == 1 or a.graph_comm)),
+                # N^2 ordered pair terms per step (what a one-sided sum evaluates) ...
+                "effective_interactions_per_s": float(cfg.n) * cfg.n * a.steps / wall,
+                # ... and the pair evaluations actually performed (sym: N(N-1)/2 per step)
+                "pair_evals_per_s": pairs * a.steps / wall,
+                "sampled_rel_err": err,
                 "nonfinite": int(bad),
             },
         }
+        if phase is not None:
+            out["comm_ms"] = phase["comm_ms"]
+            out["exposed_comm_ms"] = phase["exposed_comm_ms"]
+            out["config"]["phase"] = {k: phase[k] for k in (
+                "steps", "step_ms", "gather_ms", "exchange_ms", "exposed_gather_ms",
+                "exposed_exchange_ms", "gate_wait_ms", "gate_timeouts")}
         print(json.dumps(out), flush=True)
     comm.shutdown(dist)
     return 0

@@ -1,15 +1,20 @@
 """Per-GPU step time of ONE rank of a P-rank run, measured on one GPU.
 
-Runs rank r's exact launch shapes (local chunks + remote chunks on two compute streams +
-reduce/integrate) with the all-gather treated as done (GRAVSIM_EMULATE_RANK=1), so
-ms/step ~ what each GPU of a P-GPU node spends on compute per step; the RCCL all-gather is
-overlapped with the local chunks in the real run. Predicted strong-scaling efficiency =
-ms(P=1) / (P * ms(P)).  Not physics: remote slices hold stale positions.
-    python bench/rank_shape.py --n 1048576 --ranks 1,2,4,8
+Runs rank r's exact launch shapes (sym: gather -> force units -> group reduce -> group-sum
+exchange beside the row reduce -> finalize; split: local + remote chunks on two compute
+streams -> reduce/integrate) under GRAVSIM_EMULATE_RANK=1. The collectives are either free
+(--comm-gbps 0, round 1's emulation) or modeled: a comm_model kernel of the collective's
+exact byte count on the comm stream that stays resident for latency + bytes / rate
+(csrc/hip/comm_model.hip), so the emulated step pays for an xGMI all-gather and exchange
+and shows how much of it the schedule hides. Predicted strong-scaling efficiency =
+ms(P=1) / (P * ms(P)). Not physics: remote slices hold stale positions.
+
+    python bench/rank_shape.py --n 1048576 --ranks 1,2,4,8 --comm-gbps 0,64 --overlap 0,3
 """
 from __future__ import annotations
 
 import argparse
+import itertools
 import json
 import os
 import sys
@@ -29,24 +34,35 @@ def main() -> int:
     ap.add_argument("--kernel", default="auto", help="comma list")
     ap.add_argument("--strategy", default="allgather", help="comma list: allgather,ring")
     ap.add_argument("--mode", default="auto", help="comma list: auto,split,sym")
+    ap.add_argument("--comm-gbps", default="0",
+                    help="comma list of modeled per-rank collective rates in GB/s (0: free)")
+    ap.add_argument("--comm-us", type=float, default=15.0, help="modeled latency per collective")
+    ap.add_argument("--comm-wgs", type=int, default=16, help="workgroups of a modeled collective")
+    ap.add_argument("--overlap", default="0", help="comma list of sym overlap modes 0..3")
+    ap.add_argument("--graph", action="store_true", help="replay multi-rank steps from a graph")
+    ap.add_argument("--rank", type=int, default=-1, help="emulated rank (default: the last)")
     a = ap.parse_args()
+    os.environ["GRAVSIM_EMU_COMM_US"] = str(a.comm_us)
+    os.environ["GRAVSIM_EMU_COMM_WGS"] = str(a.comm_wgs)
     import torch  # noqa: F401
 
     import gravsim  # noqa: F401
     from gravsim.config import SimConfig
     from gravsim.runtime.engines import HipEngine
 
-    base = None
-    import itertools
-
+    base = {}
     grid = list(itertools.product([int(x) for x in a.ranks.split(",")],
                                   [int(x) for x in a.ipl.split(",")], a.kernel.split(","),
-                                  a.strategy.split(","), a.mode.split(",")))
-    for P, ipl, kernel, strategy, mode in grid:
+                                  a.strategy.split(","), a.mode.split(","),
+                                  [float(x) for x in a.comm_gbps.split(",")],
+                                  [int(x) for x in a.overlap.split(",")]))
+    for P, ipl, kernel, strategy, mode, gbps, ov in grid:
+        os.environ["GRAVSIM_EMU_COMM_GBPS"] = str(gbps)
         cfg = SimConfig(n=a.n, dtype=a.dtype, device="gpu", ipl=ipl, kernel=kernel,
-                        strategy=strategy, mode=mode)
-        r = P - 1 if P > 1 else 0  # a rank with its own chunks at the end
+                        strategy=strategy, mode=mode, graph_comm=a.graph)
+        r = (a.rank if a.rank >= 0 else P - 1) if P > 1 else 0
         e = HipEngine(cfg, r, P)
+        e.set_overlap(ov)
         e.init_ics("solar+random", cfg.seed)
         e.step(2)
         e.sync()
@@ -54,11 +70,21 @@ def main() -> int:
         e.step(a.steps)
         e.sync()
         ms = 1e3 * (time.perf_counter() - t0) / a.steps
-        base = base or ms * P
+        phase = None
+        if P > 1:
+            e.set_timing(True)
+            e.step(2)
+            phase = e.phase_stats()
+            e.set_timing(False)
+        key = (ipl, kernel, strategy, mode, a.dtype)
+        if P == 1:
+            base[key] = ms
+        b = base.get(key)
         print(json.dumps(dict(P=P, rank=r, n=a.n, dtype=a.dtype, ipl=ipl, kernel=kernel,
-                              strategy=strategy, mode=e.native_layout["mode"], ms_per_step=ms,
-                              predicted_efficiency=base / (P * ms),
-                              predicted_body_updates_per_s=a.n / (ms * 1e-3),
+                              strategy=strategy, mode=e.native_layout["mode"], comm_gbps=gbps,
+                              comm_us=a.comm_us, overlap=ov, graph=a.graph, ms_per_step=ms,
+                              predicted_efficiency=(b / (P * ms)) if b else None,
+                              predicted_body_updates_per_s=a.n / (ms * 1e-3), phase=phase,
                               layout=e.native_layout)), flush=True)
         e.close()
     return 0

@@ -244,6 +244,73 @@ __device__ __forceinline__ void run_tiles(const SymArgs& a, ISetK<T>& is, TileSe
   }
 }
 
+// Shell segments of row A whose j-chunks all lie in the rank's own rows: a prefix of the
+// row's segments (chunks A+1 .. < a0 + rows, wrapped chunks count as remote). Segment s is
+// local iff A + 1 + (min((s+1) * seg_tiles, h_tiles) - 1) / T < a0 + rows.
+template <typename T>
+__device__ __forceinline__ int local_segs(const SymArgs& a, int A, int seg_tiles) {
+  constexpr int kT = Geo<T>::kTilesPerChunk;
+  const int h_tiles = shell_len(A, a.NC) * kT;
+  const int segs = (h_tiles + seg_tiles - 1) / seg_tiles;
+  const int own_after = a.a0 + a.rows - 1 - A;
+  if (own_after <= 0) return 0;
+  if (h_tiles <= own_after * kT) return segs;
+  return min(segs, own_after * kT / seg_tiles);
+}
+
+// units 6: the grid lists every unit of the band, local ones (diagonal parts, then the
+// rank-local shell segments, row by row) before the remote ones (row by row). Workgroups are
+// dispatched in grid order, so the gathered rows are needed only after ~the local share of
+// the step has been handed out. Returns true for a remote (gated) unit.
+template <typename T>
+__device__ __forceinline__ bool local_first_unit(const SymArgs& a, int b, int* br, int* s) {
+  const int seg_tiles = a.L * Geo<T>::kTilesPerQuantum;
+  for (int r = 0; r < a.band_rows; ++r) {
+    const int n = a.D + local_segs<T>(a, a.a0 + a.band0 + r, seg_tiles);
+    if (b < n) {
+      *br = r;
+      *s = b < a.D ? a.S + b : b - a.D;
+      return false;
+    }
+    b -= n;
+  }
+  for (int r = 0; r < a.band_rows; ++r) {
+    const int nl = local_segs<T>(a, a.a0 + a.band0 + r, seg_tiles);
+    if (b < a.S - nl) {
+      *br = r;
+      *s = nl + b;
+      return true;
+    }
+    b -= a.S - nl;
+  }
+  *br = a.band_rows;  // unreachable for grid = band_rows * (S + D)
+  *s = 0;
+  return false;
+}
+
+// Remote unit of a gated launch: wait (one lane, then the workgroup) until the comm stream
+// has published the all-gather. The agent-scope acquire orders the following position reads
+// after the collective's writes. Bounded: past gate_ticks the unit raises gate_diag[0] and
+// proceeds (the host reports the step as failed) instead of hanging the GPU.
+__device__ __forceinline__ void gate_wait(const SymArgs& a) {
+  if (threadIdx.x == 0) {
+    const uint64_t t0 = wall_clock64();
+    uint64_t waited = 0;
+    while (__hip_atomic_load(a.gate, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
+      __builtin_amdgcn_s_sleep(4);
+      waited = wall_clock64() - t0;
+      if (waited > a.gate_ticks) {
+        __hip_atomic_store(a.gate_diag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+    if (waited > 0)
+      __hip_atomic_fetch_max(a.gate_diag + 1, (unsigned)min(waited, (uint64_t)0xffffffffu),
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+}
+
 // One workgroup per unit (row a, segment s); s == S is the row's diagonal chunk.
 template <typename T, bool EXACT>
 __device__ __forceinline__ void force_sym_body(const SymArgs& a) {
@@ -254,7 +321,10 @@ __device__ __forceinline__ void force_sym_body(const SymArgs& a) {
   // Units per row: S shell segments, then D parts of the diagonal chunk.
   // br: row within the band (index into Pi/Pj/Pd); the rank's row is band0 + br.
   int br, s;
-  if (a.units == 1) {
+  bool gated = false;
+  if (a.units == 6) {
+    gated = local_first_unit<T>(a, blockIdx.x, &br, &s) && a.gate != nullptr;
+  } else if (a.units == 1) {
     br = blockIdx.x / a.D;
     s = a.S + blockIdx.x % a.D;
   } else if (a.units == 2 || a.units == 4) {  // shell units: all (2) or the non-local ones (4)
@@ -278,7 +348,7 @@ __device__ __forceinline__ void force_sym_body(const SymArgs& a) {
     const int u0 = s * seg_tiles;
     if (u0 >= h_tiles) return;  // past this row's shell: never read
     seq.u1 = min(u0 + seg_tiles, h_tiles);
-    if (a.units >= 4) {
+    if (a.units == 4 || a.units == 5) {
       // Rank-local: every j-chunk of the segment is one of the rank's own rows, so it needs
       // no gathered positions (chunks A+1 .. < a0 + rows: no wrap below NC).
       const bool local = A + 1 + (seq.u1 - 1) / G::kTilesPerChunk < a.a0 + a.rows;
@@ -286,6 +356,7 @@ __device__ __forceinline__ void force_sym_body(const SymArgs& a) {
     }
     seq.u = seq.valid(u0);
   }
+  if (gated) gate_wait(a);
   const V4* X4 = static_cast<const V4*>(a.X);
   ISetK<T> is;
   const int64_t i_row0 = (int64_t)A * kSymC + w * G::kTileI;
@@ -411,6 +482,9 @@ template <typename T>
 __global__ __launch_bounds__(256) void sym_finalize_kernel(SymArgs a) {
   using V4 = sym::Vec4<T>;
   const int64_t li = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  // The gated force launch of this step has completed (stream order): re-arm its gate for
+  // the next all-gather into the same buffer (two steps on).
+  if (a.gate && li == 0) __hip_atomic_store(a.gate, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (li >= a.n_local) return;
   const int64_t gi = a.i_begin + li;
   V4* vel = static_cast<V4*>(a.vel);
@@ -456,6 +530,7 @@ template <typename T>
 hipError_t launch_force_sym_t(const SymArgs& a, hipStream_t s) {
   const int units = a.band_rows * (a.units == 1 ? a.D : (a.units == 2 || a.units == 4) ? a.S
                                                                                       : a.S + a.D);
+  if (a.units == 6 && a.band_rows != a.rows) return hipErrorInvalidValue;  // one band only
   if (units <= 0) return hipSuccess;
   const dim3 grid(units), block(Geo<T>::kThreads);
   if constexpr (sizeof(T) == 8) {

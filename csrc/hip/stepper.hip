@@ -120,6 +120,32 @@ struct gs_stepper {
   int32_t sym_NC = 0, sym_H = 0, sym_L = 0, sym_S_n = 0, sym_D = 1;
   int32_t sym_band = 0;  // rows per band (Pi/Pj/Pd hold one band)
   hipEvent_t ev_sym = nullptr;
+  // Per-rank emulation with modeled collectives (GRAVSIM_EMU_COMM_GBPS > 0): every all-gather
+  // and group-sum exchange becomes a comm_model_kernel of the same byte count on s_comm.
+  double emu_gbps = 0.0, emu_lat_us = 15.0;
+  int emu_wgs = 16;
+  void* emu_buf = nullptr;
+  size_t emu_cap = 0;
+  double clk_khz = 100000.0;  // device wall clock (wall_clock64) rate
+  // Gather gates (sym_overlap 3): [0], [1] gate of X[0] / X[1]; [2] timeout flag; [3] longest
+  // wait of a gated unit in wall-clock ticks (since the last phase_stats call).
+  unsigned* gate_buf = nullptr;
+  bool gate_used = false;
+  double gate_timeout_s = 10.0;
+  // Phase timing of eager steps (timed): one event set per step, summed by phase_stats.
+  struct PhaseEv {
+    hipEvent_t t0, end, g0, g1, w0, w1, x0, x1, j0, j1;
+    bool g, w, x, j;
+  };
+  std::vector<PhaseEv> pev;
+  int pev_used = 0;
+  PhaseEv* pe = nullptr;  // the step being enqueued
+  // Progress events (one per enqueued step or graph period) for the bounded wait: its
+  // deadline restarts whenever one more completes, so it bounds progress, not the run.
+  std::vector<hipEvent_t> prog;
+  int64_t prog_rec = 0, prog_done = 0;
+  double step_timeout_s = 0.0;  // 0: unbounded
+  bool graph_failed = false;    // multi-rank capture refused: eager fallback
 };
 
 namespace {
@@ -158,6 +184,53 @@ struct Range {
 };
 
 size_t row_bytes(const gs_stepper* s) { return 4 * s->esz; }
+
+// A multi-rank exchange is active: a real communicator, or the per-rank emulation.
+bool xcomm(const gs_stepper* s) { return s->have_comm || s->emulate; }
+// Remote slices must be brought in before they are read (RCCL, emulation, virtual ranks).
+bool multi(const gs_stepper* s) { return s->have_comm || s->emulate || s->virt; }
+
+// Bytes one rank receives per step: the all-gather's remote slices, and the group sums the
+// other ranks send it (sym schedule).
+size_t gather_bytes(const gs_stepper* s) {
+  return (size_t)(s->cfg.nranks - 1) * s->L.n_local * row_bytes(s);
+}
+size_t exchange_bytes(const gs_stepper* s) {
+  return (size_t)(s->cfg.nranks - 1) * (gs::kSymGroups / s->cfg.nranks) * 3 * s->L.n_local *
+         s->esz;
+}
+
+// Emulated collective on s_comm (GRAVSIM_EMU_COMM_GBPS > 0): the byte count moved through HBM
+// by emu_wgs workgroups that stay resident for latency + bytes / rate (comm_model.hip).
+int comm_model(gs_stepper* s, const void* src, size_t bytes) {
+  if (s->emu_gbps <= 0.0 || bytes == 0) return 0;
+  if (bytes > s->emu_cap) bytes = s->emu_cap;  // (sized at create for the larger collective)
+  const double us = s->emu_lat_us + (double)bytes / (s->emu_gbps * 1e3);
+  const uint64_t ticks = (uint64_t)(us * s->clk_khz / 1e3);
+  GS_HIP(gs::launch_comm_model(src, s->emu_buf, bytes, ticks, s->emu_wgs, s->s_comm));
+  return 0;
+}
+
+// Phase events of the step being enqueued (timed eager steps; at most 256 per phase_stats).
+gs_stepper::PhaseEv* phase_begin(gs_stepper* s) {
+  if (s->pev_used >= (int)s->pev.size()) {
+    if (s->pev.size() >= 256) return nullptr;
+    gs_stepper::PhaseEv e{};
+    for (hipEvent_t* p : {&e.t0, &e.end, &e.g0, &e.g1, &e.w0, &e.w1, &e.x0, &e.x1, &e.j0, &e.j1})
+      if (hipEventCreate(p) != hipSuccess) return nullptr;
+    s->pev.push_back(e);
+  }
+  gs_stepper::PhaseEv* p = &s->pev[s->pev_used++];
+  p->g = p->w = p->x = p->j = false;
+  return p;
+}
+#define GS_MARK(field, flag, stream)                             \
+  do {                                                           \
+    if (s->pe) {                                                 \
+      GS_HIP(hipEventRecord(s->pe->field, (stream)));            \
+      s->pe->flag = true;                                        \
+    }                                                            \
+  } while (0)
 
 template <typename T>
 gs::KArgs<T> base_args(gs_stepper* s, int cur) {
@@ -217,6 +290,9 @@ gs::SymArgs sym_args(gs_stepper* s, int cur) {
   a.cut2 = s->cfg.cutoff * s->cfg.cutoff;
   a.band0 = 0;
   a.band_rows = a.rows;
+  a.gate = nullptr;
+  a.gate_diag = s->gate_buf + 2;
+  a.gate_ticks = (uint64_t)(s->gate_timeout_s * s->clk_khz * 1e3);
   return a;
 }
 
@@ -231,9 +307,12 @@ int sym_exchange_rccl(gs_stepper* s, bool join = true) {
   const ncclDataType_t dt = s->esz == 8 ? ncclFloat64 : ncclFloat32;
   GS_HIP(hipEventRecord(s->ev_ready, s->s_comp));
   GS_HIP(hipStreamWaitEvent(s->s_comm, s->ev_ready, 0));
+  GS_MARK(x0, x, s->s_comm);
   GS_HIP(hipMemcpyAsync(s->sym_R + (size_t)r * bytes, s->sym_S + (size_t)r * bytes, bytes,
                         hipMemcpyDeviceToDevice, s->s_comm));
-  if (P > 1) {
+  if (s->emulate) {
+    if (comm_model(s, s->sym_S, exchange_bytes(s))) return -1;
+  } else if (P > 1) {
     GS_NCCL(ncclGroupStart());
     for (int q = 0; q < P; ++q) {
       if (q == r) continue;
@@ -242,8 +321,13 @@ int sym_exchange_rccl(gs_stepper* s, bool join = true) {
     }
     GS_NCCL(ncclGroupEnd());
   }
+  GS_MARK(x1, x, s->s_comm);
   GS_HIP(hipEventRecord(s->ev_sym, s->s_comm));
-  if (join) GS_HIP(hipStreamWaitEvent(s->s_comp, s->ev_sym, 0));
+  if (join) {
+    GS_MARK(j0, j, s->s_comp);
+    GS_HIP(hipStreamWaitEvent(s->s_comp, s->ev_sym, 0));
+    GS_MARK(j1, j, s->s_comp);
+  }
   return 0;
 }
 
@@ -332,14 +416,26 @@ int choose_groups(gs_stepper* s, int span, bool phi, bool concurrent = false) {
   return best;
 }
 
-int gather(gs_stepper* s, int cur) {
-  if (!s->have_comm || s->full[cur]) return 0;
+// In-place all-gather of X[cur] on s_comm (ev_gathered marks completion). With `gate` the
+// comm stream also publishes completion to a force launch already running (units 6).
+int gather(gs_stepper* s, int cur, bool gate = false) {
+  if (!xcomm(s) || s->full[cur]) return 0;
   char* buf = static_cast<char*>(s->X[cur]);
   const size_t count = (size_t)s->L.n_local * 4;
   GS_HIP(hipEventRecord(s->ev_ready, s->s_comp));
   GS_HIP(hipStreamWaitEvent(s->s_comm, s->ev_ready, 0));
-  GS_NCCL(ncclAllGather(buf + (size_t)s->cfg.rank * s->L.n_local * row_bytes(s), buf, count,
-                        s->esz == 4 ? ncclFloat32 : ncclFloat64, s->comm, s->s_comm));
+  GS_MARK(g0, g, s->s_comm);
+  if (s->emulate) {
+    if (comm_model(s, buf, gather_bytes(s))) return -1;
+  } else {
+    GS_NCCL(ncclAllGather(buf + (size_t)s->cfg.rank * s->L.n_local * row_bytes(s), buf, count,
+                          s->esz == 4 ? ncclFloat32 : ncclFloat64, s->comm, s->s_comm));
+  }
+  GS_MARK(g1, g, s->s_comm);
+  if (gate) {
+    GS_HIP(gs::launch_gate_set(s->gate_buf + cur, s->s_comm));
+    s->gate_used = true;
+  }
   GS_HIP(hipEventRecord(s->ev_gathered, s->s_comm));
   s->full[cur] = true;
   return 0;
@@ -431,7 +527,12 @@ int sym_force(gs_stepper* s, gs::SymArgs a, bool overlap_gather, bool exchange =
     a.units = 0;
     const bool one_band = a.band_rows == a.rows;
     const int ov = s->sym_overlap;
-    if (overlap_gather && b0 == 0 && one_band && ov == 1) {
+    if (overlap_gather && b0 == 0 && one_band && a.gate) {
+      // 3: one launch, local units first, remote units gated in-kernel on the gather.
+      a.units = 6;
+      GS_HIP(gs::launch_force_sym(a, s->s_comp));
+      a.units = 0;
+    } else if (overlap_gather && b0 == 0 && one_band && ov == 1) {
       gs::SymArgs d = a;
       d.units = 1;  // diagonal chunks beside the gather
       GS_HIP(gs::launch_force_sym(d, s->s_comp));
@@ -451,14 +552,22 @@ int sym_force(gs_stepper* s, gs::SymArgs a, bool overlap_gather, bool exchange =
       GS_HIP(gs::launch_force_sym(a, s->s_comp));
       GS_HIP(hipStreamWaitEvent(s->s_comp, s->ev_remote, 0));  // join
     } else {
-      if (overlap_gather && b0 == 0) GS_HIP(hipStreamWaitEvent(s->s_comp, s->ev_gathered, 0));
+      if (overlap_gather && b0 == 0) {
+        GS_MARK(w0, w, s->s_comp);
+        GS_HIP(hipStreamWaitEvent(s->s_comp, s->ev_gathered, 0));
+        GS_MARK(w1, w, s->s_comp);
+      }
       GS_HIP(gs::launch_force_sym(a, s->s_comp));
     }
     GS_HIP(gs::launch_sym_group_reduce(a, s->s_comp));
     const bool last = b0 + a.band_rows >= a.rows;
     if (exchange && last && sym_exchange_rccl(s, false)) return -1;
     GS_HIP(gs::launch_sym_row_reduce(a, s->s_comp));
-    if (exchange && last) GS_HIP(hipStreamWaitEvent(s->s_comp, s->ev_sym, 0));
+    if (exchange && last) {
+      GS_MARK(j0, j, s->s_comp);
+      GS_HIP(hipStreamWaitEvent(s->s_comp, s->ev_sym, 0));
+      GS_MARK(j1, j, s->s_comp);
+    }
   }
   return 0;
 }
@@ -466,13 +575,18 @@ int sym_force(gs_stepper* s, gs::SymArgs a, bool overlap_gather, bool exchange =
 int enqueue_sym(gs_stepper* s, int cur, bool need_gather, bool gathered_externally, int part,
                 bool timed) {
   gs::SymArgs a = sym_args(s, cur);
-  if (s->emulate) a.Rbuf = s->sym_S;  // timing emulation: no exchange, stale sums
+  if (s->emulate) a.Rbuf = s->sym_S;  // timing emulation: modeled exchange, stale sums
+  // Gate the remote units on the gather in-kernel (GRAVSIM_SYM_OVERLAP=3): a collective of
+  // this stepper (RCCL or modeled) and one band (the gated launch covers every unit).
+  const bool gated = part == 3 && need_gather && !gathered_externally && xcomm(s) &&
+                     s->sym_overlap == 3 && s->sym_band >= a.rows;
+  if (gated) a.gate = s->gate_buf + cur;
   if (part & 1) {
     if (need_gather) {
       if (gathered_externally) s->full[cur] = true;
-      else if (gather(s, cur)) return -1;
+      else if (gather(s, cur, gated)) return -1;
     }
-    if (sym_force(s, a, need_gather, s->have_comm)) return -1;
+    if (sym_force(s, a, need_gather, xcomm(s))) return -1;
     if (timed) GS_HIP(hipEventRecord(s->ev_local, s->s_comp));
   }
   if (part & 2) GS_HIP(gs::launch_sym_finalize(a, s->s_comp));
@@ -488,17 +602,21 @@ int enqueue_step(gs_stepper* s, bool capturing, bool gathered_externally) {
   const int kernel = s->L.kernel, ipl = s->L.ipl;
   const bool fused = s->L.mode == GS_MODE_FUSED;
   const bool timed = s->timed && !capturing;
+  s->pe = timed ? phase_begin(s) : nullptr;
   if (timed) GS_HIP(hipEventRecord(s->ev_t0, s->s_comp));
-  const bool need_gather = (s->have_comm || s->virt) && !s->full[cur];
+  if (s->pe) GS_HIP(hipEventRecord(s->pe->t0, s->s_comp));
+  const bool need_gather = multi(s) && !s->full[cur];
   if (use_sym(s)) {
     if (enqueue_sym(s, cur, need_gather, gathered_externally, 3, timed)) return -1;
     if (timed) GS_HIP(hipEventRecord(s->ev_end, s->s_comp));
-    s->full[cur ^ 1] = !(s->have_comm || s->virt);
+    if (s->pe) GS_HIP(hipEventRecord(s->pe->end, s->s_comp));
+    s->pe = nullptr;
+    s->full[cur ^ 1] = !multi(s);
     s->k += 1;
     return 0;
   }
   const bool ring = s->cfg.strategy == GS_STRATEGY_RING;
-  if (need_gather && ring && (s->emulate || !gathered_externally)) {
+  if (need_gather && ring && !gathered_externally) {
     // Ring pass with RCCL (or timing emulation: no transfer, slices treated as present).
     GS_HIP(hipEventRecord(s->ev_fork, s->s_comp));
     GS_HIP(hipStreamWaitEvent(s->s_rem, s->ev_fork, 0));
@@ -516,6 +634,8 @@ int enqueue_step(gs_stepper* s, bool capturing, bool gathered_externally) {
     }
     if (ring_finish<T>(s, a)) return -1;
     if (timed) GS_HIP(hipEventRecord(s->ev_end, s->s_comp));
+    if (s->pe) GS_HIP(hipEventRecord(s->pe->end, s->s_comp));
+    s->pe = nullptr;
     s->full[cur] = true;
     s->full[cur ^ 1] = false;
     s->k += 1;
@@ -559,7 +679,9 @@ int enqueue_step(gs_stepper* s, bool capturing, bool gathered_externally) {
     }
   }
   if (timed) GS_HIP(hipEventRecord(s->ev_end, s->s_comp));
-  s->full[cur ^ 1] = !(s->have_comm || s->virt);  // only the own slice of X[next] is fresh
+  if (s->pe) GS_HIP(hipEventRecord(s->pe->end, s->s_comp));
+  s->pe = nullptr;
+  s->full[cur ^ 1] = !multi(s);  // only the own slice of X[next] is fresh
   s->k += 1;
   return 0;
 }
@@ -623,7 +745,7 @@ template <typename T>
 int download_state(gs_stepper* s, double* pos, double* vel, double* mass) {
   const int cur = (int)(s->k & 1);
   if (pos && gather(s, cur)) return -1;
-  if (pos && s->have_comm) GS_HIP(hipStreamWaitEvent(s->s_comp, s->ev_gathered, 0));
+  if (pos && xcomm(s)) GS_HIP(hipStreamWaitEvent(s->s_comp, s->ev_gathered, 0));
   // A virtual-rank shard between steps holds only its own slice: return just those rows.
   const bool own_only = s->virt && !s->full[cur];
   GS_HIP(hipStreamSynchronize(s->s_comp));
@@ -659,7 +781,7 @@ int accel_impl(gs_stepper* s, double* acc4, bool step_path) {
     return -1;
   }
   if (gather(s, cur)) return -1;
-  if (s->have_comm) GS_HIP(hipStreamWaitEvent(s->s_comp, s->ev_gathered, 0));
+  if (xcomm(s)) GS_HIP(hipStreamWaitEvent(s->s_comp, s->ev_gathered, 0));
   {
     if (step_path && use_sym(s)) {
       if (s->virt && s->cfg.nranks > 1) {
@@ -669,7 +791,7 @@ int accel_impl(gs_stepper* s, double* acc4, bool step_path) {
       gs::SymArgs sa = sym_args(s, cur);
       sa.acc_out = s->acc;
       if (sym_force(s, sa, false)) return -1;
-      if (s->have_comm && sym_exchange_rccl(s)) return -1;
+      if (xcomm(s) && sym_exchange_rccl(s)) return -1;
       GS_HIP(gs::launch_sym_finalize(sa, s->s_comp));
       GS_HIP(hipStreamSynchronize(s->s_comp));
       std::vector<T> A((size_t)s->L.n_local * 4);
@@ -692,6 +814,89 @@ int accel_impl(gs_stepper* s, double* acc4, bool step_path) {
   std::vector<T> A((size_t)s->L.n_local * 4);
   GS_HIP(hipMemcpy(A.data(), s->acc, A.size() * sizeof(T), hipMemcpyDeviceToHost));
   for (size_t i = 0; i < A.size(); ++i) acc4[i] = (double)A[i];
+  return 0;
+}
+
+// A gated force launch (GRAVSIM_SYM_OVERLAP=3) reported that a remote unit gave up waiting
+// for the all-gather: that step read stale positions, so the run has failed.
+int gate_check(gs_stepper* s) {
+  if (!s->gate_used) return 0;
+  unsigned f = 0;
+  GS_HIP(hipMemcpy(&f, s->gate_buf + 2, sizeof(f), hipMemcpyDeviceToHost));
+  if (f) {
+    gs_set_error("gather gate timed out: a force unit waited longer than GRAVSIM_GATE_TIMEOUT_S "
+                 "for the all-gather (the step is invalid)");
+    return -1;
+  }
+  return 0;
+}
+
+// Wait until progress event `target` - 1 has completed (target == prog_rec: every stream is
+// idle). The deadline restarts whenever one more progress event completes.
+int wait_until(gs_stepper* s, int64_t target, double timeout_s) {
+  const int64_t R = (int64_t)s->prog.size();
+  const bool all = target >= s->prog_rec;
+  auto last = std::chrono::steady_clock::now();
+  for (;;) {
+    while (s->prog_done < s->prog_rec) {
+      const hipError_t q = hipEventQuery(s->prog[s->prog_done % R]);
+      if (q == hipErrorNotReady) break;
+      if (q != hipSuccess) {
+        char m[256];
+        snprintf(m, sizeof(m), "stream error: %s", hipGetErrorString(q));
+        gs_set_error(m);
+        return -1;
+      }
+      ++s->prog_done;
+      last = std::chrono::steady_clock::now();
+    }
+    bool done = s->prog_done >= target;
+    if (all) {
+      hipError_t a = hipStreamQuery(s->s_comp);
+      if (a == hipSuccess) a = hipStreamQuery(s->s_rem);
+      if (a == hipSuccess) a = hipStreamQuery(s->s_rem2);
+      const hipError_t b = hipStreamQuery(s->s_comm);
+      if ((a != hipSuccess && a != hipErrorNotReady) || (b != hipSuccess && b != hipErrorNotReady)) {
+        char m[256];
+        snprintf(m, sizeof(m), "stream error: %s / %s", hipGetErrorString(a), hipGetErrorString(b));
+        gs_set_error(m);
+        return -1;
+      }
+      done = a == hipSuccess && b == hipSuccess;
+    }
+    if (done) {
+      if (all) s->prog_done = s->prog_rec;
+      return all ? gate_check(s) : 0;
+    }
+    if (s->have_comm && gs_stepper_comm_check(s)) return -1;
+    const double el =
+        std::chrono::duration<double>(std::chrono::steady_clock::now() - last).count();
+    if (timeout_s > 0 && el > timeout_s) {
+      char m[256];
+      snprintf(m, sizeof(m),
+               "step timeout: no step completed for %.1f s (rank %d, step %lld of %lld "
+               "enqueued); communicator aborted",
+               el, s->cfg.rank, (long long)s->prog_done, (long long)s->prog_rec);
+      if (s->have_comm) {
+        (void)ncclCommAbort(s->comm);
+        s->have_comm = false;
+      }
+      gs_set_error(m);
+      return -1;
+    }
+    std::this_thread::sleep_for(std::chrono::microseconds(200));
+  }
+}
+
+// One progress event per enqueued step / graph period. At most prog.size() are outstanding:
+// past that the host waits (bounded by step_timeout_s) for the oldest before enqueuing more.
+int note_progress(gs_stepper* s) {
+  const int64_t R = (int64_t)s->prog.size();
+  if (R == 0) return 0;
+  if (s->prog_rec - s->prog_done >= R && wait_until(s, s->prog_rec - R + 1, s->step_timeout_s))
+    return -1;
+  GS_HIP(hipEventRecord(s->prog[s->prog_rec % R], s->s_comp));
+  ++s->prog_rec;
   return 0;
 }
 
@@ -721,6 +926,10 @@ int gs_stepper_create(const gs_config* cfg, gs_stepper** out) {
   s->timed = getenv("GRAVSIM_PHASE_TIMING") != nullptr;
   s->emulate = getenv("GRAVSIM_EMULATE_RANK") != nullptr && cfg->nranks > 1;
   if (const char* ov = getenv("GRAVSIM_SYM_OVERLAP")) s->sym_overlap = atoi(ov);
+  if (const char* v = getenv("GRAVSIM_EMU_COMM_GBPS")) s->emu_gbps = atof(v);
+  if (const char* v = getenv("GRAVSIM_EMU_COMM_US")) s->emu_lat_us = atof(v);
+  if (const char* v = getenv("GRAVSIM_EMU_COMM_WGS")) s->emu_wgs = atoi(v);
+  if (const char* v = getenv("GRAVSIM_GATE_TIMEOUT_S")) s->gate_timeout_s = atof(v);
   const int64_t own_first = s->L.local_begin / s->L.chunk;
   const int64_t own_last = (s->L.local_begin + s->L.n_local) / s->L.chunk;
   s->own_c0 = (int)(own_first < s->L.n_chunks ? own_first : s->L.n_chunks);
@@ -737,6 +946,12 @@ int gs_stepper_create(const gs_config* cfg, gs_stepper** out) {
   } while (0)
   FAIL_CLEAN(hipSetDevice(cfg->device));
   FAIL_CLEAN(hipDeviceGetAttribute(&s->cus, hipDeviceAttributeMultiprocessorCount, cfg->device));
+  {
+    int khz = 0;
+    if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, cfg->device) == hipSuccess &&
+        khz > 0)
+      s->clk_khz = khz;
+  }
   for (int fm = 0; fm < 3; ++fm)
     s->occ[fm] = s->esz == 4 ? gs::split_occupancy<float>(s->L.kernel, s->L.ipl, fm)
                              : gs::split_occupancy<double>(s->L.kernel, s->L.ipl, fm);
@@ -758,6 +973,8 @@ int gs_stepper_create(const gs_config* cfg, gs_stepper** out) {
   FAIL_CLEAN(hipEventCreate(&s->ev_t0));
   FAIL_CLEAN(hipEventCreate(&s->ev_local));
   FAIL_CLEAN(hipEventCreate(&s->ev_end));
+  s->prog.assign(64, nullptr);
+  for (auto& e : s->prog) FAIL_CLEAN(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   const size_t rb = row_bytes(s);
   FAIL_CLEAN(hipMalloc(&s->X[0], (size_t)s->L.n_pad * rb));
   FAIL_CLEAN(hipMalloc(&s->X[1], (size_t)s->L.n_pad * rb));
@@ -776,6 +993,15 @@ int gs_stepper_create(const gs_config* cfg, gs_stepper** out) {
   }
   FAIL_CLEAN(hipMalloc(&s->mass_dev, (size_t)s->L.n_pad * sizeof(double)));
   FAIL_CLEAN(hipMalloc(&s->nonfinite, sizeof(unsigned long long)));
+  FAIL_CLEAN(hipMalloc(&s->gate_buf, 4 * sizeof(unsigned)));
+  FAIL_CLEAN(hipMemsetAsync(s->gate_buf, 0, 4 * sizeof(unsigned), s->s_comp));
+  if (s->emulate && s->emu_gbps > 0.0) {
+    // Scratch destination of the modeled collectives (the larger of the two per step).
+    s->emu_cap = gather_bytes(s);
+    if (s->L.mode == GS_MODE_SYM && exchange_bytes(s) > s->emu_cap) s->emu_cap = exchange_bytes(s);
+    s->emu_cap &= ~(size_t)15;
+    FAIL_CLEAN(hipMalloc(&s->emu_buf, s->emu_cap ? s->emu_cap : 16));
+  }
   // Zero on the compute stream itself: it is non-blocking, so a legacy-stream hipMemset
   // would NOT be ordered before later work on it (it could land after the IC kernel).
   FAIL_CLEAN(hipMemsetAsync(s->X[0], 0, (size_t)s->L.n_pad * rb, s->s_comp));
@@ -798,7 +1024,8 @@ int gs_stepper_destroy(gs_stepper* s) {
   if (s->sym_R == s->sym_S) s->sym_R = nullptr;
   for (void* p : {s->X[0], s->X[1], s->vel, s->partial, s->acc, (void*)s->mass_dev,
                   (void*)s->nonfinite, (void*)s->sym_Pi, (void*)s->sym_Pj, (void*)s->sym_Pd,
-                  (void*)s->sym_S, (void*)s->sym_R, (void*)s->sym_Ti})
+                  (void*)s->sym_S, (void*)s->sym_R, (void*)s->sym_Ti, (void*)s->gate_buf,
+                  s->emu_buf})
     if (p) (void)hipFree(p);
   for (hipEvent_t e : {s->ev_ready, s->ev_gathered, s->ev_t0, s->ev_local, s->ev_end,
                        s->ev_remote, s->ev_fork, s->ev_rem2, s->ev_sym})
@@ -809,6 +1036,11 @@ int gs_stepper_destroy(gs_stepper* s) {
   if (s->s_rem2) (void)hipStreamDestroy(s->s_rem2);
   for (hipEvent_t e : s->ev_recv)
     if (e) (void)hipEventDestroy(e);
+  for (hipEvent_t e : s->prog)
+    if (e) (void)hipEventDestroy(e);
+  for (auto& p : s->pev)
+    for (hipEvent_t e : {p.t0, p.end, p.g0, p.g1, p.w0, p.w1, p.x0, p.x1, p.j0, p.j1})
+      if (e) (void)hipEventDestroy(e);
   delete s;
   return 0;
 }
@@ -862,33 +1094,54 @@ int gs_stepper_step(gs_stepper* s, int32_t nsteps) {
     gs_set_error("step: nranks > 1 but no RCCL communicator (call gs_stepper_comm_init)");
     return -1;
   }
-  if (s->emulate) {
-    // Timing emulation of one rank of a P-rank run: the multi-rank launches with the
-    // all-gather treated as done (remote slices hold stale data; numbers are not physics).
-    s->virt = true;
-    for (int32_t i = 0; i < nsteps; ++i)
-      if (enqueue_step_any(s, false, true)) return -1;
-    return 0;
-  }
-  // hipGraph replay only for the single-rank schedule (nothing to gather); RCCL capture is
-  // opt-in through use_graph >= 2.
-  const bool graph_ok = s->cfg.use_graph >= (s->have_comm ? 2 : 1) && !s->timed;
+  // GRAVSIM_EMULATE_RANK runs one rank's launch shapes of a P-rank run on one GPU with the
+  // collectives modeled (GRAVSIM_EMU_COMM_GBPS > 0) or free; remote slices hold stale data,
+  // so the numbers are timings, not physics.
+  // hipGraph replay of a two-step ping-pong period. Multi-rank (RCCL or emulated) steps are
+  // captured collectives included when use_graph >= 2 (the default for multi-rank runs);
+  // a capture the runtime refuses falls back to eager steps.
+  const bool graph_ok =
+      s->cfg.use_graph >= (xcomm(s) ? 2 : 1) && !s->timed && !(xcomm(s) && s->graph_failed);
   int32_t left = nsteps;
   while (left > 0) {
-    const bool period_start = (s->k & 1) == 0 && (s->have_comm ? !s->full[0] : true);
-    if (graph_ok && left >= 2 && period_start) {
-      if (!s->graph && build_graph(s)) return -1;
+    const bool period_start = (s->k & 1) == 0 && (xcomm(s) ? !s->full[0] : true);
+    if (graph_ok && left >= 2 && period_start && !s->graph_failed) {
+      if (!s->graph && build_graph(s)) {
+        if (!xcomm(s)) return -1;
+        s->graph_failed = true;  // eager from here on (the error text is kept for inspection)
+        continue;
+      }
       GS_HIP(hipGraphLaunch(s->graph, s->s_comp));
       s->k += 2;
       // After one period: X[1] was gathered in the second step, X[0] holds only the own slice.
-      s->full[0] = !s->have_comm;
+      s->full[0] = !xcomm(s);
       s->full[1] = true;
       left -= 2;
+      if (note_progress(s)) return -1;
       continue;
     }
     if (enqueue_step_any(s, false)) return -1;
     left -= 1;
+    if (note_progress(s)) return -1;
   }
+  return 0;
+}
+
+int gs_stepper_set_timing(gs_stepper* s, int32_t on) {
+  s->timed = on != 0;
+  s->pev_used = 0;
+  return 0;
+}
+
+int gs_stepper_set_overlap(gs_stepper* s, int32_t mode) {
+  if (mode < 0 || mode > 3) { gs_set_error("set_overlap: mode must be 0..3"); return -1; }
+  s->sym_overlap = mode;
+  if (s->graph) { (void)hipGraphExecDestroy(s->graph); s->graph = nullptr; }
+  return 0;
+}
+
+int gs_stepper_set_timeout(gs_stepper* s, double step_timeout_s) {
+  s->step_timeout_s = step_timeout_s > 0 ? step_timeout_s : 0.0;
   return 0;
 }
 
@@ -897,41 +1150,50 @@ int gs_stepper_sync(gs_stepper* s) {
   GS_HIP(hipStreamSynchronize(s->s_rem));
   GS_HIP(hipStreamSynchronize(s->s_rem2));
   GS_HIP(hipStreamSynchronize(s->s_comp));
-  return 0;
+  s->prog_done = s->prog_rec;
+  return gate_check(s);
 }
 
-// Bounded wait for both streams, polling RCCL async errors. A hang (a dead peer, a stuck
-// collective) or an RCCL error aborts the communicator and returns -1 instead of blocking
-// forever (the reference's MPI_ERRORS_ARE_FATAL / silent CUDA errors: SURVEY.md §5).
+// Bounded wait for every stream, polling RCCL async errors. The deadline bounds PROGRESS: it
+// restarts whenever one more enqueued step (or graph period) completes, so a long healthy
+// run never trips it while a hang (a dead peer, a stuck collective) or an RCCL error aborts
+// the communicator and returns -1 instead of blocking forever (the reference's
+// MPI_ERRORS_ARE_FATAL / silent CUDA errors: SURVEY.md §5).
 int gs_stepper_wait(gs_stepper* s, double timeout_s) {
-  const auto t0 = std::chrono::steady_clock::now();
-  for (;;) {
-    hipError_t a = hipStreamQuery(s->s_comp);
-    if (a == hipSuccess) a = hipStreamQuery(s->s_rem);
-    if (a == hipSuccess) a = hipStreamQuery(s->s_rem2);
-    const hipError_t b = hipStreamQuery(s->s_comm);
-    if (a == hipSuccess && b == hipSuccess) return 0;
-    if ((a != hipSuccess && a != hipErrorNotReady) || (b != hipSuccess && b != hipErrorNotReady)) {
-      char m[256];
-      snprintf(m, sizeof(m), "stream error: %s / %s", hipGetErrorString(a), hipGetErrorString(b));
-      gs_set_error(m);
-      return -1;
-    }
-    if (s->have_comm && gs_stepper_comm_check(s)) return -1;
-    const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-    if (timeout_s > 0 && el > timeout_s) {
-      char m[256];
-      snprintf(m, sizeof(m), "step timeout after %.1f s (rank %d); communicator aborted", el,
-               s->cfg.rank);
-      if (s->have_comm) {
-        (void)ncclCommAbort(s->comm);
-        s->have_comm = false;
-      }
-      gs_set_error(m);
-      return -1;
-    }
-    std::this_thread::sleep_for(std::chrono::microseconds(200));
+  return wait_until(s, s->prog_rec, timeout_s);
+}
+
+// Phase timing of the eager steps enqueued since gs_stepper_set_timing(s, 1) / the previous
+// call (at most 256), averaged per step. out[0] steps, [1] total ms, [2] all-gather ms and
+// [3] group-sum exchange ms (spans on the comm stream), [4] exposed gather ms and [5]
+// exposed exchange ms (compute-stream stalls on them), [6] longest in-kernel gate wait ms,
+// [7] gate timeouts. Multi-rank exposed comm = [4] + [5] (+ [6] with the gated schedule).
+int gs_stepper_phase_stats(gs_stepper* s, double* out8) {
+  for (int i = 0; i < 8; ++i) out8[i] = 0.0;
+  for (hipStream_t st : {s->s_comm, s->s_rem, s->s_rem2, s->s_comp})
+    GS_HIP(hipStreamSynchronize(st));
+  s->prog_done = s->prog_rec;
+  const int n = s->pev_used;
+  for (int i = 0; i < n; ++i) {
+    const gs_stepper::PhaseEv& p = s->pev[i];
+    float v = 0.f;
+    GS_HIP(hipEventElapsedTime(&v, p.t0, p.end));
+    out8[1] += v;
+    if (p.g) { GS_HIP(hipEventElapsedTime(&v, p.g0, p.g1)); out8[2] += v; }
+    if (p.x) { GS_HIP(hipEventElapsedTime(&v, p.x0, p.x1)); out8[3] += v; }
+    if (p.w) { GS_HIP(hipEventElapsedTime(&v, p.w0, p.w1)); out8[4] += v; }
+    if (p.j) { GS_HIP(hipEventElapsedTime(&v, p.j0, p.j1)); out8[5] += v; }
   }
+  if (n > 0)
+    for (int i = 1; i < 6; ++i) out8[i] /= n;
+  out8[0] = n;
+  unsigned d[2] = {0, 0};
+  GS_HIP(hipMemcpy(d, s->gate_buf + 2, sizeof(d), hipMemcpyDeviceToHost));
+  out8[6] = d[1] / s->clk_khz;
+  out8[7] = d[0];
+  GS_HIP(hipMemset(s->gate_buf + 2, 0, sizeof(d)));
+  s->pev_used = 0;
+  return 0;
 }
 
 int gs_stepper_accel(gs_stepper* s, double* acc4) {
@@ -974,11 +1236,17 @@ int64_t gs_stepper_steps_done(gs_stepper* s) { return s->k; }
 int gs_stepper_phase_ms(gs_stepper* s, float* local_ms, float* comm_ms, float* total_ms) {
   if (!s->timed) { gs_set_error("phase timing disabled (set GRAVSIM_PHASE_TIMING=1)"); return -1; }
   GS_HIP(hipEventSynchronize(s->ev_end));
-  float a = 0, b = 0;
+  float a = 0, b = 0, c = 0;
   GS_HIP(hipEventElapsedTime(&a, s->ev_t0, s->ev_local));
   GS_HIP(hipEventElapsedTime(&b, s->ev_t0, s->ev_end));
+  if (s->pev_used > 0) {  // the last step's collectives (all-gather + exchange spans)
+    const gs_stepper::PhaseEv& p = s->pev[s->pev_used - 1];
+    float v = 0.f;
+    if (p.g && hipEventElapsedTime(&v, p.g0, p.g1) == hipSuccess) c += v;
+    if (p.x && hipEventElapsedTime(&v, p.x0, p.x1) == hipSuccess) c += v;
+  }
   if (local_ms) *local_ms = a;
-  if (comm_ms) *comm_ms = 0.f;
+  if (comm_ms) *comm_ms = c;
   if (total_ms) *total_ms = b;
   return 0;
 }

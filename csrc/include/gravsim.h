@@ -131,7 +131,8 @@ int gs_stepper_get_state(gs_stepper* s, double* pos, double* vel, double* mass);
 // Enqueue n steps (asynchronous w.r.t. the host).
 int gs_stepper_step(gs_stepper* s, int32_t nsteps);
 int gs_stepper_sync(gs_stepper* s);
-// Bounded wait (timeout_s <= 0: unbounded) polling RCCL async errors; aborts on timeout.
+// Bounded wait (timeout_s <= 0: unbounded) polling RCCL async errors; aborts the communicator
+// when no enqueued step completes for timeout_s (the deadline bounds progress, not the run).
 int gs_stepper_wait(gs_stepper* s, double timeout_s);
 // Accelerations (+potential) of this rank's bodies for the current positions: acc4 = n_local*4.
 int gs_stepper_accel(gs_stepper* s, double* acc4);
@@ -141,8 +142,21 @@ int gs_stepper_accel_step_path(gs_stepper* s, double* acc4);
 // Non-finite guard: returns number of non-finite position/velocity components on this rank.
 int64_t gs_stepper_count_nonfinite(gs_stepper* s);
 int64_t gs_stepper_steps_done(gs_stepper* s);
-// Per-step phase timing of the last step (ms): local tile, gather wait, remote+integrate.
+// Per-step phase timing of the last step (ms): up to the local/force phase, the step's
+// collectives (all-gather + group-sum exchange spans on the comm stream), and the whole step.
 int gs_stepper_phase_ms(gs_stepper* s, float* local_ms, float* comm_ms, float* total_ms);
+// Eager steps record per-step phase events while on (hipGraph replay is off meanwhile).
+int gs_stepper_set_timing(gs_stepper* s, int32_t on);
+// Averages over the timed steps since the last call: out[0] steps, [1] step ms, [2] gather
+// ms, [3] exchange ms, [4] exposed gather ms, [5] exposed exchange ms, [6] longest in-kernel
+// gate wait ms, [7] gate timeouts.
+int gs_stepper_phase_stats(gs_stepper* s, double* out8);
+// Sym schedule work beside the all-gather: 0 wait then one launch, 1 diagonal units first,
+// 2 local units + remote units on a second stream, 3 one local-first launch with the remote
+// units gated in-kernel on the gather (GRAVSIM_SYM_OVERLAP sets the initial value).
+int gs_stepper_set_overlap(gs_stepper* s, int32_t mode);
+// Bound on the host waiting for the oldest of the enqueued steps when it runs far ahead.
+int gs_stepper_set_timeout(gs_stepper* s, double step_timeout_s);
 // Resolved force path: *exact = 1 for the hard-cutoff select, *eps2 = r^2 offset in use.
 int gs_stepper_force_mode(gs_stepper* s, int32_t* exact, double* eps2);
 void* gs_stepper_compute_stream(gs_stepper* s);

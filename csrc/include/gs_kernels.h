@@ -73,11 +73,22 @@ struct SymArgs {
   int32_t units;       // which units a force launch covers: 0 all, 1 diagonal chunks only
                        // (need only the own rows), 2 shell segments only, 4 the shell
                        // segments with a j-chunk outside the own rows, 5 every other unit
-                       // (diagonal + rank-local shell: no gathered positions needed)
+                       // (diagonal + rank-local shell: no gathered positions needed),
+                       // 6 all, ordered local-first, the others gated on `gate`
   double dt, eps2, cut2;
+  // Gather gate (units 6): remote units wait until *gate != 0 (set on the comm stream right
+  // after the all-gather; finalize clears it). gate_diag[0]: timeout flag, [1]: longest wait
+  // in wall-clock ticks. A wait longer than gate_ticks gives up and raises the flag.
+  unsigned* gate;
+  unsigned* gate_diag;
+  uint64_t gate_ticks;
 };
 
 hipError_t launch_force_sym(const SymArgs& a, hipStream_t s);
+// Modeled collective (per-rank emulation) and the gather gate (comm_model.hip).
+hipError_t launch_comm_model(const void* src, void* dst, size_t bytes, uint64_t ticks, int wgs,
+                             hipStream_t s);
+hipError_t launch_gate_set(unsigned* gate, hipStream_t s);
 hipError_t launch_sym_group_reduce(const SymArgs& a, hipStream_t s);  // accumulates into Sbuf
 hipError_t launch_sym_row_reduce(const SymArgs& a, hipStream_t s);    // the band's rows -> Ti
 hipError_t launch_sym_finalize(const SymArgs& a, hipStream_t s);

@@ -45,8 +45,14 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--ipl", type=int, default=d.ipl, choices=[0, 1, 2, 4, 8])
     p.add_argument("--chunk", type=int, default=d.chunk)
     p.add_argument("--no-graph", dest="graph", action="store_false")
-    p.add_argument("--graph-comm", action="store_true",
-                   help="capture the multi-rank step, RCCL all-gather included, in a hipGraph")
+    p.add_argument("--graph-comm", dest="graph_comm", action="store_true",
+                   help="replay multi-rank steps from a hipGraph that captures them, RCCL "
+                        "collectives included (default: eager multi-rank steps)")
+    p.add_argument("--no-graph-comm", dest="graph_comm", action="store_false",
+                   help=argparse.SUPPRESS)
+    p.add_argument("--step-timeout", dest="step_timeout_s", type=float, default=d.step_timeout_s,
+                   help="multi-rank hang detection: abort the RCCL communicator when no step "
+                        "completes for this many seconds (0 = wait forever)")
     p.add_argument("--strategy", choices=["allgather", "ring"], default=d.strategy,
                    help="multi-rank GPU exchange: one all-gather overlapped with the local "
                         "chunks, or a ring of P-1 neighbour send/recv steps computed on arrival")
@@ -90,7 +96,7 @@ def config_from_args(a: argparse.Namespace) -> SimConfig:
                      seed=a.seed, G=a.G, cutoff=a.cutoff, softening=a.softening,
                      cutoff_mode=a.cutoff_mode, integrator=a.integrator, kernel=a.kernel,
                      mode=a.mode, ipl=a.ipl, chunk=a.chunk, graph=a.graph, graph_comm=a.graph_comm,
-                     strategy=a.strategy,
+                     strategy=a.strategy, step_timeout_s=a.step_timeout_s,
                      threads=a.threads,
                      log_dir=a.log_dir, log_format=a.log_format, progress_every=a.progress_every,
                      print_positions=a.print_positions, dump_path=a.dump_path,

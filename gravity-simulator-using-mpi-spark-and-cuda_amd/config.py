@@ -41,11 +41,14 @@ class SimConfig:
     chunk: int = 0                # canonical j-chunk (0 = auto from n)
     split_groups: int = 0
     graph: bool = True            # hipGraph replay of the step loop (single rank)
-    graph_comm: bool = False      # also capture the multi-rank step (RCCL collective included)
+    graph_comm: bool = False      # also capture the multi-rank step (RCCL collectives included;
+                                  # eager fallback if the runtime refuses the capture). Off by
+                                  # default: docs/DESIGN.md "hipGraph and RCCL".
     comm: str = "auto"            # rccl (GPU) | gloo (CPU) | none
     strategy: str = "allgather"   # multi-rank exchange: allgather | ring (pipelined send/recv)
     threads: int = 0              # CPU engine OpenMP threads (0 = default)
-    step_timeout_s: float = 600.0 # multi-rank hang detection: abort RCCL after this wait
+    step_timeout_s: float = 600.0 # multi-rank hang detection: abort RCCL when no step completes
+                                  # for this long
     # observability / IO
     log_dir: Optional[str] = None     # directory for the text log (None = no file)
     log_format: str = "mpi"           # mpi | spark | cuda | none
@@ -93,6 +96,8 @@ class SimConfig:
             raise ValueError("cutoff_mode must be auto, exact or fast")
         if self.strategy not in ("allgather", "ring"):
             raise ValueError("strategy must be allgather or ring")
+        if self.step_timeout_s < 0:
+            raise ValueError("step_timeout_s must be >= 0 (0 = unbounded)")
         if self.cutoff < 0 or self.softening < 0:
             raise ValueError("cutoff and softening must be >= 0")
         return self

@@ -65,6 +65,8 @@ class HipEngine:
         L = _native.GsLayout()
         _native.check(self.lib, self.lib.gs_stepper_layout(self._s, ctypes.byref(L)), "layout")
         self.native_layout = L.as_dict()
+        if nranks > 1 and cfg.step_timeout_s:
+            self.lib.gs_stepper_set_timeout(self._s, float(cfg.step_timeout_s))
         self.layout: Layout = make_layout(cfg.n, rank, nranks, L.chunk,
                                           sym=L.mode == _native.MODE_IDS["sym"])
         assert self.layout.n_pad == L.n_pad, "Python layout mirror disagrees with native"
@@ -108,14 +110,37 @@ class HipEngine:
             _native.check(self.lib, self.lib.gs_stepper_step(self._s, int(n)), "step")
 
     def sync(self, timeout_s: float = 0.0) -> None:
-        """Wait for the enqueued steps. With a timeout (or P > 1, default 600 s) the wait
-        polls RCCL async errors and aborts the communicator on a hang."""
+        """Wait for the enqueued steps. With a timeout (or P > 1: cfg.step_timeout_s, default
+        600 s) the wait polls RCCL async errors and aborts the communicator when no step
+        completes for that long (it bounds progress, not the length of the run)."""
         if timeout_s <= 0 and self.nranks > 1:
             timeout_s = float(self.cfg.step_timeout_s or 0)
         if timeout_s > 0:
             _native.check(self.lib, self.lib.gs_stepper_wait(self._s, timeout_s), "wait")
         else:
             _native.check(self.lib, self.lib.gs_stepper_sync(self._s), "sync")
+
+    # -- phase timing / schedule knobs ------------------------------------------------------
+    def set_timing(self, on: bool) -> None:
+        """Eager steps record per-step phase events while on (graph replay pauses)."""
+        _native.check(self.lib, self.lib.gs_stepper_set_timing(self._s, int(bool(on))), "timing")
+
+    def phase_stats(self) -> dict:
+        """Per-step averages over the timed steps since set_timing(True) / the last call.
+        comm_ms: the step's collectives on the comm stream (all-gather + group-sum exchange);
+        exposed_comm_ms: how long the compute stream stalled on them (plus the longest
+        in-kernel gate wait with the gated schedule)."""
+        out = (ctypes.c_double * 8)()
+        _native.check(self.lib, self.lib.gs_stepper_phase_stats(self._s, out), "phase stats")
+        v = list(out)
+        return {"steps": int(v[0]), "step_ms": v[1], "gather_ms": v[2], "exchange_ms": v[3],
+                "exposed_gather_ms": v[4], "exposed_exchange_ms": v[5], "gate_wait_ms": v[6],
+                "gate_timeouts": int(v[7]), "comm_ms": v[2] + v[3],
+                "exposed_comm_ms": v[4] + v[5] + v[6]}
+
+    def set_overlap(self, mode: int) -> None:
+        """Sym-schedule work beside the all-gather (0..3, see gravsim.h)."""
+        _native.check(self.lib, self.lib.gs_stepper_set_overlap(self._s, int(mode)), "overlap")
 
     def state(self) -> BodySet:
         """Full positions (collective for P > 1), own velocity rows, masses."""

@@ -1,0 +1,60 @@
+#!/bin/bash
+# One parameterised GPU recipe (run on the MI355X box through gpurun):
+#   bash scripts/gpu.sh <task> [<task> ...]
+# tasks (each step under its own time limit; the first failure ends the call):
+#   tests[:<pytest -k expr>]  GPU test suite (or a subset), one process, per-test timeout
+#   smoke                     __graft_entry__.smoke()
+#   bench[:<args>]            bench.py (commas in <args> become spaces)
+#   prof[:<args>]             rocprofv3 kernel-trace stats of bench.py -> gpurun_out/prof
+#   rank[:<args>]             bench/rank_shape.py per-rank emulation (commas -> spaces)
+#   rehearsal                 torchrun / self-launch / CLI multi-rank rehearsal on one GPU
+#   configs                   bench/configs.py, every BASELINE config
+#   pmc[:<bench args>]        three rocprofv3 --pmc passes (kernel-trace only) of bench.py
+# Outputs land in gpurun_out/<task>*.log.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+out=gpurun_out
+
+args_of() { local a="${1#*:}"; [ "$a" = "$1" ] && a=""; echo "${a//,/ }"; }
+
+step() {  # $1 = limit (s), $2 = log, rest = command
+  local lim=$1 log=$2; shift 2
+  echo "== $* (limit ${lim}s) -> $log"
+  timeout -k 10 "$lim" "$@" > "$log" 2>&1
+  local rc=$?
+  tail -3 "$log"
+  if [ $rc -ne 0 ]; then echo "!! rc=$rc: $*"; tail -40 "$log"; exit $rc; fi
+}
+
+for task in "$@"; do
+  name="${task%%:*}"
+  a=$(args_of "$task")
+  case "$name" in
+    tests)
+      if [ -n "${task#tests}" ]; then k="${task#tests:}"; else k=""; fi
+      step 1500 $out/pytest_gpu${k:+_sel}.log python -u -m pytest tests -x -v -m gpu \
+        --timeout 300 --timeout-method thread ${k:+-k "$k"} ;;
+    smoke) step 300 $out/smoke.log python __graft_entry__.py smoke ;;
+    bench) step 600 $out/bench_$(date +%s).log python bench.py $a ;;
+    prof)
+      step 600 $out/prof.log rocprofv3 --kernel-trace --stats -d $out/prof -o bench \
+        --output-format csv -- python bench.py --steps 3 --warmup 1 $a
+      head -6 $out/prof/bench_kernel_stats.csv ;;
+    rank) step 1200 $out/rank_$(date +%s).log python bench/rank_shape.py $a ;;
+    rehearsal) step 900 $out/rehearsal.log bash scripts/gpu_torchrun.sh ;;
+    configs) step 1200 $out/configs.log python bench/configs.py --md $out/baseline_configs.md ;;
+    pmc)
+      for pass in "valu SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS GRBM_GUI_ACTIVE" \
+                  "cycles SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAIT_INST_ANY" \
+                  "lds SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_FMA_F32"; do
+        set -- $pass; tag=$1; shift
+        step 300 $out/pmc_$tag.log rocprofv3 --kernel-trace --pmc "$@" -d $out/pmc_$tag -o pmc \
+          --output-format csv -- python bench.py --steps 2 --warmup 1 --check-samples 0 \
+          --phase-steps 0 $a
+      done
+      python scripts/pmc_summary.py > $out/pmc_summary.txt 2>&1; cat $out/pmc_summary.txt ;;
+    *) echo "unknown task $task"; exit 2 ;;
+  esac
+done

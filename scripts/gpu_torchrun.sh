@@ -10,6 +10,10 @@ mkdir -p gpurun_out/tr
 export TMPDIR=/tmp GRAVSIM_RCCL_RANK_HOSTS=1
 out=gpurun_out/tr
 run="python -m torch.distributed.run --nnodes=1 --master-addr 127.0.0.1"
+# bench.py without a launcher starts its own ranks (parallel/launch.py)
+timeout -k 10 240 python bench.py --gpus 2 --steps 3 --warmup 1 --n 65536 > $out/bench2_self.log 2>&1 \
+  || { tail -30 $out/bench2_self.log; exit 1; }
+grep '^{' $out/bench2_self.log
 timeout -k 10 240 $run --nproc-per-node 2 --master-port 29611 bench.py --gpus 2 --steps 3 \
   --warmup 1 --num-bodies 65536 > $out/bench2.log 2>&1 || { tail -30 $out/bench2.log; exit 1; }
 grep '^{' $out/bench2.log

@@ -1,0 +1,88 @@
+"""Comm/compute split and overlap of the multi-rank sym step, measured on one GPU.
+
+Per-rank emulation (GRAVSIM_EMULATE_RANK) runs rank r's exact launch shapes of a P-rank run;
+with GRAVSIM_EMU_COMM_GBPS the all-gather and the group-sum exchange become modeled
+collectives (comm_model.hip) of their exact byte counts on the comm stream, so the phase
+events see what an xGMI collective would cost. The reference times its whole loop, the
+MPI_Allgatherv included (mpi.c:189,227-247). Overlap modes (gravsim.h, set_overlap):
+0 wait for the gather then one launch, 1 diagonal units first, 2 local units + remote units
+on two streams, 3 one local-first launch with the remote units gated in-kernel.
+"""
+import numpy as np
+import pytest
+
+from gravsim.config import SimConfig
+
+pytestmark = pytest.mark.gpu
+
+
+def _emu(monkeypatch, n, P, rank, gbps, overlap):
+    from gravsim.runtime.engines import HipEngine
+
+    monkeypatch.setenv("GRAVSIM_EMULATE_RANK", "1")
+    monkeypatch.setenv("GRAVSIM_EMU_COMM_GBPS", str(gbps))
+    monkeypatch.setenv("GRAVSIM_EMU_COMM_US", "15")
+    e = HipEngine(SimConfig(n=n, dtype="fp32", device="gpu", mode="sym"), rank, P)
+    e.set_overlap(overlap)
+    return e
+
+
+def test_overlap_modes_same_bits(hip, monkeypatch):
+    """Every overlap mode computes every unit exactly once into the same slots: the emulated
+    rank's state after 4 steps is bitwise identical for modes 0..3 (a unit missed by the
+    local-first order of mode 3 would leave uninitialised partials behind)."""
+    res = []
+    for ov in (0, 1, 2, 3):
+        e = _emu(monkeypatch, 262144, 8, 5, 64, ov)
+        e.init_ics("solar+random", 2)
+        e.step(4)
+        e.sync()
+        b = e.state()
+        own = e.layout.real_local
+        res.append((b.pos[own.start:own.stop].copy(), b.vel[own.start:own.stop].copy()))
+        e.close()
+    for pos, vel in res[1:]:
+        assert np.array_equal(pos, res[0][0])
+        assert np.array_equal(vel, res[0][1])
+
+
+def test_phase_split_reports_modeled_comm(hip, monkeypatch):
+    """Phase events: the modeled gather (7/8 of 262144 x 16 B = 3.67 MB at 8 GB/s + 15 us =
+    474 us) and exchange (2.75 MB: 359 us) show up as comm time; with overlap 0 the compute
+    stream stalls for the whole gather, with overlap 3 it never waits on it (the gated units
+    absorb what is left of it) and the step is shorter."""
+    out = {}
+    for ov in (0, 3):
+        e = _emu(monkeypatch, 262144, 8, 7, 8, ov)
+        e.init_ics("solar+random", 2)
+        e.step(2)
+        e.sync()
+        e.set_timing(True)
+        e.step(4)
+        out[ov] = e.phase_stats()
+        e.set_timing(False)
+        e.close()
+    p0, p3 = out[0], out[3]
+    for p in (p0, p3):
+        assert p["steps"] == 4
+        assert p["gather_ms"] > 0.9 * 0.474, p
+        assert p["exchange_ms"] > 0.9 * 0.359, p
+        assert p["gate_timeouts"] == 0
+    assert p0["exposed_gather_ms"] > 0.8 * p0["gather_ms"], p0
+    assert p3["exposed_gather_ms"] == 0.0, p3
+    assert p3["gate_wait_ms"] < p3["gather_ms"], p3
+    assert p3["step_ms"] < p0["step_ms"], (p0, p3)
+
+
+def test_gate_times_out_instead_of_hanging(hip, monkeypatch):
+    """A gather that never publishes (modeled at 0.001 GB/s: ~3.7 s) against a 0.2 s gate
+    budget: the gated units give up, the step completes, and sync raises."""
+    monkeypatch.setenv("GRAVSIM_GATE_TIMEOUT_S", "0.2")
+    e = _emu(monkeypatch, 65536, 8, 3, 0.001, 3)
+    try:
+        e.init_ics("solar+random", 2)
+        e.step(2)
+        with pytest.raises(RuntimeError, match="gate timed out"):
+            e.sync()
+    finally:
+        e.close()

@@ -1,0 +1,82 @@
+"""The sym schedule at the size the headline bench runs (N = 1,048,576 fp32), and its
+multi-rank machinery at that geometry.
+
+The reference's own largest run is N = 50,000 (cuda.cu:121); the bench runs 1M, where the
+schedule has NC = 512 chunk rows, one 6.4 GB band of partial slots, and (16M / 8 ranks)
+several bands per rank. Oracles: an fp64 row sum of the native CPU engine for sampled bodies
+(the intended physics, not reference output), and bitwise equality across
+band counts and virtual-rank counts (the canonical decomposition fixes every sum's order).
+"""
+import numpy as np
+import pytest
+
+from gravsim.config import SimConfig
+
+pytestmark = pytest.mark.gpu
+
+N1M = 1 << 20
+
+
+def _cpu_rows(pos, mass, rows, cutoff=1e-10):
+    """fp64 accelerations of global bodies `rows` (contiguous) against all bodies."""
+    from gravsim.config import G_SI
+    from gravsim.ops import _native
+
+    n = len(mass)
+    X = np.zeros((n, 4))
+    X[:, :3] = pos
+    X[:, 3] = G_SI * mass
+    lib = _native.cpu_lib()
+    out = np.zeros((rows.stop - rows.start, 4))
+    _native.check(lib, lib.gs_cpu_accel_f64(_native.dptr(X), n, rows.start, rows.stop, 2048,
+                                            cutoff ** 2, 0.0, _native.dptr(out)), "cpu accel")
+    return out[:, :3]
+
+
+def test_sym_1m_step_path_accel_sampled(hip):
+    """The step's own force path at N = 1M (device ICs, the bench's data) against fp64 row
+    sums for 4 x 64 sampled bodies, including the Sun (row 0)."""
+    from gravsim.runtime.engines import HipEngine
+
+    e = HipEngine(SimConfig(n=N1M, dtype="fp32", device="gpu"))
+    try:
+        assert e.native_layout["mode"] == 3
+        e.init_ics("solar+random", 20250307)
+        a = e.accel(step_path=True)
+        st = e.state()
+    finally:
+        e.close()
+    errs = []
+    for s0 in (0, 262_144 + 17, 700_001, N1M - 64):
+        rows = slice(s0, s0 + 64)
+        ref = _cpu_rows(st.pos, st.mass, rows)
+        got = a[rows, :3]
+        errs.append(np.linalg.norm(got - ref, axis=1) / np.linalg.norm(ref, axis=1))
+    err = np.concatenate(errs)
+    # fp32 terms summed over 1M bodies in a fixed tree of partials: ~1e-6 typical
+    assert np.median(err) < 2e-5, np.median(err)
+    assert err.max() < 1e-3, err.max()
+
+
+def test_sym_1m_bands_bitwise(hip, monkeypatch):
+    """N = 1M (NC = 512 rows, 12.02 MiB of partial slots per row) in 4 bands of 128 rows (the
+    multi-band path the 16M / 8-rank config runs with 4 bands of 256 rows) and in 6 uneven
+    bands (5 x 100 + 12) gives the same bits as one band, over 2 steps; so does a
+    2-virtual-rank run with 2 bands per rank."""
+    from gravsim.runtime.engines import VirtualGroup
+
+    cfg = SimConfig(n=N1M, dtype="fp32", device="gpu", mode="sym")
+    out = []
+    for P, band_mb in ((1, None), (1, "1540"), (1, "1210"), (2, "1540")):
+        if band_mb:
+            monkeypatch.setenv("GRAVSIM_SYM_BAND_MB", band_mb)
+        else:
+            monkeypatch.delenv("GRAVSIM_SYM_BAND_MB", raising=False)
+        g = VirtualGroup(cfg, P)
+        g.init_ics("solar+random", 3)
+        g.step(2)
+        out.append(g.state())
+        g.close()
+    for o in out[1:]:
+        assert np.array_equal(out[0].pos, o.pos)
+        assert np.array_equal(out[0].vel, o.vel)

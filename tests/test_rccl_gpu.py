@@ -26,10 +26,11 @@ def _port():
 
 
 def _worker(rank, world, port, out_dir, n, steps, strategy="allgather", mode="auto",
-            dtype="fp32"):
+            dtype="fp32", env=None):
     # one "host" per rank (see the module docstring): gravsim.parallel.comm.rccl_rank_hosts
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK="0", GRAVSIM_RCCL_RANK_HOSTS="1")
+    os.environ.update(env or {})
     import gravsim  # noqa: F401
     from gravsim.config import SimConfig
     from gravsim.parallel import comm
@@ -70,24 +71,30 @@ def _worker(rank, world, port, out_dir, n, steps, strategy="allgather", mode="au
         comm.shutdown(dist)
 
 
-@pytest.mark.parametrize("world,strategy,mode,dtype,n", [
-    (2, "allgather", "auto", "fp32", 5000),
-    (2, "ring", "auto", "fp32", 5000),
-    (2, "allgather", "sym", "fp32", 20000),
-    (4, "allgather", "sym", "fp32", 20000),
-    (8, "allgather", "sym", "fp32", 20000),  # the 8-GPU shape: one group per destination
-    (2, "allgather", "sym", "fp64", 20000),
-    (4, "ring", "split", "fp32", 9000),
+OV3 = {"GRAVSIM_SYM_OVERLAP": "3"}  # one local-first launch, remote units gated in-kernel
+
+
+@pytest.mark.parametrize("world,strategy,mode,dtype,n,env", [
+    (2, "allgather", "auto", "fp32", 5000, None),
+    (2, "ring", "auto", "fp32", 5000, None),
+    (2, "allgather", "sym", "fp32", 20000, None),
+    (4, "allgather", "sym", "fp32", 20000, None),
+    (8, "allgather", "sym", "fp32", 20000, None),  # the 8-GPU shape: one group per destination
+    (2, "allgather", "sym", "fp64", 20000, None),
+    (4, "ring", "split", "fp32", 9000, None),
+    (4, "allgather", "sym", "fp32", 40000, OV3),
+    (8, "allgather", "sym", "fp32", 40000, OV3),
+    (2, "allgather", "sym", "fp64", 20000, OV3),
     # (4, "allgather", "sym-graph", ...): capturing the multi-rank step over RCCL's socket
     # transport segfaulted inside a rank (profiles/r1_rccl_multi_rank_tests.log); graph
     # capture of the collectives stays opt-in (--graph-comm) and is covered on one rank below.
 ])
-def test_rccl_multi_rank_match_single_rank(hip, tmp_path, world, strategy, mode, dtype, n):
+def test_rccl_multi_rank_match_single_rank(hip, tmp_path, world, strategy, mode, dtype, n, env):
     """P real RCCL ranks (one process each) give the same bits as one rank without a
     communicator (the canonical decomposition makes the result P-independent)."""
     steps = 5
     mp.start_processes(_worker, args=(world, _port(), str(tmp_path), n, steps, strategy, mode,
-                                      dtype),
+                                      dtype, env),
                        nprocs=world, start_method="spawn", join=True)
     status = open(tmp_path / "status.txt").read()
     assert status == "ok", f"RCCL with {world} ranks: {status[:300]}"
@@ -109,7 +116,8 @@ def test_rccl_multi_rank_match_single_rank(hip, tmp_path, world, strategy, mode,
 
 
 @pytest.mark.parametrize("graph,strategy", [(1, "allgather"), (2, "allgather"), (1, "ring"),
-                                            (2, "ring"), (1, "sym"), (2, "sym")])
+                                            (2, "ring"), (1, "sym"), (2, "sym"), (1, "sym3"),
+                                            (2, "sym3")])
 def test_rccl_one_rank_full_schedule_bitwise(hip, monkeypatch, graph, strategy):
     """A live 1-rank RCCL communicator drives the whole multi-rank step (in-place
     ncclAllGather, concurrent local/remote split, ordered reduce) — eagerly and captured into
@@ -118,10 +126,14 @@ def test_rccl_one_rank_full_schedule_bitwise(hip, monkeypatch, graph, strategy):
     from gravsim.runtime.engines import HipEngine
 
     monkeypatch.setenv("GRAVSIM_FORCE_COMM", "1")
-    # "sym": the Newton-3 schedule (all-gather, then the group-sum exchange through RCCL).
-    mode = "sym" if strategy == "sym" else "auto"
+    # "sym": the Newton-3 schedule (all-gather, then the group-sum exchange through RCCL);
+    # "sym3": the same with the gated local-first launch (graph 2 captures the gate kernels).
+    sym = strategy.startswith("sym")
+    if strategy == "sym3":
+        monkeypatch.setenv("GRAVSIM_SYM_OVERLAP", "3")
+    mode = "sym" if sym else "auto"
     cfg = SimConfig(n=6000, dtype="fp32", device="gpu", chunk=1024, mode=mode,
-                    strategy="allgather" if strategy == "sym" else strategy)
+                    strategy="allgather" if sym else strategy)
     eng = HipEngine(cfg)
     eng.lib.gs_stepper_destroy(eng._s)  # rebuild with the requested graph mode
     import ctypes
@@ -141,6 +153,7 @@ def test_rccl_one_rank_full_schedule_bitwise(hip, monkeypatch, graph, strategy):
     got = eng.state().pos
     eng.close()
     monkeypatch.delenv("GRAVSIM_FORCE_COMM")
+    monkeypatch.delenv("GRAVSIM_SYM_OVERLAP", raising=False)
     ref_eng = HipEngine(cfg)
     ref_eng.init_ics("solar+random", 4)
     ref_eng.step(7)
