@@ -241,7 +241,7 @@ def main(argv=None) -> int:
             out["exposed_comm_ms"] = phase["exposed_comm_ms"]
             out["config"]["phase"] = {k: phase[k] for k in (
                 "steps", "step_ms", "gather_ms", "exchange_ms", "exposed_gather_ms",
-                "exposed_exchange_ms", "gate_wait_ms", "gate_timeouts")}
+                "exposed_exchange_ms", "deferred_units")}
         print(json.dumps(out), flush=True)
     comm.shutdown(dist)
     return 0

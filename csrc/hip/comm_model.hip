@@ -8,8 +8,9 @@
 //   reference times its whole loop, MPI_Allgatherv included (mpi.c:189,227-247); round-1
 //   emulations treated the exchange as free.
 // * gate_set_kernel: publishes "the all-gather into X[cur] is complete" to the force launch
-//   that is already running (GRAVSIM_SYM_OVERLAP=3, nbody_sym.hip): one agent-scope release
-//   store after the collective on the comm stream.
+//   that may already be running (GRAVSIM_SYM_OVERLAP=3, nbody_sym.hip): one agent-scope
+//   release store after the collective on the comm stream. Force units only test it (no
+//   spinning), so the collective never competes with waiting workgroups for CUs.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 

@@ -244,71 +244,58 @@ __device__ __forceinline__ void run_tiles(const SymArgs& a, ISetK<T>& is, TileSe
   }
 }
 
-// Shell segments of row A whose j-chunks all lie in the rank's own rows: a prefix of the
-// row's segments (chunks A+1 .. < a0 + rows, wrapped chunks count as remote). Segment s is
-// local iff A + 1 + (min((s+1) * seg_tiles, h_tiles) - 1) / T < a0 + rows.
-template <typename T>
-__device__ __forceinline__ int local_segs(const SymArgs& a, int A, int seg_tiles) {
-  constexpr int kT = Geo<T>::kTilesPerChunk;
-  const int h_tiles = shell_len(A, a.NC) * kT;
-  const int segs = (h_tiles + seg_tiles - 1) / seg_tiles;
-  const int own_after = a.a0 + a.rows - 1 - A;
-  if (own_after <= 0) return 0;
-  if (h_tiles <= own_after * kT) return segs;
-  return min(segs, own_after * kT / seg_tiles);
-}
-
 // units 6: the grid lists every unit of the band, local ones (diagonal parts, then the
 // rank-local shell segments, row by row) before the remote ones (row by row). Workgroups are
 // dispatched in grid order, so the gathered rows are needed only after ~the local share of
-// the step has been handed out. Returns true for a remote (gated) unit.
-template <typename T>
-__device__ __forceinline__ bool local_first_unit(const SymArgs& a, int b, int* br, int* s) {
-  const int seg_tiles = a.L * Geo<T>::kTilesPerQuantum;
-  for (int r = 0; r < a.band_rows; ++r) {
-    const int n = a.D + local_segs<T>(a, a.a0 + a.band0 + r, seg_tiles);
-    if (b < n) {
-      *br = r;
-      *s = b < a.D ? a.S + b : b - a.D;
-      return false;
-    }
-    b -= n;
+// the step has been handed out. lf = [local prefix (rows + 1) | remote prefix (rows + 1)]
+// per rank row, built on the host (gs_sym_local_segs): the row of unit b is a binary search.
+// Returns true for a remote (gated) unit.
+__device__ __forceinline__ int prefix_row(const int32_t* pre, int rows, int b) {
+  int lo = 0, hi = rows;  // pre[lo] <= b < pre[hi]
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (pre[mid] <= b) lo = mid;
+    else hi = mid;
   }
-  for (int r = 0; r < a.band_rows; ++r) {
-    const int nl = local_segs<T>(a, a.a0 + a.band0 + r, seg_tiles);
-    if (b < a.S - nl) {
-      *br = r;
-      *s = nl + b;
-      return true;
-    }
-    b -= a.S - nl;
-  }
-  *br = a.band_rows;  // unreachable for grid = band_rows * (S + D)
-  *s = 0;
-  return false;
+  return lo;
 }
 
-// Remote unit of a gated launch: wait (one lane, then the workgroup) until the comm stream
-// has published the all-gather. The agent-scope acquire orders the following position reads
-// after the collective's writes. Bounded: past gate_ticks the unit raises gate_diag[0] and
-// proceeds (the host reports the step as failed) instead of hanging the GPU.
-__device__ __forceinline__ void gate_wait(const SymArgs& a) {
+__device__ __forceinline__ bool local_first_unit(const SymArgs& a, int b, int* br, int* s) {
+  const int32_t* lpre = a.lf;
+  const int32_t* rpre = a.lf + a.rows + 1;
+  if (b < lpre[a.rows]) {
+    const int r = prefix_row(lpre, a.rows, b);
+    const int k = b - lpre[r];
+    *br = r;
+    *s = k < a.D ? a.S + k : k - a.D;
+    return false;
+  }
+  b -= lpre[a.rows];
+  const int r = prefix_row(rpre, a.rows, b);
+  const int nl = (lpre[r + 1] - lpre[r]) - a.D;  // the row's local shell segments
+  *br = r;
+  *s = nl + (b - rpre[r]);
+  return true;
+}
+
+// Remote unit of the local-first launch (units 6): go ahead if the comm stream has already
+// published the all-gather (the agent-scope acquire orders the position reads after the
+// collective's writes); otherwise append the unit to the deferred list and leave. No
+// workgroup ever waits on the collective, so RCCL's kernels always find CUs; the deferred
+// units run in a second launch (units 7) queued behind the gather event.
+__device__ __forceinline__ bool gate_open_or_defer(const SymArgs& a) {
+  __shared__ int open_s;
   if (threadIdx.x == 0) {
-    const uint64_t t0 = wall_clock64();
-    uint64_t waited = 0;
-    while (__hip_atomic_load(a.gate, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
-      __builtin_amdgcn_s_sleep(4);
-      waited = wall_clock64() - t0;
-      if (waited > a.gate_ticks) {
-        __hip_atomic_store(a.gate_diag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
+    const bool open = __hip_atomic_load(a.gate, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+    if (!open) {
+      const unsigned k =
+          __hip_atomic_fetch_add(a.defer, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      a.defer[1 + k] = blockIdx.x;
     }
-    if (waited > 0)
-      __hip_atomic_fetch_max(a.gate_diag + 1, (unsigned)min(waited, (uint64_t)0xffffffffu),
-                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    open_s = open ? 1 : 0;
   }
   __syncthreads();
+  return open_s != 0;
 }
 
 // One workgroup per unit (row a, segment s); s == S is the row's diagonal chunk.
@@ -323,7 +310,9 @@ __device__ __forceinline__ void force_sym_body(const SymArgs& a) {
   int br, s;
   bool gated = false;
   if (a.units == 6) {
-    gated = local_first_unit<T>(a, blockIdx.x, &br, &s) && a.gate != nullptr;
+    gated = local_first_unit(a, blockIdx.x, &br, &s) && a.gate != nullptr;
+  } else if (a.units == 7) {  // deferred unit a.defer_index of the units-6 launch
+    local_first_unit(a, (int)a.defer[1 + a.defer_index], &br, &s);
   } else if (a.units == 1) {
     br = blockIdx.x / a.D;
     s = a.S + blockIdx.x % a.D;
@@ -356,7 +345,7 @@ __device__ __forceinline__ void force_sym_body(const SymArgs& a) {
     }
     seq.u = seq.valid(u0);
   }
-  if (gated) gate_wait(a);
+  if (gated && !gate_open_or_defer(a)) return;
   const V4* X4 = static_cast<const V4*>(a.X);
   ISetK<T> is;
   const int64_t i_row0 = (int64_t)A * kSymC + w * G::kTileI;
@@ -391,13 +380,33 @@ __device__ __forceinline__ void force_sym_body(const SymArgs& a) {
   }
 }
 
-template <bool EXACT>
-__global__ __launch_bounds__(Geo<float>::kThreads) GS_SYM_WPE32 void force_sym_kernel_f32(SymArgs a) {
-  force_sym_body<float, EXACT>(a);
+// units 7 runs a separate instantiation (DEFER): a small grid that walks the deferred list
+// with a stride of the grid. The list is usually empty (the gather finished long before the
+// remote units were dispatched), and a grid of one workgroup per possible unit would cost more
+// than the gather it hides. The main kernel is unchanged by it (same registers, no spills).
+template <typename T, bool EXACT, bool DEFER>
+__device__ __forceinline__ void force_sym_entry(SymArgs a) {
+  if constexpr (!DEFER) {
+    force_sym_body<T, EXACT>(a);
+  } else {
+    const unsigned n = a.defer[0];
+    if (blockIdx.x == 0 && threadIdx.x == 0 && n > 0)
+      __hip_atomic_fetch_max(a.defer_max, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (unsigned k = blockIdx.x; k < n; k += gridDim.x) {
+      a.defer_index = (int32_t)k;
+      force_sym_body<T, EXACT>(a);
+      __syncthreads();  // the next unit reuses the LDS tiles
+    }
+  }
 }
-template <bool EXACT>
+
+template <bool EXACT, bool DEFER = false>
+__global__ __launch_bounds__(Geo<float>::kThreads) GS_SYM_WPE32 void force_sym_kernel_f32(SymArgs a) {
+  force_sym_entry<float, EXACT, DEFER>(a);
+}
+template <bool EXACT, bool DEFER = false>
 __global__ __launch_bounds__(Geo<double>::kThreads) GS_SYM_WPE64 void force_sym_kernel_f64(SymArgs a) {
-  force_sym_body<double, EXACT>(a);
+  force_sym_entry<double, EXACT, DEFER>(a);
 }
 
 // S_g(x) for this rank's groups and every body x of a real chunk: rows A of group g in
@@ -482,9 +491,12 @@ template <typename T>
 __global__ __launch_bounds__(256) void sym_finalize_kernel(SymArgs a) {
   using V4 = sym::Vec4<T>;
   const int64_t li = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  // The gated force launch of this step has completed (stream order): re-arm its gate for
-  // the next all-gather into the same buffer (two steps on).
-  if (a.gate && li == 0) __hip_atomic_store(a.gate, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // This step's gated launches have completed (stream order): re-arm the gate for the next
+  // all-gather into the same buffer (two steps on) and empty the deferred list.
+  if (a.gate && li == 0) {
+    __hip_atomic_store(a.gate, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(a.defer, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   if (li >= a.n_local) return;
   const int64_t gi = a.i_begin + li;
   V4* vel = static_cast<V4*>(a.vel);
@@ -528,17 +540,29 @@ __global__ __launch_bounds__(256) void sym_finalize_kernel(SymArgs a) {
 
 template <typename T>
 hipError_t launch_force_sym_t(const SymArgs& a, hipStream_t s) {
-  const int units = a.band_rows * (a.units == 1 ? a.D : (a.units == 2 || a.units == 4) ? a.S
-                                                                                      : a.S + a.D);
-  if (a.units == 6 && a.band_rows != a.rows) return hipErrorInvalidValue;  // one band only
+  int units = a.band_rows * (a.units == 1 ? a.D : (a.units == 2 || a.units == 4) ? a.S
+                                                                                 : a.S + a.D);
+  if (a.units >= 6 && (a.band_rows != a.rows || !a.lf)) return hipErrorInvalidValue;
+  if (a.units == 7) units = a.defer_grid;  // strided walk over the deferred list
   if (units <= 0) return hipSuccess;
   const dim3 grid(units), block(Geo<T>::kThreads);
+  const bool d = a.units == 7;
   if constexpr (sizeof(T) == 8) {
-    if (a.exact) hipLaunchKernelGGL(force_sym_kernel_f64<true>, grid, block, 0, s, a);
-    else hipLaunchKernelGGL(force_sym_kernel_f64<false>, grid, block, 0, s, a);
+    if (a.exact) {
+      if (d) hipLaunchKernelGGL((force_sym_kernel_f64<true, true>), grid, block, 0, s, a);
+      else hipLaunchKernelGGL((force_sym_kernel_f64<true>), grid, block, 0, s, a);
+    } else {
+      if (d) hipLaunchKernelGGL((force_sym_kernel_f64<false, true>), grid, block, 0, s, a);
+      else hipLaunchKernelGGL((force_sym_kernel_f64<false>), grid, block, 0, s, a);
+    }
   } else {
-    if (a.exact) hipLaunchKernelGGL(force_sym_kernel_f32<true>, grid, block, 0, s, a);
-    else hipLaunchKernelGGL(force_sym_kernel_f32<false>, grid, block, 0, s, a);
+    if (a.exact) {
+      if (d) hipLaunchKernelGGL((force_sym_kernel_f32<true, true>), grid, block, 0, s, a);
+      else hipLaunchKernelGGL((force_sym_kernel_f32<true>), grid, block, 0, s, a);
+    } else {
+      if (d) hipLaunchKernelGGL((force_sym_kernel_f32<false, true>), grid, block, 0, s, a);
+      else hipLaunchKernelGGL((force_sym_kernel_f32<false>), grid, block, 0, s, a);
+    }
   }
   return hipGetLastError();
 }

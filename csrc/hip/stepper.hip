@@ -127,11 +127,11 @@ struct gs_stepper {
   void* emu_buf = nullptr;
   size_t emu_cap = 0;
   double clk_khz = 100000.0;  // device wall clock (wall_clock64) rate
-  // Gather gates (sym_overlap 3): [0], [1] gate of X[0] / X[1]; [2] timeout flag; [3] longest
-  // wait of a gated unit in wall-clock ticks (since the last phase_stats call).
+  // Gather gates (sym_overlap 3): [0], [1] gate of X[0] / X[1]; [3] the most units one step
+  // deferred past the gather (since the last phase_stats call). defer: count + unit list.
   unsigned* gate_buf = nullptr;
-  bool gate_used = false;
-  double gate_timeout_s = 10.0;
+  unsigned* defer = nullptr;
+  int32_t* sym_lf = nullptr;  // units-6 order: local / remote unit prefix per rank row
   // Phase timing of eager steps (timed): one event set per step, summed by phase_stats.
   struct PhaseEv {
     hipEvent_t t0, end, g0, g1, w0, w1, x0, x1, j0, j1;
@@ -291,8 +291,11 @@ gs::SymArgs sym_args(gs_stepper* s, int cur) {
   a.band0 = 0;
   a.band_rows = a.rows;
   a.gate = nullptr;
-  a.gate_diag = s->gate_buf + 2;
-  a.gate_ticks = (uint64_t)(s->gate_timeout_s * s->clk_khz * 1e3);
+  a.defer = s->defer;
+  a.defer_max = s->gate_buf + 3;
+  a.lf = s->sym_lf;
+  a.defer_grid = 2 * s->cus;  // resident force workgroups: 2 per CU
+  a.defer_index = 0;
   return a;
 }
 
@@ -329,6 +332,21 @@ int sym_exchange_rccl(gs_stepper* s, bool join = true) {
     GS_MARK(j1, j, s->s_comp);
   }
   return 0;
+}
+
+// Rank-local shell segments of row A: the prefix of the row's S segments (L quanta of 128
+// bodies each, 16 quanta per chunk) whose j-chunks A+1 .. all lie in the rank rows
+// [a0, a0 + rows); wrapped chunks count as remote. Mirrors the units 4/5 test of the force
+// kernel (A + 1 + (u1 - 1) / tiles_per_chunk < a0 + rows) in quanta, independent of the tile.
+int sym_local_segs(int A, int NC, int a0, int rows, int L, int S) {
+  const int h = A < NC / 2 ? NC / 2 : NC / 2 - 1;  // shell length in chunks
+  const int segs = (16 * h + L - 1) / L;
+  const int own_after = a0 + rows - 1 - A;
+  int n;
+  if (own_after <= 0) n = 0;
+  else if (h <= own_after) n = segs;
+  else n = segs < own_after * 16 / L ? segs : own_after * 16 / L;
+  return n < S ? n : S;
 }
 
 int ensure_sym(gs_stepper* s) {
@@ -432,10 +450,7 @@ int gather(gs_stepper* s, int cur, bool gate = false) {
                           s->esz == 4 ? ncclFloat32 : ncclFloat64, s->comm, s->s_comm));
   }
   GS_MARK(g1, g, s->s_comm);
-  if (gate) {
-    GS_HIP(gs::launch_gate_set(s->gate_buf + cur, s->s_comm));
-    s->gate_used = true;
-  }
+  if (gate) GS_HIP(gs::launch_gate_set(s->gate_buf + cur, s->s_comm));
   GS_HIP(hipEventRecord(s->ev_gathered, s->s_comm));
   s->full[cur] = true;
   return 0;
@@ -528,8 +543,14 @@ int sym_force(gs_stepper* s, gs::SymArgs a, bool overlap_gather, bool exchange =
     const bool one_band = a.band_rows == a.rows;
     const int ov = s->sym_overlap;
     if (overlap_gather && b0 == 0 && one_band && a.gate) {
-      // 3: one launch, local units first, remote units gated in-kernel on the gather.
+      // 3: one launch with the local units first; remote units run in it once the gather is
+      // published, or are deferred to a second launch queued behind the gather event.
       a.units = 6;
+      GS_HIP(gs::launch_force_sym(a, s->s_comp));
+      GS_MARK(w0, w, s->s_comp);
+      GS_HIP(hipStreamWaitEvent(s->s_comp, s->ev_gathered, 0));
+      GS_MARK(w1, w, s->s_comp);
+      a.units = 7;
       GS_HIP(gs::launch_force_sym(a, s->s_comp));
       a.units = 0;
     } else if (overlap_gather && b0 == 0 && one_band && ov == 1) {
@@ -817,20 +838,6 @@ int accel_impl(gs_stepper* s, double* acc4, bool step_path) {
   return 0;
 }
 
-// A gated force launch (GRAVSIM_SYM_OVERLAP=3) reported that a remote unit gave up waiting
-// for the all-gather: that step read stale positions, so the run has failed.
-int gate_check(gs_stepper* s) {
-  if (!s->gate_used) return 0;
-  unsigned f = 0;
-  GS_HIP(hipMemcpy(&f, s->gate_buf + 2, sizeof(f), hipMemcpyDeviceToHost));
-  if (f) {
-    gs_set_error("gather gate timed out: a force unit waited longer than GRAVSIM_GATE_TIMEOUT_S "
-                 "for the all-gather (the step is invalid)");
-    return -1;
-  }
-  return 0;
-}
-
 // Wait until progress event `target` - 1 has completed (target == prog_rec: every stream is
 // idle). The deadline restarts whenever one more progress event completes.
 int wait_until(gs_stepper* s, int64_t target, double timeout_s) {
@@ -866,7 +873,7 @@ int wait_until(gs_stepper* s, int64_t target, double timeout_s) {
     }
     if (done) {
       if (all) s->prog_done = s->prog_rec;
-      return all ? gate_check(s) : 0;
+      return 0;
     }
     if (s->have_comm && gs_stepper_comm_check(s)) return -1;
     const double el =
@@ -929,7 +936,6 @@ int gs_stepper_create(const gs_config* cfg, gs_stepper** out) {
   if (const char* v = getenv("GRAVSIM_EMU_COMM_GBPS")) s->emu_gbps = atof(v);
   if (const char* v = getenv("GRAVSIM_EMU_COMM_US")) s->emu_lat_us = atof(v);
   if (const char* v = getenv("GRAVSIM_EMU_COMM_WGS")) s->emu_wgs = atoi(v);
-  if (const char* v = getenv("GRAVSIM_GATE_TIMEOUT_S")) s->gate_timeout_s = atof(v);
   const int64_t own_first = s->L.local_begin / s->L.chunk;
   const int64_t own_last = (s->L.local_begin + s->L.n_local) / s->L.chunk;
   s->own_c0 = (int)(own_first < s->L.n_chunks ? own_first : s->L.n_chunks);
@@ -995,6 +1001,23 @@ int gs_stepper_create(const gs_config* cfg, gs_stepper** out) {
   FAIL_CLEAN(hipMalloc(&s->nonfinite, sizeof(unsigned long long)));
   FAIL_CLEAN(hipMalloc(&s->gate_buf, 4 * sizeof(unsigned)));
   FAIL_CLEAN(hipMemsetAsync(s->gate_buf, 0, 4 * sizeof(unsigned), s->s_comp));
+  if (s->L.mode == GS_MODE_SYM) {
+    // Deferred-unit list of the gated launch (one band's units) and the local-first order.
+    const int rows = s->sym_NC / cfg->nranks;
+    const size_t units = (size_t)rows * (s->sym_S_n + s->sym_D) + 1;
+    FAIL_CLEAN(hipMalloc(&s->defer, units * sizeof(unsigned)));
+    FAIL_CLEAN(hipMemsetAsync(s->defer, 0, units * sizeof(unsigned), s->s_comp));
+    std::vector<int32_t> lf((size_t)2 * (rows + 1), 0);
+    const int a0 = cfg->rank * rows;
+    for (int r = 0; r < rows; ++r) {
+      const int nl = sym_local_segs(a0 + r, s->sym_NC, a0, rows, s->sym_L, s->sym_S_n);
+      lf[r + 1] = lf[r] + s->sym_D + nl;
+      lf[rows + 1 + r + 1] = lf[rows + 1 + r] + s->sym_S_n - nl;
+    }
+    FAIL_CLEAN(hipMalloc(&s->sym_lf, lf.size() * sizeof(int32_t)));
+    FAIL_CLEAN(hipMemcpy(s->sym_lf, lf.data(), lf.size() * sizeof(int32_t),
+                         hipMemcpyHostToDevice));
+  }
   if (s->emulate && s->emu_gbps > 0.0) {
     // Scratch destination of the modeled collectives (the larger of the two per step).
     s->emu_cap = gather_bytes(s);
@@ -1025,7 +1048,7 @@ int gs_stepper_destroy(gs_stepper* s) {
   for (void* p : {s->X[0], s->X[1], s->vel, s->partial, s->acc, (void*)s->mass_dev,
                   (void*)s->nonfinite, (void*)s->sym_Pi, (void*)s->sym_Pj, (void*)s->sym_Pd,
                   (void*)s->sym_S, (void*)s->sym_R, (void*)s->sym_Ti, (void*)s->gate_buf,
-                  s->emu_buf})
+                  (void*)s->defer, (void*)s->sym_lf, s->emu_buf})
     if (p) (void)hipFree(p);
   for (hipEvent_t e : {s->ev_ready, s->ev_gathered, s->ev_t0, s->ev_local, s->ev_end,
                        s->ev_remote, s->ev_fork, s->ev_rem2, s->ev_sym})
@@ -1151,7 +1174,7 @@ int gs_stepper_sync(gs_stepper* s) {
   GS_HIP(hipStreamSynchronize(s->s_rem2));
   GS_HIP(hipStreamSynchronize(s->s_comp));
   s->prog_done = s->prog_rec;
-  return gate_check(s);
+  return 0;
 }
 
 // Bounded wait for every stream, polling RCCL async errors. The deadline bounds PROGRESS: it
@@ -1166,8 +1189,8 @@ int gs_stepper_wait(gs_stepper* s, double timeout_s) {
 // Phase timing of the eager steps enqueued since gs_stepper_set_timing(s, 1) / the previous
 // call (at most 256), averaged per step. out[0] steps, [1] total ms, [2] all-gather ms and
 // [3] group-sum exchange ms (spans on the comm stream), [4] exposed gather ms and [5]
-// exposed exchange ms (compute-stream stalls on them), [6] longest in-kernel gate wait ms,
-// [7] gate timeouts. Multi-rank exposed comm = [4] + [5] (+ [6] with the gated schedule).
+// exposed exchange ms (compute-stream stalls on them: exposed comm = [4] + [5]), [6] the
+// most force units one step deferred past the gather (overlap 3), [7] reserved (0).
 int gs_stepper_phase_stats(gs_stepper* s, double* out8) {
   for (int i = 0; i < 8; ++i) out8[i] = 0.0;
   for (hipStream_t st : {s->s_comm, s->s_rem, s->s_rem2, s->s_comp})
@@ -1189,8 +1212,8 @@ int gs_stepper_phase_stats(gs_stepper* s, double* out8) {
   out8[0] = n;
   unsigned d[2] = {0, 0};
   GS_HIP(hipMemcpy(d, s->gate_buf + 2, sizeof(d), hipMemcpyDeviceToHost));
-  out8[6] = d[1] / s->clk_khz;
-  out8[7] = d[0];
+  out8[6] = d[1];
+  out8[7] = 0.0;
   GS_HIP(hipMemset(s->gate_buf + 2, 0, sizeof(d)));
   s->pev_used = 0;
   return 0;

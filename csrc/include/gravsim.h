@@ -148,12 +148,13 @@ int gs_stepper_phase_ms(gs_stepper* s, float* local_ms, float* comm_ms, float* t
 // Eager steps record per-step phase events while on (hipGraph replay is off meanwhile).
 int gs_stepper_set_timing(gs_stepper* s, int32_t on);
 // Averages over the timed steps since the last call: out[0] steps, [1] step ms, [2] gather
-// ms, [3] exchange ms, [4] exposed gather ms, [5] exposed exchange ms, [6] longest in-kernel
-// gate wait ms, [7] gate timeouts.
+// ms, [3] exchange ms, [4] exposed gather ms, [5] exposed exchange ms (compute-stream stalls),
+// [6] the most force units a step deferred past the gather (overlap 3), [7] reserved.
 int gs_stepper_phase_stats(gs_stepper* s, double* out8);
 // Sym schedule work beside the all-gather: 0 wait then one launch, 1 diagonal units first,
-// 2 local units + remote units on a second stream, 3 one local-first launch with the remote
-// units gated in-kernel on the gather (GRAVSIM_SYM_OVERLAP sets the initial value).
+// 2 local units + remote units on a second stream, 3 one local-first launch whose remote
+// units run once the gather is published or are deferred to a second launch behind it
+// (GRAVSIM_SYM_OVERLAP sets the initial value).
 int gs_stepper_set_overlap(gs_stepper* s, int32_t mode);
 // Bound on the host waiting for the oldest of the enqueued steps when it runs far ahead.
 int gs_stepper_set_timeout(gs_stepper* s, double step_timeout_s);

@@ -74,14 +74,19 @@ struct SymArgs {
                        // (need only the own rows), 2 shell segments only, 4 the shell
                        // segments with a j-chunk outside the own rows, 5 every other unit
                        // (diagonal + rank-local shell: no gathered positions needed),
-                       // 6 all, ordered local-first, the others gated on `gate`
+                       // 6 all, local units first, remote units gated on `gate`,
+                       // 7 the units the units-6 launch deferred (after the gather)
   double dt, eps2, cut2;
-  // Gather gate (units 6): remote units wait until *gate != 0 (set on the comm stream right
-  // after the all-gather; finalize clears it). gate_diag[0]: timeout flag, [1]: longest wait
-  // in wall-clock ticks. A wait longer than gate_ticks gives up and raises the flag.
+  // Gather gate (units 6/7): set on the comm stream right after the all-gather; a remote unit
+  // that finds it still closed appends itself to defer[1..] (count defer[0]) and exits, and
+  // the units-7 launch behind the gather event runs them. Finalize clears gate and count.
+  // defer_max: the largest deferred count seen (diagnostics).
   unsigned* gate;
-  unsigned* gate_diag;
-  uint64_t gate_ticks;
+  unsigned* defer;
+  unsigned* defer_max;
+  const int32_t* lf;    // [rows + 1] local-unit prefix, [rows + 1] remote-unit prefix per row
+  int32_t defer_grid;   // units 7: workgroups walking the deferred list
+  int32_t defer_index;  // (device-side) the deferred entry a units-7 workgroup is running
 };
 
 hipError_t launch_force_sym(const SymArgs& a, hipStream_t s);

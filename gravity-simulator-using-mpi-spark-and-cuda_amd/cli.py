@@ -160,6 +160,8 @@ def main(argv: Optional[list[str]] = None) -> int:
         return _launch(a.nproc, raw)
     cfg = config_from_args(a)
     dist = comm.init()
+    from .runtime.simulation import NonFiniteError
+
     try:
         if a.sweep:
             sizes = [int(x) for x in a.sweep.split(",") if x]
@@ -173,6 +175,9 @@ def main(argv: Optional[list[str]] = None) -> int:
             log = RunLog(cfg.log_format, cfg.log_dir if dist.is_root else None,
                          echo=dist.is_root and not a.quiet)
             run_one(cfg, dist, log, a.quiet)
+    except NonFiniteError as e:  # the NaN/Inf guard (--nan-check-every): fail loudly
+        print(f"gravsim: error: {e}", file=sys.stderr, flush=True)
+        return 3
     finally:
         comm.shutdown(dist)
     return 0

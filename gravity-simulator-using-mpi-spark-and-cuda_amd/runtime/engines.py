@@ -128,15 +128,15 @@ class HipEngine:
     def phase_stats(self) -> dict:
         """Per-step averages over the timed steps since set_timing(True) / the last call.
         comm_ms: the step's collectives on the comm stream (all-gather + group-sum exchange);
-        exposed_comm_ms: how long the compute stream stalled on them (plus the longest
-        in-kernel gate wait with the gated schedule)."""
+        exposed_comm_ms: how long the compute stream stalled on them; deferred_units: the
+        most force units a step had to run after the gather (overlap 3)."""
         out = (ctypes.c_double * 8)()
         _native.check(self.lib, self.lib.gs_stepper_phase_stats(self._s, out), "phase stats")
         v = list(out)
         return {"steps": int(v[0]), "step_ms": v[1], "gather_ms": v[2], "exchange_ms": v[3],
-                "exposed_gather_ms": v[4], "exposed_exchange_ms": v[5], "gate_wait_ms": v[6],
-                "gate_timeouts": int(v[7]), "comm_ms": v[2] + v[3],
-                "exposed_comm_ms": v[4] + v[5] + v[6]}
+                "exposed_gather_ms": v[4], "exposed_exchange_ms": v[5],
+                "deferred_units": int(v[6]), "comm_ms": v[2] + v[3],
+                "exposed_comm_ms": v[4] + v[5]}
 
     def set_overlap(self, mode: int) -> None:
         """Sym-schedule work beside the all-gather (0..3, see gravsim.h)."""

@@ -21,6 +21,7 @@ from __future__ import annotations
 
 import os
 import time
+import warnings
 from typing import Optional
 
 import numpy as np
@@ -67,6 +68,16 @@ class Simulation:
             self.engine.load(c.bodies)
             self.step0 = c.step
             self.staggered = c.meta.get("velocity") == "half-step"
+            stored_dt = float(c.meta.get("dt", cfg.dt))
+            if self.staggered and stored_dt != cfg.dt:
+                # Half-step velocities v_{k-1/2} belong to the checkpoint's dt: synchronise
+                # them with THAT dt first; the new stagger (below) then uses cfg.dt.
+                self._half_kick(+1.0, stored_dt)
+                self.staggered = False
+            for key in ("G", "cutoff", "softening"):
+                if key in c.meta and float(c.meta[key]) != float(getattr(cfg, key)):
+                    warnings.warn(f"resuming a checkpoint written with {key}={c.meta[key]} "
+                                  f"under {key}={getattr(cfg, key)}", stacklevel=2)
         else:
             self.engine.init_ics(cfg.init, cfg.seed)
         if cfg.integrator == "leapfrog" and not self.staggered:
@@ -93,11 +104,11 @@ class Simulation:
             acc[rows.start:rows.stop] = self.engine.accel()[: len(rows), :3]
         return acc
 
-    def _half_kick(self, sign: float) -> None:
+    def _half_kick(self, sign: float, dt: Optional[float] = None) -> None:
         """v += sign * a(x) dt/2 on every body (collective): the leapfrog stagger."""
         b = self.engine.state()
         acc = self._own_accel()
-        b.vel = b.vel + sign * 0.5 * self.cfg.dt * acc
+        b.vel = b.vel + sign * 0.5 * (self.cfg.dt if dt is None else dt) * acc
         self.engine.load(b)
 
     def raw_state(self) -> BodySet:

@@ -4,12 +4,15 @@
 # tasks (each step under its own time limit; the first failure ends the call):
 #   tests[:<pytest -k expr>]  GPU test suite (or a subset), one process, per-test timeout
 #   smoke                     __graft_entry__.smoke()
-#   bench[:<args>]            bench.py (commas in <args> become spaces)
+#   bench[:<args>]            bench.py ("+" in <args> becomes a space)
 #   prof[:<args>]             rocprofv3 kernel-trace stats of bench.py -> gpurun_out/prof
-#   rank[:<args>]             bench/rank_shape.py per-rank emulation (commas -> spaces)
+#   rank[:<args>]             bench/rank_shape.py per-rank emulation ("+" -> space)
 #   rehearsal                 torchrun / self-launch / CLI multi-rank rehearsal on one GPU
 #   configs                   bench/configs.py, every BASELINE config
 #   pmc[:<bench args>]        three rocprofv3 --pmc passes (kernel-trace only) of bench.py
+#   trace[:<rank_shape args>] rocprofv3 kernel trace of bench/rank_shape.py + overlap report
+#   rankprof[:<rank_shape args>] rocprofv3 kernel-trace stats of bench/rank_shape.py
+#   counters                  rocprofv3 -L (the PMC counters this box offers)
 # Outputs land in gpurun_out/<task>*.log.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
@@ -17,7 +20,7 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 out=gpurun_out
 
-args_of() { local a="${1#*:}"; [ "$a" = "$1" ] && a=""; echo "${a//,/ }"; }
+args_of() { local a="${1#*:}"; [ "$a" = "$1" ] && a=""; echo "${a//+/ }"; }
 
 step() {  # $1 = limit (s), $2 = log, rest = command
   local lim=$1 log=$2; shift 2
@@ -55,6 +58,16 @@ for task in "$@"; do
           --phase-steps 0 $a
       done
       python scripts/pmc_summary.py > $out/pmc_summary.txt 2>&1; cat $out/pmc_summary.txt ;;
+    trace)
+      step 600 $out/trace.log rocprofv3 --kernel-trace -d $out/trace -o tr --output-format csv \
+        -- python bench/rank_shape.py $a
+      t=$(find $out/trace -name "*kernel_trace.csv" | head -1)
+      python scripts/overlap_report.py "$t" | tee $out/trace_overlap.txt ;;
+    rankprof)
+      step 900 $out/rankprof.log rocprofv3 --kernel-trace --stats -d $out/rankprof -o rp \
+        --output-format csv -- python bench/rank_shape.py $a
+      head -8 $out/rankprof/rp_kernel_stats.csv ;;
+    counters) step 120 $out/counters.txt rocprofv3 -L ;;
     *) echo "unknown task $task"; exit 2 ;;
   esac
 done

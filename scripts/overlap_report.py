@@ -1,5 +1,6 @@
 """Comm/compute overlap from a rocprofv3 kernel trace (virtual ranks: the all-gather runs as
-blit copies on the comm stream; real RCCL: nccl kernels).
+blit copies on the comm stream; per-rank emulation: comm_model kernels; real RCCL: nccl
+kernels).
 
 For every exchange kernel (copy or nccl) reports how much of its duration ran concurrently
 with a force kernel, and the per-step timeline summary.
@@ -15,7 +16,7 @@ def main(path: str) -> int:
            r.get("Stream_Id", "?")) for r in rows]
     force = [(s, e) for s, e, n, _ in ks if "force_" in n]
     comm = [(s, e, n, st) for s, e, n, st in ks
-            if "copyBuffer" in n or "nccl" in n.lower()]
+            if "copyBuffer" in n or "nccl" in n.lower() or "comm_model" in n]
     if not force or not comm:
         print("no force or exchange kernels in trace")
         return 1

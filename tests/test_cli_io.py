@@ -178,3 +178,52 @@ def test_dump_every_writes_periodic_mpi_dumps(tmp_path, capsys):
     assert d3.exists() and d6.exists()
     assert d6.read_text() == final.read_text() and d3.read_text() != d6.read_text()
     assert d3.read_text().count("Particle ") == 50
+
+
+def _poisoned_checkpoint(tmp_path, n=64):
+    from gravsim.models import initial_conditions as ic
+
+    b = ic.solar_random(n, seed=3)
+    b.pos[5, 2] = np.nan
+    p = tmp_path / "poison.gsck"
+    ck.save(str(p), b, 0, dict(dt=3600.0, dtype="fp64", velocity="synchronized"))
+    return p
+
+
+@pytest.mark.parametrize("device", ["cpu", pytest.param("gpu", marks=pytest.mark.gpu)])
+def test_cli_nan_guard_exits_nonzero(tmp_path, device):
+    """--nan-check-every 1 on a poisoned state: the run stops at the first check with the
+    guard's message and a non-zero exit (the reference printed inf/NaN silently, D1-D3)."""
+    p = _poisoned_checkpoint(tmp_path)
+    r = subprocess.run([sys.executable, "-m", "gravsim", "--n", "64", "--steps", "5", "--device",
+                        device, "--resume", str(p), "--nan-check-every", "1", "--log-format",
+                        "none", "--quiet"], cwd=ROOT, capture_output=True, text=True,
+                       timeout=240)
+    assert r.returncode == 3, (r.returncode, r.stderr[-800:])
+    assert "non-finite position/velocity components at step 1" in r.stderr
+
+
+def test_resume_leapfrog_with_new_dt_resynchronises(tmp_path):
+    """A leapfrog checkpoint holds v_{k-1/2} for ITS dt. Resuming with another dt first
+    synchronises with the stored dt, then re-staggers with the new one: the same as resuming
+    the synchronized state of that checkpoint under the new dt."""
+    cfg = SimConfig(n=200, steps=4, dtype="fp64", device="cpu", integrator="leapfrog",
+                    checkpoint_dir=str(tmp_path), checkpoint_every=4)
+    sim = Simulation(cfg)
+    sim.run()
+    sync = sim.global_state()  # synchronized velocities at step 4
+    sim.close()
+    path = ck.path_for(str(tmp_path), 4)
+    assert ck.load(path).meta["velocity"] == "half-step"
+    a = Simulation(cfg.replace(resume=path, checkpoint_every=0, dt=1800.0))
+    a.run(3)
+    got = a.global_state()
+    a.close()
+    sp = tmp_path / "sync.gsck"
+    ck.save(str(sp), sync, 4, dict(dt=3600.0, velocity="synchronized"))
+    b = Simulation(cfg.replace(resume=str(sp), checkpoint_every=0, dt=1800.0))
+    b.run(3)
+    ref = b.global_state()
+    b.close()
+    assert np.allclose(got.pos, ref.pos, rtol=1e-13, atol=0)
+    assert np.allclose(got.vel, ref.vel, rtol=1e-10, atol=1e-12)

@@ -160,3 +160,64 @@ def test_rccl_one_rank_full_schedule_bitwise(hip, monkeypatch, graph, strategy):
     ref = ref_eng.state().pos
     ref_eng.close()
     assert np.array_equal(got, ref)
+
+
+def _dead_peer_worker(rank, world, port, out_dir):
+    """Rank 1 dies after the communicator is up, before any step's collective; rank 0 steps
+    and must get an error from its bounded wait instead of hanging in the exchange."""
+    import time
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK="0", GRAVSIM_RCCL_RANK_HOSTS="1")
+    import gravsim  # noqa: F401
+    from gravsim.config import SimConfig
+    from gravsim.parallel import comm
+    from gravsim.runtime.engines import HipEngine
+
+    dist = comm.init(timeout_s=60)
+    cfg = SimConfig(n=20000, dtype="fp32", device="gpu", chunk=1024, mode="sym",
+                    step_timeout_s=10)
+    eng = HipEngine(cfg, rank, world, device=0, dist=dist)
+    uid = HipEngine.unique_id() if rank == 0 else None
+    eng.comm_init(comm.broadcast_bytes(dist, uid))
+    eng.init_ics("solar+random", 5)
+    eng.sync()
+    comm.barrier(dist)
+    if rank != 0:
+        os._exit(0)  # the peer is gone: no step, no collective, no clean shutdown
+    t0 = time.time()
+    msg = "no error"
+    try:
+        eng.step(3)
+        eng.sync(timeout_s=10)
+    except RuntimeError as e:
+        msg = str(e)
+    with open(os.path.join(out_dir, "rank0.txt"), "w") as f:
+        f.write(f"{time.time() - t0:.2f}\n{msg}")
+    os._exit(3 if "communicator aborted" in msg else 4)  # skip teardown with a dead peer
+
+
+def test_rccl_dead_peer_aborts_instead_of_hanging(hip, tmp_path):
+    """Failure detection (the reference has none, cuda.cu:145-177): a dead peer
+    turns into an aborted communicator and a non-zero exit within the step timeout."""
+    import multiprocessing
+
+    ctx = multiprocessing.get_context("spawn")
+    port = _port()
+    procs = [ctx.Process(target=_dead_peer_worker, args=(r, 2, port, str(tmp_path)))
+             for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(90)
+    alive = [p for p in procs if p.is_alive()]
+    for p in alive:
+        p.kill()
+        p.join(10)
+    assert not alive, "a rank hung with a dead peer"
+    assert procs[1].exitcode == 0
+    assert procs[0].exitcode == 3, (procs[0].exitcode, (tmp_path / "rank0.txt").read_text()
+                                    if (tmp_path / "rank0.txt").exists() else "")
+    took, msg = (tmp_path / "rank0.txt").read_text().split("\n", 1)
+    assert "communicator aborted" in msg
+    assert float(took) < 30.0, took
