@@ -286,7 +286,11 @@ __device__ __forceinline__ bool local_first_unit(const SymArgs& a, int b, int* b
 __device__ __forceinline__ bool gate_open_or_defer(const SymArgs& a) {
   __shared__ int open_s;
   if (threadIdx.x == 0) {
-    const bool open = __hip_atomic_load(a.gate, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+    // (gate_probe: timing probes only, per-rank emulation: 1 skips the check, 2 loads relaxed)
+    const bool open = a.gate_probe == 1 ? true
+                      : a.gate_probe == 2
+                          ? __hip_atomic_load(a.gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u
+                          : __hip_atomic_load(a.gate, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != 0u;
     if (!open) {
       const unsigned k =
           __hip_atomic_fetch_add(a.defer, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

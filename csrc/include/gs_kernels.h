@@ -87,6 +87,7 @@ struct SymArgs {
   const int32_t* lf;    // [rows + 1] local-unit prefix, [rows + 1] remote-unit prefix per row
   int32_t defer_grid;   // units 7: workgroups walking the deferred list
   int32_t defer_index;  // (device-side) the deferred entry a units-7 workgroup is running
+  int32_t gate_probe;   // timing probe of the emulation only (GRAVSIM_GATE_PROBE): 0 acquire
 };
 
 hipError_t launch_force_sym(const SymArgs& a, hipStream_t s);

@@ -74,6 +74,9 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--record-path", default=None, help="trajectory .npy (frames x n x 3)")
     p.add_argument("--nan-check-every", type=int, default=0)
     p.add_argument("--metrics-json", default=None, help="append the run's JSON metrics line here")
+    p.add_argument("--phase-timing", action="store_true",
+                   help="GPU: time every step's phases with events and report the comm/compute "
+                        "split (comm_ms, exposed_comm_ms) in the metrics (eager steps)")
     p.add_argument("--sweep", default=None,
                    help="comma-separated N values: run each config in turn (pyspark.py sweep)")
     p.add_argument("--nproc", "--gpus", dest="nproc", type=int, default=0,
@@ -103,7 +106,8 @@ def config_from_args(a: argparse.Namespace) -> SimConfig:
                      dump_every=a.dump_every,
                      checkpoint_dir=a.checkpoint_dir, checkpoint_every=a.checkpoint_every,
                      resume=resume, record_every=a.record_every, record_path=a.record_path,
-                     nan_check_every=a.nan_check_every, metrics_json=a.metrics_json).validate()
+                     nan_check_every=a.nan_check_every, metrics_json=a.metrics_json,
+                     phase_timing=a.phase_timing).validate()
 
 
 def run_one(cfg: SimConfig, dist, log, quiet: bool = False, final: bool = True) -> dict:

@@ -63,6 +63,8 @@ class SimConfig:
     record_path: Optional[str] = None
     nan_check_every: int = 0          # NaN/Inf guard period (0 = only at the end)
     metrics_json: Optional[str] = None
+    phase_timing: bool = False        # GPU: per-step phase events (comm/compute split in the
+                                      # metrics; eager steps, no graph replay)
 
     def validate(self) -> "SimConfig":
         if self.n < 1:

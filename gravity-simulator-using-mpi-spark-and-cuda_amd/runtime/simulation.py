@@ -156,6 +156,9 @@ class Simulation:
         periods = [p for p in (cfg.progress_every if log else 0, cfg.checkpoint_every,
                                cfg.record_every, cfg.nan_check_every, cfg.dump_every)
                    if p and p > 0]
+        timing = cfg.phase_timing and isinstance(self.engine, HipEngine)
+        if timing:
+            self.engine.set_timing(True)
         comm.barrier(self.dist)
         t0 = time.perf_counter()
         s = 0
@@ -176,6 +179,14 @@ class Simulation:
         self.engine.sync()
         wall = time.perf_counter() - t0
         wall = comm.allreduce_max(self.dist, wall)
+        extra = {}
+        if timing:  # the comm/compute split, max over ranks
+            ph = self.engine.phase_stats()
+            self.engine.set_timing(False)
+            for k in ("step_ms", "comm_ms", "exposed_comm_ms", "gather_ms", "exchange_ms"):
+                ph[k] = comm.allreduce_max(self.dist, ph[k])
+            extra = {"phase": ph, "comm_ms": ph["comm_ms"],
+                     "exposed_comm_ms": ph["exposed_comm_ms"]}
         self.check_finite()
         lay = getattr(self.engine, "native_layout", {})
         from ..ops._native import KERNEL_NAMES, MODE_NAMES
@@ -183,7 +194,7 @@ class Simulation:
         return RunMetrics(n=cfg.n, steps=steps, dt=cfg.dt, dtype=cfg.dtype, device=self.device,
                           nranks=self.dist.world, wall_s=wall,
                           kernel=KERNEL_NAMES.get(lay.get("kernel", 0), "cpu"),
-                          mode=MODE_NAMES.get(lay.get("mode", 0), "cpu"))
+                          mode=MODE_NAMES.get(lay.get("mode", 0), "cpu"), extra=extra)
 
     def dump_path_for(self, step: int) -> str:
         cfg = self.cfg

@@ -10,6 +10,7 @@
 #   rehearsal                 torchrun / self-launch / CLI multi-rank rehearsal on one GPU
 #   configs                   bench/configs.py, every BASELINE config
 #   pmc[:<bench args>]        three rocprofv3 --pmc passes (kernel-trace only) of bench.py
+#   pmcrank[:<rank args>]     the same passes over bench/rank_shape.py
 #   trace[:<rank_shape args>] rocprofv3 kernel trace of bench/rank_shape.py + overlap report
 #   rankprof[:<rank_shape args>] rocprofv3 kernel-trace stats of bench/rank_shape.py
 #   counters                  rocprofv3 -L (the PMC counters this box offers)
@@ -48,16 +49,19 @@ for task in "$@"; do
     rank) step 1200 $out/rank_$(date +%s).log python bench/rank_shape.py $a ;;
     rehearsal) step 900 $out/rehearsal.log bash scripts/gpu_torchrun.sh ;;
     configs) step 1200 $out/configs.log python bench/configs.py --md $out/baseline_configs.md ;;
-    pmc)
-      for pass in "valu SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS GRBM_GUI_ACTIVE" \
-                  "cycles SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAIT_INST_ANY" \
-                  "lds SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_FMA_F32"; do
+    pmc|pmcrank)
+      # pmc: bench.py (+ args); pmcrank: bench/rank_shape.py (+ args), e.g. an fp64 rank shape
+      if [ "$name" = pmc ]; then prog="bench.py --steps 2 --warmup 1 --check-samples 0 --phase-steps 0 $a"
+      else prog="bench/rank_shape.py $a"; fi
+      rm -rf $out/pmc_valu $out/pmc_cycles $out/pmc_lds
+      for pass in "valu SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU_FMA_F64 GRBM_GUI_ACTIVE" \
+                  "cycles SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64" \
+                  "lds SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU_FMA_F32 SQ_INSTS_SMEM"; do
         set -- $pass; tag=$1; shift
         step 300 $out/pmc_$tag.log rocprofv3 --kernel-trace --pmc "$@" -d $out/pmc_$tag -o pmc \
-          --output-format csv -- python bench.py --steps 2 --warmup 1 --check-samples 0 \
-          --phase-steps 0 $a
+          --output-format csv -- python $prog
       done
-      python scripts/pmc_summary.py > $out/pmc_summary.txt 2>&1; cat $out/pmc_summary.txt ;;
+      python scripts/pmc_summary.py > $out/${name}_summary.txt 2>&1; cat $out/${name}_summary.txt ;;
     trace)
       step 600 $out/trace.log rocprofv3 --kernel-trace -d $out/trace -o tr --output-format csv \
         -- python bench/rank_shape.py $a

@@ -94,3 +94,34 @@ def test_slow_gather_defers_remote_units(hip, monkeypatch):
     assert np.array_equal(res[0], res[1])
     assert deferred[0] == 0
     assert deferred[1] > 0
+
+
+def test_long_healthy_run_does_not_trip_step_timeout(hip):
+    """The bounded wait bounds progress, not the run: 1500 steps of 65,536 bodies (~1.1 s of
+    queued GPU work, far past a 0.3 s budget) complete without a timeout, because one more
+    step finishes every ~0.8 ms (a 600 s budget over a whole queued run used to
+    abort long healthy multi-rank runs)."""
+    from gravsim.runtime.engines import HipEngine
+
+    e = HipEngine(SimConfig(n=65536, dtype="fp32", device="gpu", mode="sym", graph=False))
+    try:
+        e.lib.gs_stepper_set_timeout(e._s, 0.3)
+        e.init_ics("solar+random", 1)
+        e.step(1500)
+        e.sync(timeout_s=0.3)
+        assert e.steps_done == 1500 and e.nonfinite() == 0
+    finally:
+        e.close()
+
+
+def test_stalled_step_trips_step_timeout(hip, monkeypatch):
+    """A step that cannot finish for ~1.8 s (a modeled gather at 0.0005 GB/s) against a
+    0.3 s progress budget: the wait reports a step timeout instead of blocking."""
+    e = _emu(monkeypatch, 65536, 8, 3, 0.0005, 0)
+    try:
+        e.init_ics("solar+random", 2)
+        e.step(2)
+        with pytest.raises(RuntimeError, match="step timeout: no step completed"):
+            e.sync(timeout_s=0.3)
+    finally:
+        e.close()
