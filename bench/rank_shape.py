@@ -43,6 +43,9 @@ def main() -> int:
     ap.add_argument("--rank", type=int, default=-1, help="emulated rank (default: the last)")
     ap.add_argument("--repeat", type=int, default=1, help="run the whole grid this many times "
                     "(alternating configurations, for A/B on a noisy clock)")
+    ap.add_argument("--lf-fill", default="",
+                    help="comma list of GRAVSIM_SYM_LF_FILL values (local units dispatched first "
+                         "by the gated launch; -1 all); empty: built-in default")
     ap.add_argument("--gate-probe", default="0",
                     help="comma list; timing probes of the gated launch: 0 acquire (real), "
                          "1 no check (order only), 2 relaxed load")
@@ -61,10 +64,15 @@ def main() -> int:
                                   a.strategy.split(","), a.mode.split(","),
                                   [float(x) for x in a.comm_gbps.split(",")],
                                   [int(x) for x in a.overlap.split(",")],
-                                  [int(x) for x in a.gate_probe.split(",")]))
-    for P, ipl, kernel, strategy, mode, gbps, ov, gp in grid * a.repeat:
+                                  [int(x) for x in a.gate_probe.split(",")],
+                                  a.lf_fill.split(",")))
+    for P, ipl, kernel, strategy, mode, gbps, ov, gp, fill in grid * a.repeat:
         os.environ["GRAVSIM_EMU_COMM_GBPS"] = str(gbps)
         os.environ["GRAVSIM_GATE_PROBE"] = str(gp)
+        if fill:
+            os.environ["GRAVSIM_SYM_LF_FILL"] = fill
+        else:
+            os.environ.pop("GRAVSIM_SYM_LF_FILL", None)
         cfg = SimConfig(n=a.n, dtype=a.dtype, device="gpu", ipl=ipl, kernel=kernel,
                         strategy=strategy, mode=mode, graph_comm=a.graph)
         r = (a.rank if a.rank >= 0 else P - 1) if P > 1 else 0
@@ -89,7 +97,8 @@ def main() -> int:
         b = base.get(key)
         print(json.dumps(dict(P=P, rank=r, n=a.n, dtype=a.dtype, ipl=ipl, kernel=kernel,
                               strategy=strategy, mode=e.native_layout["mode"], comm_gbps=gbps,
-                              comm_us=a.comm_us, overlap=ov, gate_probe=gp, graph=a.graph,
+                              comm_us=a.comm_us, overlap=ov, gate_probe=gp, lf_fill=fill,
+                              graph=a.graph,
                               ms_per_step=ms,
                               predicted_efficiency=(b / (P * ms)) if b else None,
                               predicted_body_updates_per_s=a.n / (ms * 1e-3), phase=phase,

@@ -247,35 +247,14 @@ __device__ __forceinline__ void run_tiles(const SymArgs& a, ISetK<T>& is, TileSe
 // units 6: the grid lists every unit of the band, local ones (diagonal parts, then the
 // rank-local shell segments, row by row) before the remote ones (row by row). Workgroups are
 // dispatched in grid order, so the gathered rows are needed only after ~the local share of
-// the step has been handed out. lf = [local prefix (rows + 1) | remote prefix (rows + 1)]
-// per rank row, built on the host (gs_sym_local_segs): the row of unit b is a binary search.
-// Returns true for a remote (gated) unit.
-__device__ __forceinline__ int prefix_row(const int32_t* pre, int rows, int b) {
-  int lo = 0, hi = rows;  // pre[lo] <= b < pre[hi]
-  while (hi - lo > 1) {
-    const int mid = (lo + hi) >> 1;
-    if (pre[mid] <= b) lo = mid;
-    else hi = mid;
-  }
-  return lo;
-}
-
+// the step has been handed out. The order is a host-built map (one uniform load per
+// workgroup: unit -> row << 16 | segment, bit 31 = remote); a search through prefix sums put
+// a chain of dependent loads in front of every workgroup and cost 2 % of the step.
 __device__ __forceinline__ bool local_first_unit(const SymArgs& a, int b, int* br, int* s) {
-  const int32_t* lpre = a.lf;
-  const int32_t* rpre = a.lf + a.rows + 1;
-  if (b < lpre[a.rows]) {
-    const int r = prefix_row(lpre, a.rows, b);
-    const int k = b - lpre[r];
-    *br = r;
-    *s = k < a.D ? a.S + k : k - a.D;
-    return false;
-  }
-  b -= lpre[a.rows];
-  const int r = prefix_row(rpre, a.rows, b);
-  const int nl = (lpre[r + 1] - lpre[r]) - a.D;  // the row's local shell segments
-  *br = r;
-  *s = nl + (b - rpre[r]);
-  return true;
+  const uint32_t m = (uint32_t)a.lf[b];
+  *br = (int)((m >> 16) & 0x7fffu);
+  *s = (int)(m & 0xffffu);
+  return (m >> 31) != 0u;
 }
 
 // Remote unit of the local-first launch (units 6): go ahead if the comm stream has already

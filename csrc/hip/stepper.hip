@@ -131,7 +131,7 @@ struct gs_stepper {
   // deferred past the gather (since the last phase_stats call). defer: count + unit list.
   unsigned* gate_buf = nullptr;
   unsigned* defer = nullptr;
-  int32_t* sym_lf = nullptr;  // units-6 order: local / remote unit prefix per rank row
+  int32_t* sym_lf = nullptr;  // units-6 order: unit -> row << 16 | segment (bit 31 remote)
   int gate_probe = 0;         // GRAVSIM_GATE_PROBE (emulation timing probes only)
   // Phase timing of eager steps (timed): one event set per step, summed by phase_stats.
   struct PhaseEv {
@@ -602,7 +602,7 @@ int enqueue_sym(gs_stepper* s, int cur, bool need_gather, bool gathered_external
   // Gate the remote units on the gather in-kernel (GRAVSIM_SYM_OVERLAP=3): a collective of
   // this stepper (RCCL or modeled) and one band (the gated launch covers every unit).
   const bool gated = part == 3 && need_gather && !gathered_externally && xcomm(s) &&
-                     s->sym_overlap == 3 && s->sym_band >= a.rows;
+                     s->sym_overlap == 3 && s->sym_band >= a.rows && s->sym_lf;
   if (gated) a.gate = s->gate_buf + cur;
   if (part & 1) {
     if (need_gather) {
@@ -757,6 +757,9 @@ int upload_state(gs_stepper* s, const double* pos, const double* vel, const doub
                         s->s_comp));
   GS_HIP(hipMemcpyAsync(s->vel, V.data(), V.size() * sizeof(T), hipMemcpyHostToDevice,
                         s->s_comp));
+  if (s->emulate)  // (see gs_stepper_init_ics)
+    GS_HIP(hipMemcpyAsync(s->X[1], s->X[0], (size_t)np * 4 * sizeof(T), hipMemcpyDeviceToDevice,
+                          s->s_comp));
   GS_HIP(hipStreamSynchronize(s->s_comp));
   s->k = 0;
   s->full[0] = true;
@@ -1010,16 +1013,40 @@ int gs_stepper_create(const gs_config* cfg, gs_stepper** out) {
     const size_t units = (size_t)rows * (s->sym_S_n + s->sym_D) + 1;
     FAIL_CLEAN(hipMalloc(&s->defer, units * sizeof(unsigned)));
     FAIL_CLEAN(hipMemsetAsync(s->defer, 0, units * sizeof(unsigned), s->s_comp));
-    std::vector<int32_t> lf((size_t)2 * (rows + 1), 0);
+    // unit -> row << 16 | segment (bit 31: remote), local units first (gs_kernels.h)
+    // Only the first `fill` units need to be local: enough to keep the GPU busy while the
+    // gather runs (default two dispatch waves, 4 workgroups per CU; GRAVSIM_SYM_LF_FILL, -1:
+    // every local unit first). The rest keep the row-major order of the ungated launch.
+    std::vector<int32_t> lf;
+    if (rows < 32768 && s->sym_S_n + s->sym_D < 65536) lf.reserve(units);  // else: no map
     const int a0 = cfg->rank * rows;
-    for (int r = 0; r < rows; ++r) {
-      const int nl = sym_local_segs(a0 + r, s->sym_NC, a0, rows, s->sym_L, s->sym_S_n);
-      lf[r + 1] = lf[r] + s->sym_D + nl;
-      lf[rows + 1 + r + 1] = lf[rows + 1 + r] + s->sym_S_n - nl;
+    long fill = 4L * s->cus;
+    if (const char* v = getenv("GRAVSIM_SYM_LF_FILL")) fill = atol(v);
+    std::vector<int> nl(rows);
+    std::vector<char> moved((size_t)rows * (s->sym_S_n + s->sym_D), 0);
+    const int per = s->sym_S_n + s->sym_D;
+    for (int r = 0; r < rows && lf.capacity(); ++r) {
+      nl[r] = sym_local_segs(a0 + r, s->sym_NC, a0, rows, s->sym_L, s->sym_S_n);
+      for (int q = 0; q < s->sym_D && (fill < 0 || (long)lf.size() < fill); ++q) {
+        lf.push_back((r << 16) | (s->sym_S_n + q));
+        moved[(size_t)r * per + s->sym_S_n + q] = 1;
+      }
+      for (int g = 0; g < nl[r] && (fill < 0 || (long)lf.size() < fill); ++g) {
+        lf.push_back((r << 16) | g);
+        moved[(size_t)r * per + g] = 1;
+      }
     }
-    FAIL_CLEAN(hipMalloc(&s->sym_lf, lf.size() * sizeof(int32_t)));
-    FAIL_CLEAN(hipMemcpy(s->sym_lf, lf.data(), lf.size() * sizeof(int32_t),
-                         hipMemcpyHostToDevice));
+    for (int r = 0; r < rows && lf.capacity(); ++r)
+      for (int u = 0; u < per; ++u) {  // the ungated order: segments, then diagonal parts
+        if (moved[(size_t)r * per + u]) continue;
+        const bool remote = u < s->sym_S_n && u >= nl[r];
+        lf.push_back((int32_t)((remote ? 0x80000000u : 0u) | ((uint32_t)r << 16) | (uint32_t)u));
+      }
+    if (!lf.empty()) {
+      FAIL_CLEAN(hipMalloc(&s->sym_lf, lf.size() * sizeof(int32_t)));
+      FAIL_CLEAN(hipMemcpy(s->sym_lf, lf.data(), lf.size() * sizeof(int32_t),
+                           hipMemcpyHostToDevice));
+    }
   }
   if (s->emulate && s->emu_gbps > 0.0) {
     // Scratch destination of the modeled collectives (the larger of the two per step).
@@ -1097,6 +1124,14 @@ int gs_stepper_init_ics(gs_stepper* s, int32_t ic, uint64_t seed) {
   s->k = 0;
   s->full[0] = true;
   s->full[1] = false;
+  if (s->emulate) {
+    // The emulated rank never receives remote rows: give X[1] the same realistic positions as
+    // X[0] so odd steps do not run on all-zero remote rows (lower power, higher clocks: the
+    // force kernel measured 5 % faster on them, profiles/r2_trace_steps_parity.txt).
+    GS_HIP(hipMemcpyAsync(s->X[1], s->X[0], (size_t)s->L.n_pad * row_bytes(s),
+                          hipMemcpyDeviceToDevice, s->s_comp));
+    GS_HIP(hipStreamSynchronize(s->s_comp));
+  }
   if (s->graph) { (void)hipGraphExecDestroy(s->graph); s->graph = nullptr; }
   return 0;
 }

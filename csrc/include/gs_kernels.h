@@ -84,7 +84,7 @@ struct SymArgs {
   unsigned* gate;
   unsigned* defer;
   unsigned* defer_max;
-  const int32_t* lf;    // [rows + 1] local-unit prefix, [rows + 1] remote-unit prefix per row
+  const int32_t* lf;    // units 6 order: unit -> row << 16 | segment (bit 31: remote unit)
   int32_t defer_grid;   // units 7: workgroups walking the deferred list
   int32_t defer_index;  // (device-side) the deferred entry a units-7 workgroup is running
   int32_t gate_probe;   // timing probe of the emulation only (GRAVSIM_GATE_PROBE): 0 acquire

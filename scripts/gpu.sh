@@ -66,7 +66,8 @@ for task in "$@"; do
       step 600 $out/trace.log rocprofv3 --kernel-trace -d $out/trace -o tr --output-format csv \
         -- python bench/rank_shape.py $a
       t=$(find $out/trace -name "*kernel_trace.csv" | head -1)
-      python scripts/overlap_report.py "$t" | tee $out/trace_overlap.txt ;;
+      python scripts/overlap_report.py "$t" | tee $out/trace_overlap.txt
+      python scripts/trace_steps.py "$t" | tee $out/trace_steps.txt ;;
     rankprof)
       step 900 $out/rankprof.log rocprofv3 --kernel-trace --stats -d $out/rankprof -o rp \
         --output-format csv -- python bench/rank_shape.py $a
