@@ -1,7 +1,10 @@
 """Kernel/schedule sweep in ONE process (interleaved rounds, §5.4 rule 24 of the HIP guide).
 
     python bench/sweep.py --n 1048576 --steps 3 --rounds 2 --grid "kernel=lds,smem;ipl=1,2,4;mode=fused,split"
-Prints one JSON line per (config, round) and a summary sorted by median ms/step.
+    python bench/sweep.py --n 65536 --grid "mode=sym;env.GRAVSIM_SYM_DIAG_LAST=0,1"
+Axes named env.<VAR> set that environment variable while the engine is created (the native
+stepper reads its A/B knobs at creation). Prints one JSON line per (config, round) and a
+summary sorted by median ms/step.
 """
 from __future__ import annotations
 
@@ -39,8 +42,17 @@ def main() -> int:
     combos = [dict(c) for c in itertools.product(*axes)]
     engines = []
     for c in combos:
-        cfg = SimConfig(n=a.n, dtype=a.dtype, device="gpu", **c)
+        env = {k[4:]: v for k, v in c.items() if k.startswith("env.")}
+        kw = {k: v for k, v in c.items() if not k.startswith("env.")}
+        saved = {k: os.environ.get(k) for k in env}
+        os.environ.update(env)
+        cfg = SimConfig(n=a.n, dtype=a.dtype, device="gpu", **kw)
         e = HipEngine(cfg)
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
         e.init_ics("solar+random", cfg.seed)
         e.step(1)
         e.sync()

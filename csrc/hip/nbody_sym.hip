@@ -302,7 +302,20 @@ __device__ __forceinline__ void force_sym_body(const SymArgs& a) {
   } else if (a.units == 2 || a.units == 4) {  // shell units: all (2) or the non-local ones (4)
     br = blockIdx.x / a.S;
     s = blockIdx.x % a.S;
-  } else {  // every unit (0), or the diagonal ones + the rank-local shell ones (5)
+  } else if (a.units == 0 && a.diag_last) {
+    // Every unit: the shell segments row by row, then all diagonal parts. A diagonal part is
+    // one-sided (about half the issue time of a shell segment), so dispatching them last fills
+    // the launch's final, partial wave of workgroups with short jobs.
+    const int shell = a.band_rows * a.S;
+    if ((int)blockIdx.x < shell) {
+      br = blockIdx.x / a.S;
+      s = blockIdx.x % a.S;
+    } else {
+      const int k = blockIdx.x - shell;
+      br = k / a.D;
+      s = a.S + k % a.D;
+    }
+  } else {  // the diagonal ones + the rank-local shell ones (5), or every unit row by row
     br = blockIdx.x / (a.S + a.D);
     s = blockIdx.x % (a.S + a.D);
   }

@@ -133,6 +133,7 @@ struct gs_stepper {
   unsigned* defer = nullptr;
   int32_t* sym_lf = nullptr;  // units-6 order: unit -> row << 16 | segment (bit 31 remote)
   int gate_probe = 0;         // GRAVSIM_GATE_PROBE (emulation timing probes only)
+  int diag_last = 1;          // GRAVSIM_SYM_DIAG_LAST=0: row-by-row unit order (A/B only)
   // Phase timing of eager steps (timed): one event set per step, summed by phase_stats.
   struct PhaseEv {
     hipEvent_t t0, end, g0, g1, w0, w1, x0, x1, j0, j1;
@@ -298,6 +299,7 @@ gs::SymArgs sym_args(gs_stepper* s, int cur) {
   a.defer_grid = 2 * s->cus;  // resident force workgroups: 2 per CU
   a.defer_index = 0;
   a.gate_probe = s->emulate ? s->gate_probe : 0;
+  a.diag_last = s->diag_last;
   return a;
 }
 
@@ -942,6 +944,7 @@ int gs_stepper_create(const gs_config* cfg, gs_stepper** out) {
   if (const char* v = getenv("GRAVSIM_EMU_COMM_US")) s->emu_lat_us = atof(v);
   if (const char* v = getenv("GRAVSIM_EMU_COMM_WGS")) s->emu_wgs = atoi(v);
   if (const char* v = getenv("GRAVSIM_GATE_PROBE")) s->gate_probe = atoi(v);
+  if (const char* v = getenv("GRAVSIM_SYM_DIAG_LAST")) s->diag_last = atoi(v);
   const int64_t own_first = s->L.local_begin / s->L.chunk;
   const int64_t own_last = (s->L.local_begin + s->L.n_local) / s->L.chunk;
   s->own_c0 = (int)(own_first < s->L.n_chunks ? own_first : s->L.n_chunks);

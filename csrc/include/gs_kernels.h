@@ -88,6 +88,7 @@ struct SymArgs {
   int32_t defer_grid;   // units 7: workgroups walking the deferred list
   int32_t defer_index;  // (device-side) the deferred entry a units-7 workgroup is running
   int32_t gate_probe;   // timing probe of the emulation only (GRAVSIM_GATE_PROBE): 0 acquire
+  int32_t diag_last;    // units 0: shell segments first, diagonal parts last (else row by row)
 };
 
 hipError_t launch_force_sym(const SymArgs& a, hipStream_t s);

@@ -7,6 +7,7 @@
 #   bench[:<args>]            bench.py ("+" in <args> becomes a space)
 #   prof[:<args>]             rocprofv3 kernel-trace stats of bench.py -> gpurun_out/prof
 #   rank[:<args>]             bench/rank_shape.py per-rank emulation ("+" -> space)
+#   sweep[:<args>]            bench/sweep.py in-process interleaved A/B
 #   rehearsal                 torchrun / self-launch / CLI multi-rank rehearsal on one GPU
 #   configs                   bench/configs.py, every BASELINE config
 #   pmc[:<bench args>]        three rocprofv3 --pmc passes (kernel-trace only) of bench.py
@@ -47,6 +48,7 @@ for task in "$@"; do
         --output-format csv -- python bench.py --steps 3 --warmup 1 $a
       head -6 $out/prof/bench_kernel_stats.csv ;;
     rank) step 1200 $out/rank_$(date +%s).log python bench/rank_shape.py $a ;;
+    sweep) step 1200 $out/sweep_$(date +%s).log python bench/sweep.py $a ;;
     rehearsal) step 900 $out/rehearsal.log bash scripts/gpu_torchrun.sh ;;
     configs) step 1200 $out/configs.log python bench/configs.py --md $out/baseline_configs.md ;;
     pmc|pmcrank)
