@@ -359,11 +359,14 @@ int ensure_sym(gs_stepper* s) {
     return -1;
   const size_t nl = (size_t)s->L.n_local, rows = (size_t)s->sym_NC / s->cfg.nranks;
   const size_t e = s->esz;
-  // Rows per band: the partial slots of one band stay within the budget (default 32 GiB,
-  // GRAVSIM_SYM_BAND_MB overrides; tests use a tiny budget to force many bands). 1M bodies
-  // need 6.4 GB for all rows (one band); 16M on 8 ranks would need 109 GB per rank.
+  // Rows per band: the partial slots of one band stay within the budget: half of the free
+  // HBM at creation (an MI355X has 288 GB; at least 32 GiB), GRAVSIM_SYM_BAND_MB overrides
+  // (tests use a tiny budget to force many bands). 1M bodies need 6.4 GB for all rows; 16M
+  // on 8 ranks needs 109 GB per rank, one band on an otherwise empty MI355X.
   const size_t per_row = (size_t)(s->sym_S_n + s->sym_H + s->sym_D) * 3 * gs::kSymC * e;
   size_t budget = (size_t)32 << 30;
+  size_t free_b = 0, total_b = 0;
+  if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b / 2 > budget) budget = free_b / 2;
   if (const char* mb = getenv("GRAVSIM_SYM_BAND_MB")) budget = (size_t)atoll(mb) << 20;
   size_t band = budget / per_row;
   if (band < 1) band = 1;
