@@ -79,18 +79,18 @@ __device__ __forceinline__ void interact(T xi, T yi, T zi, T xj, T yj, T zj, T m
     // fp64 step path: refine r^-3 directly instead of r^-1. With y0 = v_rsq_f64(r2) and
     // e = 1 - r2 y0^2 (|e| <= 1.1e-7), r^-3 = y0^3 (1 - e)^(-3/2) = y0^3 (1 + 3/2 e + 15/8 e^2)
     // + O(e^3 ~ 1e-21): 7 f64 ops where a Halley-refined r^-1 followed by mu r^-1 r^-2 takes 8.
-    const bool ok = FM == FM_FAST || r2 >= cut2;
-    const T rr = ok ? r2 : T(1);
-    const T y0 = __builtin_amdgcn_rsq(rr);
+    // FM_EXACT: one select on s; an inf/NaN formed below the cutoff (r = 0: rsq = inf,
+    // e = NaN) never leaves it (selecting the rsq input too cost 2 more v_cndmask).
+    const T y0 = __builtin_amdgcn_rsq(r2);
     const T y2 = y0 * y0;
-    const T e = fma_(-rr, y2, T(1));
+    const T e = fma_(-r2, y2, T(1));
     // 1.875 and 1.5 are not inline f64 constants: made opaque (loop-invariant, eps2 is a
     // finite kernel argument) so they live in VGPRs instead of being re-materialised by
     // v_mov_b32 pairs for a v_fmac in every interaction.
     const T c15 = T(1.5) + eps2 * T(0), c1875 = T(1.875) + eps2 * T(0);
     const T corr = fma_(e, fma_(e, c1875, c15), T(1));
     T s = (muj * (y2 * y0)) * corr;
-    if constexpr (FM == FM_EXACT) s = ok ? s : T(0);
+    if constexpr (FM == FM_EXACT) s = r2 >= cut2 ? s : T(0);
     ax = fma_(s, dx, ax);
     ay = fma_(s, dy, ay);
     az = fma_(s, dz, az);

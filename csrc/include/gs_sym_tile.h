@@ -304,16 +304,15 @@ __device__ __forceinline__ void meet_j(ISetT<double, I>& a, double xj, double yj
   for (int i = 0; i < I; ++i) {
     const double dx = xj - a.x[i], dy = yj - a.y[i], dz = zj - a.z[i];
     const double r2 = __builtin_fma(dz, dz, __builtin_fma(dy, dy, __builtin_fma(dx, dx, eps2)));
-    // EXACT (reference hard cutoff): the pair's r^-3 is 0 below the cutoff; the rsq input is
-    // replaced so no inf/NaN is formed on the way.
-    const bool ok = !EXACT || r2 >= cut2;
-    const double rr = EXACT ? (ok ? r2 : 1.0) : r2;
-    const double y0 = __builtin_amdgcn_rsq(rr);
+    // EXACT (reference hard cutoff): the pair's r^-3 is 0 below the cutoff. One select on w
+    // (as the fp32 tiles do): an inf/NaN formed below the cutoff (r = 0: rsq = inf, e = NaN)
+    // never leaves it. Selecting the rsq input as well cost 2 more v_cndmask per pair.
+    const double y0 = __builtin_amdgcn_rsq(r2);
     const double y2 = y0 * y0;
-    const double e = __builtin_fma(-rr, y2, 1.0);
+    const double e = __builtin_fma(-r2, y2, 1.0);
     const double corr = __builtin_fma(e, __builtin_fma(e, c1875, c15), 1.0);
     double w = (y2 * y0) * corr;
-    if constexpr (EXACT) w = ok ? w : 0.0;
+    if constexpr (EXACT) w = r2 >= cut2 ? w : 0.0;
     const double si = mj * w;
     a.ax[i] = __builtin_fma(si, dx, a.ax[i]);
     a.ay[i] = __builtin_fma(si, dy, a.ay[i]);
