@@ -55,8 +55,10 @@ def parse(argv=None) -> argparse.Namespace:
                     help="capture multi-rank steps, RCCL collectives included, in a hipGraph")
     ap.add_argument("--no-graph-comm", dest="graph_comm", action="store_false",
                     help=argparse.SUPPRESS)
-    ap.add_argument("--overlap", type=int, default=None, choices=[0, 1, 2, 3],
-                    help="sym work beside the all-gather (default: GRAVSIM_SYM_OVERLAP or 0)")
+    ap.add_argument("--overlap", default="auto", choices=["auto", "0", "1", "2", "3"],
+                    help="sym work beside the all-gather. auto (multi-rank sym): the gated "
+                         "local-first launch (3) if a 2-step self-check from the same ICs "
+                         "gives the same bits as the ungated schedule (0), else 0")
     ap.add_argument("--dt", type=float, default=3600.0)
     ap.add_argument("--cutoff-mode", default="auto", choices=["auto", "exact", "fast"])
     ap.add_argument("--strategy", default="allgather", choices=["allgather", "ring"],
@@ -106,6 +108,29 @@ def sampled_error(eng, cfg, samples: int, seed: int = 7) -> float:
     return worst
 
 
+def overlap_self_check(eng, cfg, dist, comm, steps: int = 2):
+    """Run `steps` steps from the benchmark ICs with the ungated sym schedule (overlap 0) and
+    with the gated local-first launch (overlap 3), on every rank, and keep 3 only if both give
+    the same bits everywhere (they evaluate the same units into the same slots: docs/DESIGN.md
+    §7). Untimed. Returns (mode, verdict)."""
+    import numpy as np
+
+    out = []
+    for ov in (0, 3):
+        eng.set_overlap(ov)
+        eng.init_ics("solar+random", cfg.seed)
+        eng.step(steps)
+        eng.sync()
+        b = eng.state()
+        own = eng.layout.real_local
+        out.append((b.pos[own.start:own.stop].copy(), b.vel[own.start:own.stop].copy()))
+    same = all(np.array_equal(x, y) for x, y in zip(out[0], out[1]))
+    bad = comm.allreduce_sum(dist, 0.0 if same else 1.0)
+    if bad:
+        return 0, f"gated launch differed from the ungated one on {int(bad)} rank(s): overlap 0"
+    return 3, f"gated == ungated bitwise after {steps} steps on every rank"
+
+
 def main(argv=None) -> int:
     raw = list(sys.argv[1:] if argv is None else argv)
     a = parse(raw)
@@ -144,11 +169,16 @@ def main(argv=None) -> int:
                     ipl=a.ipl, graph=a.graph, graph_comm=a.graph_comm,
                     cutoff_mode=a.cutoff_mode, strategy=a.strategy).validate()
     eng = HipEngine(cfg, rank, world, device=dev, dist=dist)
-    if a.overlap is not None:
-        eng.set_overlap(a.overlap)
     if world > 1:
         uid = HipEngine.unique_id() if rank == 0 else None
         eng.comm_init(comm.broadcast_bytes(dist, uid))
+    sym = _native.MODE_NAMES.get(eng.native_layout["mode"]) == "sym"
+    overlap, overlap_check = (0, None)
+    if a.overlap != "auto":
+        overlap = int(a.overlap)
+    elif world > 1 and sym:
+        overlap, overlap_check = overlap_self_check(eng, cfg, dist, comm)
+    eng.set_overlap(overlap)
     eng.init_ics("solar+random", cfg.seed)
     eng.sync()
 
@@ -228,6 +258,8 @@ def main(argv=None) -> int:
                 f"fast (core^2={fmode['eps2']:.3g} m^2; bit-identical to the 1e-10 m hard cutoff "
                 "for separations above ~mm)",
                 "graph": bool(a.graph and (world == 1 or a.graph_comm)),
+                "overlap": overlap,
+                "overlap_check": overlap_check,
                 # N^2 ordered pair terms per step (what a one-sided sum evaluates) ...
                 "effective_interactions_per_s": float(cfg.n) * cfg.n * a.steps / wall,
                 # ... and the pair evaluations actually performed (sym: N(N-1)/2 per step)

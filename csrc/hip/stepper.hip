@@ -1042,12 +1042,16 @@ int gs_stepper_create(const gs_config* cfg, gs_stepper** out) {
         moved[(size_t)r * per + g] = 1;
       }
     }
-    for (int r = 0; r < rows && lf.capacity(); ++r)
-      for (int u = 0; u < per; ++u) {  // the ungated order: segments, then diagonal parts
-        if (moved[(size_t)r * per + u]) continue;
-        const bool remote = u < s->sym_S_n && u >= nl[r];
-        lf.push_back((int32_t)((remote ? 0x80000000u : 0u) | ((uint32_t)r << 16) | (uint32_t)u));
-      }
+    // The ungated launch's order for the rest: shell segments row by row, then the diagonal
+    // parts (dispatched last, they fill the final partial wave).
+    for (int pass = 0; pass < 2 && lf.capacity(); ++pass)
+      for (int r = 0; r < rows; ++r)
+        for (int u = pass ? s->sym_S_n : 0; u < (pass ? per : s->sym_S_n); ++u) {
+          if (moved[(size_t)r * per + u]) continue;
+          const bool remote = u < s->sym_S_n && u >= nl[r];
+          lf.push_back(
+              (int32_t)((remote ? 0x80000000u : 0u) | ((uint32_t)r << 16) | (uint32_t)u));
+        }
     if (!lf.empty()) {
       FAIL_CLEAN(hipMalloc(&s->sym_lf, lf.size() * sizeof(int32_t)));
       FAIL_CLEAN(hipMemcpy(s->sym_lf, lf.data(), lf.size() * sizeof(int32_t),

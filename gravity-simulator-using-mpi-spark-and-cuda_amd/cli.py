@@ -53,6 +53,10 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--step-timeout", dest="step_timeout_s", type=float, default=d.step_timeout_s,
                    help="multi-rank hang detection: abort the RCCL communicator when no step "
                         "completes for this many seconds (0 = wait forever)")
+    p.add_argument("--overlap", type=int, choices=[-1, 0, 1, 2, 3], default=d.overlap,
+                   help="multi-rank sym schedule: work beside the all-gather (3: one launch, "
+                        "rank-local units first, remote units once the gather is published; "
+                        "-1: built-in default)")
     p.add_argument("--strategy", choices=["allgather", "ring"], default=d.strategy,
                    help="multi-rank GPU exchange: one all-gather overlapped with the local "
                         "chunks, or a ring of P-1 neighbour send/recv steps computed on arrival")
@@ -99,7 +103,7 @@ def config_from_args(a: argparse.Namespace) -> SimConfig:
                      seed=a.seed, G=a.G, cutoff=a.cutoff, softening=a.softening,
                      cutoff_mode=a.cutoff_mode, integrator=a.integrator, kernel=a.kernel,
                      mode=a.mode, ipl=a.ipl, chunk=a.chunk, graph=a.graph, graph_comm=a.graph_comm,
-                     strategy=a.strategy, step_timeout_s=a.step_timeout_s,
+                     strategy=a.strategy, step_timeout_s=a.step_timeout_s, overlap=a.overlap,
                      threads=a.threads,
                      log_dir=a.log_dir, log_format=a.log_format, progress_every=a.progress_every,
                      print_positions=a.print_positions, dump_path=a.dump_path,

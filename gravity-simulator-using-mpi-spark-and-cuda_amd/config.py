@@ -46,6 +46,9 @@ class SimConfig:
                                   # default: docs/DESIGN.md "hipGraph and RCCL".
     comm: str = "auto"            # rccl (GPU) | gloo (CPU) | none
     strategy: str = "allgather"   # multi-rank exchange: allgather | ring (pipelined send/recv)
+    overlap: int = -1             # sym work beside the all-gather: 0 none, 1 diagonal units
+                                  # first, 2 two streams, 3 gated local-first launch; -1 native
+                                  # default (GRAVSIM_SYM_OVERLAP or 0)
     threads: int = 0              # CPU engine OpenMP threads (0 = default)
     step_timeout_s: float = 600.0 # multi-rank hang detection: abort RCCL when no step completes
                                   # for this long
@@ -98,6 +101,8 @@ class SimConfig:
             raise ValueError("cutoff_mode must be auto, exact or fast")
         if self.strategy not in ("allgather", "ring"):
             raise ValueError("strategy must be allgather or ring")
+        if self.overlap not in (-1, 0, 1, 2, 3):
+            raise ValueError("overlap must be -1 (default) or 0..3")
         if self.step_timeout_s < 0:
             raise ValueError("step_timeout_s must be >= 0 (0 = unbounded)")
         if self.cutoff < 0 or self.softening < 0:

@@ -67,6 +67,8 @@ class HipEngine:
         self.native_layout = L.as_dict()
         if nranks > 1 and cfg.step_timeout_s:
             self.lib.gs_stepper_set_timeout(self._s, float(cfg.step_timeout_s))
+        if cfg.overlap >= 0:
+            self.set_overlap(cfg.overlap)
         self.layout: Layout = make_layout(cfg.n, rank, nranks, L.chunk,
                                           sym=L.mode == _native.MODE_IDS["sym"])
         assert self.layout.n_pad == L.n_pad, "Python layout mirror disagrees with native"

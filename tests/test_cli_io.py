@@ -227,3 +227,28 @@ def test_resume_leapfrog_with_new_dt_resynchronises(tmp_path):
     b.close()
     assert np.allclose(got.pos, ref.pos, rtol=1e-13, atol=0)
     assert np.allclose(got.vel, ref.vel, rtol=1e-10, atol=1e-12)
+
+
+def test_metrics_pair_counts():
+    from gravsim.utils.metrics import RunMetrics
+
+    m = RunMetrics(n=1000, steps=10, dt=1.0, dtype="fp32", device="gpu", nranks=1, wall_s=2.0,
+                   mode="sym")
+    assert m.effective_interactions_per_s == pytest.approx(1000 * 1000 * 10 / 2.0)
+    assert m.pair_evals_per_s == pytest.approx(1000 * 999 / 2 * 10 / 2.0)
+    d = json.loads(m.to_json())
+    assert "interactions_per_s" not in d and d["pair_evals_per_s"] == m.pair_evals_per_s
+    m.mode = "split"
+    assert m.pair_evals_per_s == m.effective_interactions_per_s
+
+
+def test_cli_multi_rank_flags_parse():
+    from gravsim.cli import build_parser, config_from_args
+
+    a = build_parser().parse_args(["--n", "64", "--step-timeout", "30", "--graph-comm",
+                                   "--phase-timing", "--gpus", "2"])
+    cfg = config_from_args(a)
+    assert cfg.step_timeout_s == 30 and cfg.graph_comm and cfg.phase_timing and a.nproc == 2
+    assert not config_from_args(build_parser().parse_args(["--n", "64"])).graph_comm
+    with pytest.raises(ValueError):
+        SimConfig(step_timeout_s=-1).validate()
