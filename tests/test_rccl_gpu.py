@@ -85,9 +85,13 @@ OV3 = {"GRAVSIM_SYM_OVERLAP": "3"}  # one local-first launch, remote units gated
     (4, "allgather", "sym", "fp32", 40000, OV3),
     (8, "allgather", "sym", "fp32", 40000, OV3),
     (2, "allgather", "sym", "fp64", 20000, OV3),
-    # (4, "allgather", "sym-graph", ...): capturing the multi-rank step over RCCL's socket
-    # transport segfaulted inside a rank (profiles/r1_rccl_multi_rank_tests.log); graph
-    # capture of the collectives stays opt-in (--graph-comm) and is covered on one rank below.
+    # "sym-graph": capturing the multi-rank step over RCCL's socket transport segfaulted
+    # inside a rank in round 1 (profiles/r1_rccl_multi_rank_tests.log); graph capture of the
+    # collectives stays opt-in (--graph-comm), is covered on one rank below, and the
+    # multi-process case runs only on request (GRAVSIM_TEST_GRAPH_COMM=1).
+    *([(4, "allgather", "sym-graph", "fp32", 20000, None),
+       (4, "allgather", "sym-graph", "fp32", 40000, OV3)]
+      if os.environ.get("GRAVSIM_TEST_GRAPH_COMM") == "1" else []),
 ])
 def test_rccl_multi_rank_match_single_rank(hip, tmp_path, world, strategy, mode, dtype, n, env):
     """P real RCCL ranks (one process each) give the same bits as one rank without a
