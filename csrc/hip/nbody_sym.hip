@@ -534,6 +534,101 @@ __global__ __launch_bounds__(256) void sym_finalize_kernel(SymArgs a) {
   static_cast<V4*>(a.X_next)[gi] = xn;
 }
 
+// One rank, one band: the group reduce, the row reduce and finalize in ONE kernel (no Sbuf /
+// Ti round trip, two launches fewer: at 65K bodies the three took ~28 us plus launch gaps of
+// a 0.73 ms step). The sums keep the exact order of the three-kernel path, so the bits are
+// the same: Ti = sum_q Pd (q ascending) + sum_s Pi (s ascending); S_g = sum of Pj over the
+// rows of group g (ascending, from 0); a = Ti + S_0 + ... + S_7. Block: 3 waves, wave k sums
+// component k of 64 bodies (coalesced partial reads); wave 0 then integrates the 64 bodies.
+template <typename T>
+__global__ __launch_bounds__(192) void sym_tail_kernel(SymArgs a) {
+  using V4 = sym::Vec4<T>;
+  __shared__ T acc_s[3][64];
+  const int k = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int64_t li = (int64_t)blockIdx.x * 64 + l;
+  if (a.gate && blockIdx.x == 0 && threadIdx.x == 0) {
+    __hip_atomic_store(a.gate, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(a.defer, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  const int64_t gi = a.i_begin + li;
+  const bool real = li < a.n_local && gi < a.n_real;
+  if (real) {
+    const int X = (int)(gi / kSymC), c = (int)(gi % kSymC);
+    const int br = X - a.a0;  // one band: band0 = 0, the body's own row
+    // Ti (sym_row_reduce_kernel order)
+    const T* pd = static_cast<const T*>(a.Pd) + (int64_t)br * a.D * 3 * kSymC + k * kSymC + c;
+    T ti = pd[0];
+    for (int q = 1; q < a.D; ++q) ti += pd[q * 3 * kSymC];
+    const int segs = (16 * shell_len(X, a.NC) + a.L - 1) / a.L;
+    const T* pi = static_cast<const T*>(a.Pi) + (int64_t)br * a.S * 3 * kSymC + k * kSymC + c;
+    constexpr int U = 8;
+    int sg = 0;
+    for (; sg + U <= segs; sg += U) {
+      T v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u] = __builtin_nontemporal_load(pi + (int64_t)(sg + u) * 3 * kSymC);
+#pragma unroll
+      for (int u = 0; u < U; ++u) ti += v[u];
+    }
+    for (; sg < segs; ++sg) ti += __builtin_nontemporal_load(pi + (int64_t)sg * 3 * kSymC);
+    // + S_g for g ascending (sym_group_reduce_kernel order, sums from 0; finalize order)
+    const int R = a.NC / kSymGroups;
+    const T* Pj = static_cast<const T*>(a.Pj) + k * kSymC + c;
+    // Rows outside X's shell add +0.0: an identity here, since a sum started at +0.0 never
+    // becomes -0.0, so the loads can be batched 8 at a time like the row reduce (validity is
+    // wave-uniform: the 64 bodies of a wave share their chunk X).
+    for (int g = 0; g < kSymGroups; ++g) {
+      const int hi = min((g + 1) * R, a.real_chunks);
+      T sgv = T(0);
+      for (int A0 = g * R; A0 < hi; A0 += U) {
+        T v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int A = A0 + u;
+          const int d = (X - A + a.NC) % a.NC;
+          const bool ok = A < hi && d != 0 && d <= shell_len(A, a.NC);
+          v[u] = ok ? Pj[((int64_t)(A - a.a0) * a.H + (d - 1)) * 3 * kSymC] : T(0);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) sgv += v[u];
+      }
+      ti += sgv;
+    }
+    acc_s[k][l] = ti;
+  }
+  __syncthreads();
+  if (k != 0 || li >= a.n_local) return;
+  V4* vel = static_cast<V4*>(a.vel);
+  const V4 zero = {T(0), T(0), T(0), T(0)};
+  if (!real) {
+    if (a.acc_out) {
+      static_cast<V4*>(a.acc_out)[li] = zero;
+    } else {
+      vel[li] = zero;
+      static_cast<V4*>(a.X_next)[gi] = zero;
+    }
+    return;
+  }
+  const T ax = acc_s[0][l], ay = acc_s[1][l], az = acc_s[2][l];
+  if (a.acc_out) {
+    static_cast<V4*>(a.acc_out)[li] = V4{ax, ay, az, T(0)};
+    return;
+  }
+  const T dt = (T)a.dt;  // kick-drift exactly as sym_finalize_kernel
+  const V4 xi = static_cast<const V4*>(a.X)[gi];
+  V4 v = vel[li];
+  v.x = v.x + ax * dt;
+  v.y = v.y + ay * dt;
+  v.z = v.z + az * dt;
+  V4 xn;
+  xn.x = xi.x + v.x * dt;
+  xn.y = xi.y + v.y * dt;
+  xn.z = xi.z + v.z * dt;
+  xn.w = xi.w;
+  vel[li] = v;
+  static_cast<V4*>(a.X_next)[gi] = xn;
+}
+
 template <typename T>
 hipError_t launch_force_sym_t(const SymArgs& a, hipStream_t s) {
   int units = a.band_rows * (a.units == 1 ? a.D : (a.units == 2 || a.units == 4) ? a.S
@@ -589,6 +684,14 @@ hipError_t launch_sym_finalize(const SymArgs& a, hipStream_t s) {
   const dim3 grid((unsigned)((a.n_local + 255) / 256));
   if (a.fp64) hipLaunchKernelGGL(sym_finalize_kernel<double>, grid, dim3(256), 0, s, a);
   else hipLaunchKernelGGL(sym_finalize_kernel<float>, grid, dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_sym_tail(const SymArgs& a, hipStream_t s) {
+  if (a.P != 1 || a.band_rows != a.rows) return hipErrorInvalidValue;  // one rank, one band
+  const dim3 grid((unsigned)((a.n_local + 63) / 64));
+  if (a.fp64) hipLaunchKernelGGL(sym_tail_kernel<double>, grid, dim3(192), 0, s, a);
+  else hipLaunchKernelGGL(sym_tail_kernel<float>, grid, dim3(192), 0, s, a);
   return hipGetLastError();
 }
 

@@ -134,6 +134,7 @@ struct gs_stepper {
   int32_t* sym_lf = nullptr;  // units-6 order: unit -> row << 16 | segment (bit 31 remote)
   int gate_probe = 0;         // GRAVSIM_GATE_PROBE (emulation timing probes only)
   int diag_last = 1;          // GRAVSIM_SYM_DIAG_LAST=0: row-by-row unit order (A/B only)
+  int fuse_tail = -1;         // GRAVSIM_SYM_FUSED_TAIL: -1 by size (<= 256K), 0 off, 1 on
   // Phase timing of eager steps (timed): one event set per step, summed by phase_stats.
   struct PhaseEv {
     hipEvent_t t0, end, g0, g1, w0, w1, x0, x1, j0, j1;
@@ -542,6 +543,16 @@ int ring_finish(gs_stepper* s, const gs::KArgs<T>& a) {
 // With `exchange` the RCCL group-sum exchange starts right
 // after the last group reduce and runs beside the last row reduce; the compute stream joins
 // it afterwards.
+// One rank (no exchange, no virtual shards), one band, up to 256K bodies: the group reduce,
+// row reduce and finalize run as one sym_tail_kernel (same bits). Interleaved A/B
+// (profiles/r2_fused_tail_ab.jsonl): 65K 0.707 vs 0.708 ms, 256K 10.51 vs 10.57 ms, but 1M
+// 166.8 vs 166.1 ms, where the fused kernel's 8x fewer threads for the group sums lose.
+// GRAVSIM_SYM_FUSED_TAIL=0 / 1 forces the three-kernel / fused tail at any size.
+bool fused_tail(const gs_stepper* s) {
+  const bool size_ok = s->fuse_tail > 0 || (s->fuse_tail < 0 && s->sym_NC <= 128);
+  return size_ok && s->cfg.nranks == 1 && !multi(s) && s->sym_band >= s->sym_NC;
+}
+
 int sym_force(gs_stepper* s, gs::SymArgs a, bool overlap_gather, bool exchange = false) {
   for (int b0 = 0; b0 < a.rows; b0 += s->sym_band) {
     a.band0 = b0;
@@ -587,6 +598,7 @@ int sym_force(gs_stepper* s, gs::SymArgs a, bool overlap_gather, bool exchange =
       }
       GS_HIP(gs::launch_force_sym(a, s->s_comp));
     }
+    if (fused_tail(s)) continue;  // reductions + integrate in sym_tail_kernel (one band)
     GS_HIP(gs::launch_sym_group_reduce(a, s->s_comp));
     const bool last = b0 + a.band_rows >= a.rows;
     if (exchange && last && sym_exchange_rccl(s, false)) return -1;
@@ -617,7 +629,10 @@ int enqueue_sym(gs_stepper* s, int cur, bool need_gather, bool gathered_external
     if (sym_force(s, a, need_gather, xcomm(s))) return -1;
     if (timed) GS_HIP(hipEventRecord(s->ev_local, s->s_comp));
   }
-  if (part & 2) GS_HIP(gs::launch_sym_finalize(a, s->s_comp));
+  if (part & 2) {
+    if (fused_tail(s)) GS_HIP(gs::launch_sym_tail(a, s->s_comp));
+    else GS_HIP(gs::launch_sym_finalize(a, s->s_comp));
+  }
   return 0;
 }
 
@@ -823,7 +838,8 @@ int accel_impl(gs_stepper* s, double* acc4, bool step_path) {
       sa.acc_out = s->acc;
       if (sym_force(s, sa, false)) return -1;
       if (xcomm(s) && sym_exchange_rccl(s)) return -1;
-      GS_HIP(gs::launch_sym_finalize(sa, s->s_comp));
+      if (fused_tail(s)) GS_HIP(gs::launch_sym_tail(sa, s->s_comp));
+      else GS_HIP(gs::launch_sym_finalize(sa, s->s_comp));
       GS_HIP(hipStreamSynchronize(s->s_comp));
       std::vector<T> A((size_t)s->L.n_local * 4);
       GS_HIP(hipMemcpy(A.data(), s->acc, A.size() * sizeof(T), hipMemcpyDeviceToHost));
@@ -948,6 +964,7 @@ int gs_stepper_create(const gs_config* cfg, gs_stepper** out) {
   if (const char* v = getenv("GRAVSIM_EMU_COMM_WGS")) s->emu_wgs = atoi(v);
   if (const char* v = getenv("GRAVSIM_GATE_PROBE")) s->gate_probe = atoi(v);
   if (const char* v = getenv("GRAVSIM_SYM_DIAG_LAST")) s->diag_last = atoi(v);
+  if (const char* v = getenv("GRAVSIM_SYM_FUSED_TAIL")) s->fuse_tail = atoi(v) != 0 ? 1 : 0;
   const int64_t own_first = s->L.local_begin / s->L.chunk;
   const int64_t own_last = (s->L.local_begin + s->L.n_local) / s->L.chunk;
   s->own_c0 = (int)(own_first < s->L.n_chunks ? own_first : s->L.n_chunks);

@@ -99,6 +99,8 @@ hipError_t launch_gate_set(unsigned* gate, hipStream_t s);
 hipError_t launch_sym_group_reduce(const SymArgs& a, hipStream_t s);  // accumulates into Sbuf
 hipError_t launch_sym_row_reduce(const SymArgs& a, hipStream_t s);    // the band's rows -> Ti
 hipError_t launch_sym_finalize(const SymArgs& a, hipStream_t s);
+// One rank, one band: group reduce + row reduce + finalize in one kernel, same bits.
+hipError_t launch_sym_tail(const SymArgs& a, hipStream_t s);
 int sym_occupancy(int fp64);
 
 template <typename T>

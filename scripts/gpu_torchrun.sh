@@ -24,6 +24,11 @@ timeout -k 10 240 $run --nproc-per-node 2 --master-port 29613 bench.py --gpus 2 
   --warmup 1 --num-bodies 65536 --strategy ring --mode split > $out/bench2_ring.log 2>&1 \
   || { tail -30 $out/bench2_ring.log; exit 1; }
 grep '^{' $out/bench2_ring.log
+# The driver's N=8 shape: bench.py --gpus 8 at the headline N = 1M, 8 ranks sharing this GPU
+# (RCCL over loopback sockets; throughput meaningless, the contract and the path are not).
+timeout -k 10 600 python bench.py --gpus 8 --steps 2 --warmup 1 --n 1048576 > $out/bench8_1m.log 2>&1 \
+  || { tail -30 $out/bench8_1m.log; exit 1; }
+grep '^{' $out/bench8_1m.log
 # CLI: 2 ranks (sym, checkpoint every 3) vs 1 rank, then a 1-rank resume of the 2-rank
 # checkpoint; the three final dumps must be identical text.
 common="--n 40000 --device gpu --mode sym --log-format none --quiet"

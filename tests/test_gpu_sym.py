@@ -202,3 +202,22 @@ def test_sym_bands_bitwise(hip, monkeypatch, P, dtype):
         g.close()
     assert np.array_equal(out[0].pos, out[1].pos)
     assert np.array_equal(out[0].vel, out[1].vel)
+
+
+@pytest.mark.parametrize("n,dtype", [(20000, "fp32"), (65536, "fp32"), (40000, "fp64")])
+def test_sym_fused_tail_bitwise(hip, monkeypatch, n, dtype):
+    """One rank, one band: group reduce + row reduce + finalize fused into sym_tail_kernel
+    keeps every sum's order, so steps and step-path accelerations are bitwise those of the
+    three-kernel tail (GRAVSIM_SYM_FUSED_TAIL=0)."""
+    out = []
+    for fused in ("0", "1"):
+        monkeypatch.setenv("GRAVSIM_SYM_FUSED_TAIL", fused)
+        e = _engine(n, dtype)
+        e.init_ics("solar+random", 13)
+        a = e.accel(step_path=True)
+        e.step(3)
+        out.append((a, e.state()))
+        e.close()
+    assert np.array_equal(out[0][0], out[1][0])
+    assert np.array_equal(out[0][1].pos, out[1][1].pos)
+    assert np.array_equal(out[0][1].vel, out[1][1].vel)
