@@ -165,7 +165,16 @@ def main(argv: Optional[list[str]] = None) -> int:
     raw = list(sys.argv[1:] if argv is None else argv)
     a = build_parser().parse_args(raw)
     if a.nproc > 1 and "WORLD_SIZE" not in os.environ:
+        if a.device != "cpu":
+            import torch  # device_count() does not initialise the GPU on this image
+
+            if a.device == "gpu" or torch.cuda.device_count() > 0:
+                from .parallel import launch
+
+                launch.check_device_count(a.nproc)  # one rank per GPU
         return _launch(a.nproc, raw)
+    if a.nproc > 0 and int(os.environ.get("WORLD_SIZE", "1")) != a.nproc:
+        raise SystemExit(f"--gpus/--nproc {a.nproc} but WORLD_SIZE {os.environ.get('WORLD_SIZE')}")
     cfg = config_from_args(a)
     dist = comm.init()
     from .runtime.simulation import NonFiniteError
