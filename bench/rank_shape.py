@@ -46,6 +46,9 @@ def main() -> int:
     ap.add_argument("--lf-fill", default="",
                     help="comma list of GRAVSIM_SYM_LF_FILL values (local units dispatched first "
                          "by the gated launch; -1 all); empty: built-in default")
+    ap.add_argument("--parity", default="1",
+                    help="comma list of GRAVSIM_SYM_PARITY (1: antipodal pairs split by row "
+                         "parity; 0: round 1's rows-below-NC/2 rule)")
     ap.add_argument("--diag-last", default="1",
                     help="comma list of GRAVSIM_SYM_DIAG_LAST (1: diagonal units dispatched last)")
     ap.add_argument("--gate-probe", default="0",
@@ -67,9 +70,11 @@ def main() -> int:
                                   [float(x) for x in a.comm_gbps.split(",")],
                                   [int(x) for x in a.overlap.split(",")],
                                   [int(x) for x in a.gate_probe.split(",")],
-                                  a.lf_fill.split(","), a.diag_last.split(",")))
-    for P, ipl, kernel, strategy, mode, gbps, ov, gp, fill, dl in grid * a.repeat:
+                                  a.lf_fill.split(","), a.diag_last.split(","),
+                                  a.parity.split(",")))
+    for P, ipl, kernel, strategy, mode, gbps, ov, gp, fill, dl, par in grid * a.repeat:
         os.environ["GRAVSIM_SYM_DIAG_LAST"] = dl
+        os.environ["GRAVSIM_SYM_PARITY"] = par
         os.environ["GRAVSIM_EMU_COMM_GBPS"] = str(gbps)
         os.environ["GRAVSIM_GATE_PROBE"] = str(gp)
         if fill:
@@ -101,7 +106,7 @@ def main() -> int:
         print(json.dumps(dict(P=P, rank=r, n=a.n, dtype=a.dtype, ipl=ipl, kernel=kernel,
                               strategy=strategy, mode=e.native_layout["mode"], comm_gbps=gbps,
                               comm_us=a.comm_us, overlap=ov, gate_probe=gp, lf_fill=fill,
-                              diag_last=int(dl),
+                              diag_last=int(dl), parity=int(par),
                               graph=a.graph,
                               ms_per_step=ms,
                               predicted_efficiency=(b / (P * ms)) if b else None,

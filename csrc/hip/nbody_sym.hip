@@ -89,7 +89,18 @@ struct Geo {
   static_assert(kTileJ <= 128 && 128 % kTileJ == 0, "a j-tile must not straddle quanta");
 };
 
-__device__ __forceinline__ int shell_len(int A, int NC) { return A < NC / 2 ? NC / 2 : NC / 2 - 1; }
+// Row A's shell: the next h(A) chunks cyclically. Distances 1 .. NC/2 - 1 are covered by the
+// row below; each antipodal pair {A, A + NC/2} by exactly one of its rows, chosen by parity
+// (A < NC/2 takes it iff A is even; NC/2 is a multiple of 4, so A + NC/2 has A's parity and
+// takes it iff A is odd). Every block of rows thus holds as many long (NC/2) as short rows,
+// so the ranks of a P-rank run carry equal work (before: ranks 0 .. P/2-1 held every long
+// row, one more unit per row, and the max over ranks paid for it).
+// (antipodal = 0 restores round 1's rule, rows A < NC/2 take every antipodal pair: A/B only,
+// GRAVSIM_SYM_PARITY=0.)
+__device__ __forceinline__ int shell_len(int A, int NC, int antipodal = 1) {
+  const bool takes = antipodal ? (A < NC / 2) == ((A & 1) == 0) : A < NC / 2;
+  return takes ? NC / 2 : NC / 2 - 1;
+}
 
 // A unit's j-tiles, in order: shell tile u of row A is tile u % T of chunk A + 1 + u / T
 // (T tiles per chunk); a diagonal unit's tile u is tile u of chunk A. All-ghost column chunks
@@ -329,7 +340,7 @@ __device__ __forceinline__ void force_sym_body(const SymArgs& a) {
     seq.u = q * seg_tiles;
     seq.u1 = a.D > 1 ? seq.u + seg_tiles : G::kTilesPerChunk;
   } else {
-    const int h_tiles = shell_len(A, a.NC) * G::kTilesPerChunk;
+    const int h_tiles = shell_len(A, a.NC, a.parity) * G::kTilesPerChunk;
     const int u0 = s * seg_tiles;
     if (u0 >= h_tiles) return;  // past this row's shell: never read
     seq.u1 = min(u0 + seg_tiles, h_tiles);
@@ -437,7 +448,7 @@ __global__ __launch_bounds__(256) void sym_group_reduce_kernel(SymArgs a) {
   }
   for (int A = lo; A < hi; ++A) {
     const int d = (X - A + a.NC) % a.NC;
-    if (d == 0 || d > shell_len(A, a.NC)) continue;
+    if (d == 0 || d > shell_len(A, a.NC, a.parity)) continue;
     const T* p = Pj + ((int64_t)(A - a.a0 - a.band0) * a.H + (d - 1)) * 3 * kSymC + c;
     sx += p[0];
     sy += p[kSymC];
@@ -464,7 +475,7 @@ __global__ __launch_bounds__(256) void sym_row_reduce_kernel(SymArgs a) {
                              k * kSymC + c;
   T acc = pd[0];
   for (int q = 1; q < a.D; ++q) acc += pd[q * 3 * kSymC];
-  const int h = shell_len(A, a.NC);
+  const int h = shell_len(A, a.NC, a.parity);
   const int segs = (16 * h + a.L - 1) / a.L;  // shell length in 128-body quanta / L
   const T* __restrict__ p = static_cast<const T*>(a.Pi) + (int64_t)br * a.S * 3 * kSymC +
                             k * kSymC + c;
@@ -559,7 +570,7 @@ __global__ __launch_bounds__(192) void sym_tail_kernel(SymArgs a) {
     const T* pd = static_cast<const T*>(a.Pd) + (int64_t)br * a.D * 3 * kSymC + k * kSymC + c;
     T ti = pd[0];
     for (int q = 1; q < a.D; ++q) ti += pd[q * 3 * kSymC];
-    const int segs = (16 * shell_len(X, a.NC) + a.L - 1) / a.L;
+    const int segs = (16 * shell_len(X, a.NC, a.parity) + a.L - 1) / a.L;
     const T* pi = static_cast<const T*>(a.Pi) + (int64_t)br * a.S * 3 * kSymC + k * kSymC + c;
     constexpr int U = 8;
     int sg = 0;
@@ -586,7 +597,7 @@ __global__ __launch_bounds__(192) void sym_tail_kernel(SymArgs a) {
         for (int u = 0; u < U; ++u) {
           const int A = A0 + u;
           const int d = (X - A + a.NC) % a.NC;
-          const bool ok = A < hi && d != 0 && d <= shell_len(A, a.NC);
+          const bool ok = A < hi && d != 0 && d <= shell_len(A, a.NC, a.parity);
           v[u] = ok ? Pj[((int64_t)(A - a.a0) * a.H + (d - 1)) * 3 * kSymC] : T(0);
         }
 #pragma unroll

@@ -135,6 +135,7 @@ struct gs_stepper {
   int gate_probe = 0;         // GRAVSIM_GATE_PROBE (emulation timing probes only)
   int diag_last = 1;          // GRAVSIM_SYM_DIAG_LAST=0: row-by-row unit order (A/B only)
   int fuse_tail = -1;         // GRAVSIM_SYM_FUSED_TAIL: -1 by size (<= 256K), 0 off, 1 on
+  int parity = 1;             // GRAVSIM_SYM_PARITY=0: round-1 antipodal rule (A/B only)
   // Phase timing of eager steps (timed): one event set per step, summed by phase_stats.
   struct PhaseEv {
     hipEvent_t t0, end, g0, g1, w0, w1, x0, x1, j0, j1;
@@ -301,6 +302,7 @@ gs::SymArgs sym_args(gs_stepper* s, int cur) {
   a.defer_index = 0;
   a.gate_probe = s->emulate ? s->gate_probe : 0;
   a.diag_last = s->diag_last;
+  a.parity = s->parity;
   return a;
 }
 
@@ -343,8 +345,9 @@ int sym_exchange_rccl(gs_stepper* s, bool join = true) {
 // bodies each, 16 quanta per chunk) whose j-chunks A+1 .. all lie in the rank rows
 // [a0, a0 + rows); wrapped chunks count as remote. Mirrors the units 4/5 test of the force
 // kernel (A + 1 + (u1 - 1) / tiles_per_chunk < a0 + rows) in quanta, independent of the tile.
-int sym_local_segs(int A, int NC, int a0, int rows, int L, int S) {
-  const int h = A < NC / 2 ? NC / 2 : NC / 2 - 1;  // shell length in chunks
+int sym_local_segs(int A, int NC, int a0, int rows, int L, int S, int parity) {
+  const bool takes = parity ? (A < NC / 2) == ((A & 1) == 0) : A < NC / 2;  // nbody_sym.hip
+  const int h = takes ? NC / 2 : NC / 2 - 1;
   const int segs = (16 * h + L - 1) / L;
   const int own_after = a0 + rows - 1 - A;
   int n;
@@ -965,6 +968,7 @@ int gs_stepper_create(const gs_config* cfg, gs_stepper** out) {
   if (const char* v = getenv("GRAVSIM_GATE_PROBE")) s->gate_probe = atoi(v);
   if (const char* v = getenv("GRAVSIM_SYM_DIAG_LAST")) s->diag_last = atoi(v);
   if (const char* v = getenv("GRAVSIM_SYM_FUSED_TAIL")) s->fuse_tail = atoi(v) != 0 ? 1 : 0;
+  if (const char* v = getenv("GRAVSIM_SYM_PARITY")) s->parity = atoi(v) != 0 ? 1 : 0;
   const int64_t own_first = s->L.local_begin / s->L.chunk;
   const int64_t own_last = (s->L.local_begin + s->L.n_local) / s->L.chunk;
   s->own_c0 = (int)(own_first < s->L.n_chunks ? own_first : s->L.n_chunks);
@@ -1049,7 +1053,7 @@ int gs_stepper_create(const gs_config* cfg, gs_stepper** out) {
     std::vector<char> moved((size_t)rows * (s->sym_S_n + s->sym_D), 0);
     const int per = s->sym_S_n + s->sym_D;
     for (int r = 0; r < rows && lf.capacity(); ++r) {
-      nl[r] = sym_local_segs(a0 + r, s->sym_NC, a0, rows, s->sym_L, s->sym_S_n);
+      nl[r] = sym_local_segs(a0 + r, s->sym_NC, a0, rows, s->sym_L, s->sym_S_n, s->parity);
       for (int q = 0; q < s->sym_D && (fill < 0 || (long)lf.size() < fill); ++q) {
         lf.push_back((r << 16) | (s->sym_S_n + q));
         moved[(size_t)r * per + s->sym_S_n + q] = 1;

@@ -39,7 +39,8 @@ inline int split_span(const KArgs<T>& a) {
 // Canonical decomposition, a function of the padded body count only (so every rank count
 // P | 8 produces the same bits): chunks of kSymC = 2048 bodies, NC = n_pad / 2048 of them,
 // G = 8 row groups of NC / 8 chunks. Chunk A pairs with the next h(A) chunks cyclically
-// (h = NC/2 for A < NC/2, NC/2 - 1 above: every unordered chunk pair exactly once) and with
+// (h = NC/2 - 1, plus the antipodal chunk A + NC/2 for half of the rows, alternating by
+// parity: every unordered chunk pair exactly once, equal work per block of rows) and with
 // itself (one-sided). Row A's shell is cut into segments of L quanta (128 bodies; see
 // gs_sym_geometry), its diagonal chunk into D parts; one workgroup per unit writes an i-side
 // partial (Pi[row][segment] or Pd[row][part]) and, for every shell tile it visits, the
@@ -89,6 +90,7 @@ struct SymArgs {
   int32_t defer_index;  // (device-side) the deferred entry a units-7 workgroup is running
   int32_t gate_probe;   // timing probe of the emulation only (GRAVSIM_GATE_PROBE): 0 acquire
   int32_t diag_last;    // units 0: shell segments first, diagonal parts last (else row by row)
+  int32_t parity;       // antipodal chunk pairs split between rows by parity (else A < NC/2)
 };
 
 hipError_t launch_force_sym(const SymArgs& a, hipStream_t s);
