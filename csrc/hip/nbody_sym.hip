@@ -446,13 +446,29 @@ __global__ __launch_bounds__(256) void sym_group_reduce_kernel(SymArgs a) {
     sy = o[a.n_local];
     sz = o[2 * a.n_local];
   }
-  for (int A = lo; A < hi; ++A) {
-    const int d = (X - A + a.NC) % a.NC;
-    if (d == 0 || d > shell_len(A, a.NC, a.parity)) continue;
-    const T* p = Pj + ((int64_t)(A - a.a0 - a.band0) * a.H + (d - 1)) * 3 * kSymC + c;
-    sx += p[0];
-    sy += p[kSymC];
-    sz += p[2 * kSymC];
+  // 4 rows' loads in flight, added in row order; rows outside X's shell add +0.0, an
+  // identity here (a sum started at +0.0 never becomes -0.0). Validity is wave-uniform.
+  constexpr int U = 4;
+  for (int A0 = lo; A0 < hi; A0 += U) {
+    T vx[U], vy[U], vz[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int A = A0 + u;
+      const int d = (X - A + a.NC) % a.NC;
+      vx[u] = vy[u] = vz[u] = T(0);
+      if (A < hi && d != 0 && d <= shell_len(A, a.NC, a.parity)) {
+        const T* p = Pj + ((int64_t)(A - a.a0 - a.band0) * a.H + (d - 1)) * 3 * kSymC + c;
+        vx[u] = p[0];
+        vy[u] = p[kSymC];
+        vz[u] = p[2 * kSymC];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      sx += vx[u];
+      sy += vy[u];
+      sz += vz[u];
+    }
   }
   o[0] = sx;
   o[a.n_local] = sy;
