@@ -5,6 +5,7 @@
 // ghost bodies (mu = 0, at the origin) to a multiple of P * chunk, so every rank owns an
 // equal contiguous slice (RCCL all-gather needs equal counts) and the j-chunk boundaries,
 // hence the floating-point summation order, do not depend on P.
+#include <vector>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -144,6 +145,73 @@ extern "C" int gs_sym_geometry(int64_t n_pad, int32_t* NC, int32_t* H, int32_t* 
   if (S) *S = (16 * h + l - 1) / l;
   if (D) *D = l < 16 ? 16 / l : 1;
   return 0;
+}
+
+// Chunk rows of the sym schedule: row A pairs with the next h(A) chunks cyclically. Distances
+// 1 .. NC/2 - 1 belong to the row below; each antipodal pair {A, A + NC/2} to one of its two
+// rows, by parity (A < NC/2 takes it iff A is even; NC/2 is a multiple of 4, so A + NC/2 has
+// A's parity and takes it iff A is odd), so any block of rows holds as many long rows as
+// short ones. parity = 0: round 1's rule (rows A < NC/2 take every antipodal pair). Mirrors
+// shell_len() in nbody_sym.hip.
+extern "C" int32_t gs_sym_shell_len(int32_t A, int32_t NC, int32_t parity) {
+  const bool takes = parity ? (A < NC / 2) == ((A & 1) == 0) : A < NC / 2;
+  return takes ? NC / 2 : NC / 2 - 1;
+}
+
+// Rank-local shell segments of row A: the prefix of the row's segments (L quanta of 128 bodies,
+// 16 quanta per chunk) whose j-chunks A+1 .. all lie in the rank rows [a0, a0 + rows); wrapped
+// chunks count as remote. The force kernel's units 4/5 test in quanta.
+static int32_t sym_local_segs(int32_t A, int32_t NC, int32_t a0, int32_t rows, int32_t L,
+                              int32_t S, int32_t parity) {
+  const int32_t h = gs_sym_shell_len(A, NC, parity);
+  const int32_t segs = (16 * h + L - 1) / L;
+  const int32_t own_after = a0 + rows - 1 - A;
+  int32_t n;
+  if (own_after <= 0) n = 0;
+  else if (h <= own_after) n = segs;
+  else n = segs < own_after * 16 / L ? segs : own_after * 16 / L;
+  return n < S ? n : S;
+}
+
+// The gated sym launch's unit order (units 6, gs_kernels.h) for rank `rank` of `nranks`, one
+// band: entry = row << 16 | unit (unit < S: shell segment, >= S: diagonal part), bit 31 set
+// for a remote unit (a j-chunk outside the rank's rows). The first `fill` entries (all local
+// units when fill < 0) are rank-local ones, row by row (diagonal parts, then local
+// segments); the rest follow the ungated order: shell segments row by row, then the diagonal
+// parts. Returns the entry count (rows * (S + D)), 0 if the 16-bit fields cannot hold the
+// geometry, -1 on error (cap too small, bad arguments).
+extern "C" int64_t gs_sym_unit_map(int64_t n_pad, int32_t rank, int32_t nranks, int32_t parity,
+                                   int64_t fill, int32_t* out, int64_t cap) {
+  int32_t NC, H, L, S, D;
+  if (nranks < 1 || rank < 0 || rank >= nranks || gs_sym_geometry(n_pad, &NC, &H, &L, &S, &D))
+    return -1;
+  if (NC % nranks) return -1;
+  const int32_t rows = NC / nranks, per = S + D, a0 = rank * rows;
+  const int64_t total = (int64_t)rows * per;
+  if (rows >= 32768 || per >= 65536) return 0;
+  if (!out || cap < total) return -1;
+  std::vector<int32_t> nl(rows);
+  std::vector<char> moved((size_t)total, 0);
+  int64_t k = 0;
+  for (int32_t r = 0; r < rows; ++r) {
+    nl[r] = sym_local_segs(a0 + r, NC, a0, rows, L, S, parity);
+    for (int32_t q = 0; q < D && (fill < 0 || k < fill); ++q) {
+      out[k++] = (r << 16) | (S + q);
+      moved[(size_t)r * per + S + q] = 1;
+    }
+    for (int32_t g = 0; g < nl[r] && (fill < 0 || k < fill); ++g) {
+      out[k++] = (r << 16) | g;
+      moved[(size_t)r * per + g] = 1;
+    }
+  }
+  for (int pass = 0; pass < 2; ++pass)
+    for (int32_t r = 0; r < rows; ++r)
+      for (int32_t u = pass ? S : 0; u < (pass ? per : S); ++u) {
+        if (moved[(size_t)r * per + u]) continue;
+        const bool remote = u < S && u >= nl[r];
+        out[k++] = (int32_t)((remote ? 0x80000000u : 0u) | ((uint32_t)r << 16) | (uint32_t)u);
+      }
+  return k;
 }
 
 // Partial-slot bytes per rank if all of the rank's rows were held at once (one band).

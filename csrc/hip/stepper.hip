@@ -341,22 +341,6 @@ int sym_exchange_rccl(gs_stepper* s, bool join = true) {
   return 0;
 }
 
-// Rank-local shell segments of row A: the prefix of the row's S segments (L quanta of 128
-// bodies each, 16 quanta per chunk) whose j-chunks A+1 .. all lie in the rank rows
-// [a0, a0 + rows); wrapped chunks count as remote. Mirrors the units 4/5 test of the force
-// kernel (A + 1 + (u1 - 1) / tiles_per_chunk < a0 + rows) in quanta, independent of the tile.
-int sym_local_segs(int A, int NC, int a0, int rows, int L, int S, int parity) {
-  const bool takes = parity ? (A < NC / 2) == ((A & 1) == 0) : A < NC / 2;  // nbody_sym.hip
-  const int h = takes ? NC / 2 : NC / 2 - 1;
-  const int segs = (16 * h + L - 1) / L;
-  const int own_after = a0 + rows - 1 - A;
-  int n;
-  if (own_after <= 0) n = 0;
-  else if (h <= own_after) n = segs;
-  else n = segs < own_after * 16 / L ? segs : own_after * 16 / L;
-  return n < S ? n : S;
-}
-
 int ensure_sym(gs_stepper* s) {
   if (s->L.mode != GS_MODE_SYM || s->sym_Pi) return 0;
   if (gs_sym_geometry(s->L.n_pad, &s->sym_NC, &s->sym_H, &s->sym_L, &s->sym_S_n, &s->sym_D))
@@ -1040,39 +1024,13 @@ int gs_stepper_create(const gs_config* cfg, gs_stepper** out) {
     const size_t units = (size_t)rows * (s->sym_S_n + s->sym_D) + 1;
     FAIL_CLEAN(hipMalloc(&s->defer, units * sizeof(unsigned)));
     FAIL_CLEAN(hipMemsetAsync(s->defer, 0, units * sizeof(unsigned), s->s_comp));
-    // unit -> row << 16 | segment (bit 31: remote), local units first (gs_kernels.h)
-    // Only the first `fill` units need to be local: enough to keep the GPU busy while the
-    // gather runs (default two dispatch waves, 4 workgroups per CU; GRAVSIM_SYM_LF_FILL, -1:
-    // every local unit first). The rest keep the row-major order of the ungated launch.
-    std::vector<int32_t> lf;
-    if (rows < 32768 && s->sym_S_n + s->sym_D < 65536) lf.reserve(units);  // else: no map
-    const int a0 = cfg->rank * rows;
-    long fill = 4L * s->cus;
+    // unit -> row << 16 | segment (bit 31: remote), local units first (layout.cpp).
+    long fill = 4L * s->cus;  // two dispatch waves of 2 workgroups per CU
     if (const char* v = getenv("GRAVSIM_SYM_LF_FILL")) fill = atol(v);
-    std::vector<int> nl(rows);
-    std::vector<char> moved((size_t)rows * (s->sym_S_n + s->sym_D), 0);
-    const int per = s->sym_S_n + s->sym_D;
-    for (int r = 0; r < rows && lf.capacity(); ++r) {
-      nl[r] = sym_local_segs(a0 + r, s->sym_NC, a0, rows, s->sym_L, s->sym_S_n, s->parity);
-      for (int q = 0; q < s->sym_D && (fill < 0 || (long)lf.size() < fill); ++q) {
-        lf.push_back((r << 16) | (s->sym_S_n + q));
-        moved[(size_t)r * per + s->sym_S_n + q] = 1;
-      }
-      for (int g = 0; g < nl[r] && (fill < 0 || (long)lf.size() < fill); ++g) {
-        lf.push_back((r << 16) | g);
-        moved[(size_t)r * per + g] = 1;
-      }
-    }
-    // The ungated launch's order for the rest: shell segments row by row, then the diagonal
-    // parts (dispatched last, they fill the final partial wave).
-    for (int pass = 0; pass < 2 && lf.capacity(); ++pass)
-      for (int r = 0; r < rows; ++r)
-        for (int u = pass ? s->sym_S_n : 0; u < (pass ? per : s->sym_S_n); ++u) {
-          if (moved[(size_t)r * per + u]) continue;
-          const bool remote = u < s->sym_S_n && u >= nl[r];
-          lf.push_back(
-              (int32_t)((remote ? 0x80000000u : 0u) | ((uint32_t)r << 16) | (uint32_t)u));
-        }
+    std::vector<int32_t> lf(units - 1);
+    const int64_t got = gs_sym_unit_map(s->L.n_pad, cfg->rank, cfg->nranks, s->parity, fill,
+                                        lf.data(), (int64_t)lf.size());
+    lf.resize(got > 0 ? (size_t)got : 0);  // 0: geometry too large for the 16-bit fields
     if (!lf.empty()) {
       FAIL_CLEAN(hipMalloc(&s->sym_lf, lf.size() * sizeof(int32_t)));
       FAIL_CLEAN(hipMemcpy(s->sym_lf, lf.data(), lf.size() * sizeof(int32_t),

@@ -93,6 +93,11 @@ int32_t gs_auto_chunk(int64_t n);
 int gs_sym_geometry(int64_t n_pad, int32_t* NC, int32_t* H, int32_t* L, int32_t* S,
                     int32_t* D);
 int64_t gs_sym_bytes(int64_t n_pad, int32_t nranks, int32_t esz);
+// Shell length of chunk row A (antipodal pairs split by parity; parity 0: rows A < NC/2).
+int32_t gs_sym_shell_len(int32_t A, int32_t NC, int32_t parity);
+// Unit order of the gated sym launch for one rank (see layout.cpp); returns the entry count.
+int64_t gs_sym_unit_map(int64_t n_pad, int32_t rank, int32_t nranks, int32_t parity,
+                        int64_t fill, int32_t* out, int64_t cap);
 
 // ---------------------------------------------------------------- counter-based RNG / ICs (host)
 // Fill bodies [begin, end) of the IC family into fp64 arrays (pos/vel: 3 per body, mass: 1).
