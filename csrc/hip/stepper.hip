@@ -33,7 +33,10 @@
 // The partial slots and summation order depend on N only, so every P dividing 8 gives the
 // same bits.
 #include <dlfcn.h>
+#include <execinfo.h>
 #include <hip/hip_runtime.h>
+#include <signal.h>
+#include <unistd.h>
 #include <math.h>
 #include <rccl/rccl.h>
 #include <stdio.h>
@@ -1419,7 +1422,39 @@ int gs_rccl_unique_id(void* out128) {
   return 0;
 }
 
+}  // extern "C"
+
+namespace {
+// GRAVSIM_CRASH_TRACE=1: a fatal signal in any thread of a rank (ours, HIP's or RCCL's
+// proxy/socket threads) prints that thread's native stack to stderr before the default
+// action runs. Host-side diagnosis only; it was added to locate the multi-process
+// graph-capture crash over RCCL sockets (profiles/r2_graph_comm_multiprocess.txt).
+void crash_trace_handler(int sig) {
+  void* frames[64];
+  const int n = backtrace(frames, 64);
+  char head[96];
+  const int len = snprintf(head, sizeof(head), "gravsim: signal %d in pid %d, native stack:\n",
+                           sig, (int)getpid());
+  if (len > 0) (void)!write(2, head, (size_t)len);
+  backtrace_symbols_fd(frames, n, 2);
+  signal(sig, SIG_DFL);
+  raise(sig);
+}
+
+void maybe_install_crash_trace() {
+  static bool done = false;
+  if (done || !getenv("GRAVSIM_CRASH_TRACE")) return;
+  done = true;
+  void* warm[1];
+  (void)backtrace(warm, 1);  // loads libgcc's unwinder now, not inside the handler
+  for (int sig : {SIGSEGV, SIGBUS, SIGFPE, SIGILL, SIGABRT}) signal(sig, crash_trace_handler);
+}
+}  // namespace
+
+extern "C" {
+
 int gs_stepper_comm_init(gs_stepper* s, const void* id128, int32_t rank, int32_t nranks) {
+  maybe_install_crash_trace();
   if (rank != s->cfg.rank || nranks != s->cfg.nranks) {
     gs_set_error("comm_init: rank/nranks differ from the stepper's layout");
     return -1;
