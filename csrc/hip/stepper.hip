@@ -1429,15 +1429,30 @@ namespace {
 // proxy/socket threads) prints that thread's native stack to stderr before the default
 // action runs. Host-side diagnosis only; it was added to locate the multi-process
 // graph-capture crash over RCCL sockets (profiles/r2_graph_comm_multiprocess.txt).
-void crash_trace_handler(int sig) {
-  void* frames[64];
-  const int n = backtrace(frames, 64);
-  char head[96];
-  const int len = snprintf(head, sizeof(head), "gravsim: signal %d in pid %d, native stack:\n",
-                           sig, (int)getpid());
+constexpr int kTraceSigs[] = {SIGSEGV, SIGBUS, SIGFPE, SIGILL, SIGABRT};
+struct sigaction g_prev_action[sizeof(kTraceSigs) / sizeof(int)];
+
+void crash_trace_handler(int sig, siginfo_t* info, void*) {
+  char head[160];
+  const int len = snprintf(head, sizeof(head),
+                           "gravsim: signal %d (addr %p) in pid %d tid %ld, native stack:\n", sig,
+                           info ? info->si_addr : nullptr, (int)getpid(), (long)gettid());
   if (len > 0) (void)!write(2, head, (size_t)len);
-  backtrace_symbols_fd(frames, n, 2);
-  signal(sig, SIG_DFL);
+  // Deep enough for a runaway recursion: print the innermost 8 and the outermost 40 frames.
+  static void* frames[1 << 18];
+  const int n = backtrace(frames, 1 << 18);
+  if (n <= 48) {
+    backtrace_symbols_fd(frames, n, 2);
+  } else {
+    backtrace_symbols_fd(frames, 8, 2);
+    const int skipped = snprintf(head, sizeof(head), "  ... %d frames ...\n", n - 48);
+    if (skipped > 0) (void)!write(2, head, (size_t)skipped);
+    backtrace_symbols_fd(frames + n - 40, 40, 2);
+  }
+  // Chain to whatever was installed before (Python's faulthandler prints every thread's
+  // Python stack), then the default action.
+  for (size_t k = 0; k < sizeof(kTraceSigs) / sizeof(int); ++k)
+    if (kTraceSigs[k] == sig) sigaction(sig, &g_prev_action[k], nullptr);
   raise(sig);
 }
 
@@ -1447,7 +1462,20 @@ void maybe_install_crash_trace() {
   done = true;
   void* warm[1];
   (void)backtrace(warm, 1);  // loads libgcc's unwinder now, not inside the handler
-  for (int sig : {SIGSEGV, SIGBUS, SIGFPE, SIGILL, SIGABRT}) signal(sig, crash_trace_handler);
+  struct sigaction sa;
+  memset(&sa, 0, sizeof(sa));
+  sa.sa_sigaction = crash_trace_handler;
+  sa.sa_flags = SA_SIGINFO | SA_RESETHAND | SA_ONSTACK;
+  // An alternate stack for this (the host's main) thread, so a stack overflow still reports.
+  static char alt[1 << 16];
+  stack_t ss;
+  memset(&ss, 0, sizeof(ss));
+  ss.ss_sp = alt;
+  ss.ss_size = sizeof(alt);
+  (void)sigaltstack(&ss, nullptr);
+  sigemptyset(&sa.sa_mask);
+  for (size_t k = 0; k < sizeof(kTraceSigs) / sizeof(int); ++k)
+    sigaction(kTraceSigs[k], &sa, &g_prev_action[k]);
 }
 }  // namespace
 
