@@ -273,7 +273,7 @@ __device__ __forceinline__ bool local_first_unit(const SymArgs& a, int b, int* b
 // collective's writes); otherwise append the unit to the deferred list and leave. No
 // workgroup ever waits on the collective, so RCCL's kernels always find CUs; the deferred
 // units run in a second launch (units 7) queued behind the gather event.
-__device__ __forceinline__ bool gate_open_or_defer(const SymArgs& a) {
+__device__ __forceinline__ bool gate_open_or_defer(const SymArgs& a, int b) {
   __shared__ int open_s;
   if (threadIdx.x == 0) {
     // (gate_probe: timing probes only, per-rank emulation: 1 skips the check, 2 loads relaxed)
@@ -284,7 +284,7 @@ __device__ __forceinline__ bool gate_open_or_defer(const SymArgs& a) {
     if (!open) {
       const unsigned k =
           __hip_atomic_fetch_add(a.defer, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      a.defer[1 + k] = blockIdx.x;
+      a.defer[1 + k] = (unsigned)b;
     }
     open_s = open ? 1 : 0;
   }
@@ -292,9 +292,10 @@ __device__ __forceinline__ bool gate_open_or_defer(const SymArgs& a) {
   return open_s != 0;
 }
 
-// One workgroup per unit (row a, segment s); s == S is the row's diagonal chunk.
+// One unit b (row a, segment s) per call; s == S is the row's diagonal chunk. b is the
+// workgroup index, or the index the workgroup fetched (SymArgs.work).
 template <typename T, bool EXACT>
-__device__ __forceinline__ void force_sym_body(const SymArgs& a) {
+__device__ __forceinline__ void force_sym_body(const SymArgs& a, int b) {
   using G = Geo<T>;
   using V4 = sym::Vec4<T>;
   __shared__ Smem<T> sm;
@@ -304,31 +305,31 @@ __device__ __forceinline__ void force_sym_body(const SymArgs& a) {
   int br, s;
   bool gated = false;
   if (a.units == 6) {
-    gated = local_first_unit(a, blockIdx.x, &br, &s) && a.gate != nullptr;
+    gated = local_first_unit(a, b, &br, &s) && a.gate != nullptr;
   } else if (a.units == 7) {  // deferred unit a.defer_index of the units-6 launch
     local_first_unit(a, (int)a.defer[1 + a.defer_index], &br, &s);
   } else if (a.units == 1) {
-    br = blockIdx.x / a.D;
-    s = a.S + blockIdx.x % a.D;
+    br = b / a.D;
+    s = a.S + b % a.D;
   } else if (a.units == 2 || a.units == 4) {  // shell units: all (2) or the non-local ones (4)
-    br = blockIdx.x / a.S;
-    s = blockIdx.x % a.S;
+    br = b / a.S;
+    s = b % a.S;
   } else if (a.units == 0 && a.diag_last) {
     // Every unit: the shell segments row by row, then all diagonal parts. A diagonal part is
     // one-sided (about half the issue time of a shell segment), so dispatching them last fills
     // the launch's final, partial wave of workgroups with short jobs.
     const int shell = a.band_rows * a.S;
-    if ((int)blockIdx.x < shell) {
-      br = blockIdx.x / a.S;
-      s = blockIdx.x % a.S;
+    if (b < shell) {
+      br = b / a.S;
+      s = b % a.S;
     } else {
-      const int k = blockIdx.x - shell;
+      const int k = b - shell;
       br = k / a.D;
       s = a.S + k % a.D;
     }
   } else {  // the diagonal ones + the rank-local shell ones (5), or every unit row by row
-    br = blockIdx.x / (a.S + a.D);
-    s = blockIdx.x % (a.S + a.D);
+    br = b / (a.S + a.D);
+    s = b % (a.S + a.D);
   }
   const int A = a.a0 + a.band0 + br;
   if ((int64_t)A * kSymC >= a.n_real) return;  // all-ghost row: never read
@@ -352,7 +353,8 @@ __device__ __forceinline__ void force_sym_body(const SymArgs& a) {
     }
     seq.u = seq.valid(u0);
   }
-  if (gated && !gate_open_or_defer(a)) return;
+  if (gated && !gate_open_or_defer(a, b)) return;
+  const unsigned long long t_start = a.utrace ? __builtin_amdgcn_s_memrealtime() : 0ull;
   const V4* X4 = static_cast<const V4*>(a.X);
   ISetK<T> is;
   const int64_t i_row0 = (int64_t)A * kSymC + w * G::kTileI;
@@ -385,35 +387,75 @@ __device__ __forceinline__ void force_sym_body(const SymArgs& a) {
       out[2 * kSymC + b] = is.az[i];
     }
   }
+  if (a.utrace && threadIdx.x == 0) {
+    // hwreg(HW_ID) whole register, hwreg(XCC_ID) bits 3:0 (ids 4 and 20 on gfx9.4+)
+    const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+    const unsigned xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20);
+    const int64_t slot = a.units == 7 ? (int64_t)a.trace_defer0 + a.defer_index : b;
+    unsigned long long* e = a.utrace + 4 * slot;
+    e[0] = t_start;
+    e[1] = __builtin_amdgcn_s_memrealtime();
+    e[2] = (unsigned long long)hw | ((unsigned long long)xcc << 32);
+    e[3] = ((unsigned long long)(unsigned)br << 32) | (unsigned)s;
+  }
 }
 
 // units 7 runs a separate instantiation (DEFER): a small grid that walks the deferred list
 // with a stride of the grid. The list is usually empty (the gather finished long before the
 // remote units were dispatched), and a grid of one workgroup per possible unit would cost more
 // than the gather it hides. The main kernel is unchanged by it (same registers, no spills).
-template <typename T, bool EXACT, bool DEFER>
+template <typename T, bool EXACT, bool DEFER, bool DYN>
 __device__ __forceinline__ void force_sym_entry(SymArgs a) {
-  if constexpr (!DEFER) {
-    force_sym_body<T, EXACT>(a);
+  if constexpr (!DEFER && !DYN) {
+    force_sym_body<T, EXACT>(a, blockIdx.x);
+  } else if constexpr (DYN) {
+    // Dynamic fetch: unit indices in launch order from a device counter. The hardware hands
+    // workgroups to the 8 XCDs in a fixed rotation, so a static unit per workgroup gives every
+    // XCD the same number of units, and the slowest XCD (they differ by up to ~4 % in
+    // throughput, bench/unit_timeline.py) sets the launch's end. Here a workgroup keeps taking
+    // units (up to unit_cap; the first wave one each, so slots free up early for a concurrent
+    // collective), and faster XCDs simply take more. Same units, same slots: same bits.
+    __shared__ unsigned next_s;
+    const int cap = (int)blockIdx.x < a.first_wave ? 1 : a.unit_cap;
+    for (int k = 0; k < cap; ++k) {
+      if (threadIdx.x == 0)
+        next_s = __hip_atomic_fetch_add(a.work, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __syncthreads();
+      const unsigned u = next_s;
+      if (u >= (unsigned)a.n_units) break;
+      force_sym_body<T, EXACT>(a, (int)u);
+      __syncthreads();  // next_s and the LDS tiles are rewritten by the next unit
+    }
+    if (threadIdx.x == 0) {
+      // The last workgroup out re-arms the counters (every other one has finished fetching:
+      // its fetches precede its exit count, acq_rel).
+      const unsigned e =
+          __hip_atomic_fetch_add(a.work + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+      if (e == gridDim.x - 1) {
+        __hip_atomic_store(a.work, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(a.work + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
   } else {
     const unsigned n = a.defer[0];
     if (blockIdx.x == 0 && threadIdx.x == 0 && n > 0)
       __hip_atomic_fetch_max(a.defer_max, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     for (unsigned k = blockIdx.x; k < n; k += gridDim.x) {
       a.defer_index = (int32_t)k;
-      force_sym_body<T, EXACT>(a);
+      force_sym_body<T, EXACT>(a, 0);
       __syncthreads();  // the next unit reuses the LDS tiles
     }
   }
 }
 
-template <bool EXACT, bool DEFER = false>
+// (separate instantiations: the static kernels keep their own register allocation)
+template <bool EXACT, bool DEFER = false, bool DYN = false>
 __global__ __launch_bounds__(Geo<float>::kThreads) GS_SYM_WPE32 void force_sym_kernel_f32(SymArgs a) {
-  force_sym_entry<float, EXACT, DEFER>(a);
+  force_sym_entry<float, EXACT, DEFER, DYN>(a);
 }
-template <bool EXACT, bool DEFER = false>
+template <bool EXACT, bool DEFER = false, bool DYN = false>
 __global__ __launch_bounds__(Geo<double>::kThreads) GS_SYM_WPE64 void force_sym_kernel_f64(SymArgs a) {
-  force_sym_entry<double, EXACT, DEFER>(a);
+  force_sym_entry<double, EXACT, DEFER, DYN>(a);
 }
 
 // S_g(x) for this rank's groups and every body x of a real chunk: rows A of group g in
@@ -663,23 +705,39 @@ hipError_t launch_force_sym_t(const SymArgs& a, hipStream_t s) {
   if (a.units >= 6 && (a.band_rows != a.rows || !a.lf)) return hipErrorInvalidValue;
   if (a.units == 7) units = a.defer_grid;  // strided walk over the deferred list
   if (units <= 0) return hipSuccess;
-  const dim3 grid(units), block(Geo<T>::kThreads);
-  const bool d = a.units == 7;
+  SymArgs b = a;
+  b.n_units = units;
+  unsigned g = (unsigned)units;
+  if (a.work && (a.units == 0 || a.units == 6) && a.unit_cap > 1 && units > a.first_wave) {
+    // first wave: one unit per workgroup; the rest: up to unit_cap each, with 25 % slack so
+    // a fast XCD can take more than its rotation share
+    const int64_t rest = units - a.first_wave;
+    const int64_t more = (5 * rest + 4LL * a.unit_cap - 1) / (4LL * a.unit_cap);
+    g = (unsigned)(a.first_wave + (more < rest ? more : rest));
+  } else {
+    b.work = nullptr;  // static: unit = blockIdx.x
+  }
+  const dim3 grid(g), block(Geo<T>::kThreads);
+  const bool d = a.units == 7, y = b.work != nullptr;
   if constexpr (sizeof(T) == 8) {
     if (a.exact) {
-      if (d) hipLaunchKernelGGL((force_sym_kernel_f64<true, true>), grid, block, 0, s, a);
-      else hipLaunchKernelGGL((force_sym_kernel_f64<true>), grid, block, 0, s, a);
+      if (d) hipLaunchKernelGGL((force_sym_kernel_f64<true, true>), grid, block, 0, s, b);
+      else if (y) hipLaunchKernelGGL((force_sym_kernel_f64<true, false, true>), grid, block, 0, s, b);
+      else hipLaunchKernelGGL((force_sym_kernel_f64<true>), grid, block, 0, s, b);
     } else {
-      if (d) hipLaunchKernelGGL((force_sym_kernel_f64<false, true>), grid, block, 0, s, a);
-      else hipLaunchKernelGGL((force_sym_kernel_f64<false>), grid, block, 0, s, a);
+      if (d) hipLaunchKernelGGL((force_sym_kernel_f64<false, true>), grid, block, 0, s, b);
+      else if (y) hipLaunchKernelGGL((force_sym_kernel_f64<false, false, true>), grid, block, 0, s, b);
+      else hipLaunchKernelGGL((force_sym_kernel_f64<false>), grid, block, 0, s, b);
     }
   } else {
     if (a.exact) {
-      if (d) hipLaunchKernelGGL((force_sym_kernel_f32<true, true>), grid, block, 0, s, a);
-      else hipLaunchKernelGGL((force_sym_kernel_f32<true>), grid, block, 0, s, a);
+      if (d) hipLaunchKernelGGL((force_sym_kernel_f32<true, true>), grid, block, 0, s, b);
+      else if (y) hipLaunchKernelGGL((force_sym_kernel_f32<true, false, true>), grid, block, 0, s, b);
+      else hipLaunchKernelGGL((force_sym_kernel_f32<true>), grid, block, 0, s, b);
     } else {
-      if (d) hipLaunchKernelGGL((force_sym_kernel_f32<false, true>), grid, block, 0, s, a);
-      else hipLaunchKernelGGL((force_sym_kernel_f32<false>), grid, block, 0, s, a);
+      if (d) hipLaunchKernelGGL((force_sym_kernel_f32<false, true>), grid, block, 0, s, b);
+      else if (y) hipLaunchKernelGGL((force_sym_kernel_f32<false, false, true>), grid, block, 0, s, b);
+      else hipLaunchKernelGGL((force_sym_kernel_f32<false>), grid, block, 0, s, b);
     }
   }
   return hipGetLastError();

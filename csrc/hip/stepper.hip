@@ -128,6 +128,12 @@ struct gs_stepper {
   double emu_gbps = 0.0, emu_lat_us = 15.0;
   int emu_wgs = 16;
   void* emu_buf = nullptr;
+  unsigned long long* utrace = nullptr;  // GRAVSIM_UNIT_TRACE: per force workgroup timeline
+  // Dynamic unit fetch of the sym force launch (GRAVSIM_SYM_DYN_CAP; <= 1: static units):
+  // units per workgroup after the first wave, and the first wave's size (resident slots).
+  int dyn_cap = 4;
+  int sym_first_wave = 0;
+  int64_t utrace_main = 0;               // entries of the main launch (deferred ones follow)
   size_t emu_cap = 0;
   double clk_khz = 100000.0;  // device wall clock (wall_clock64) rate
   // Gather gates (sym_overlap 3): [0], [1] gate of X[0] / X[1]; [3] the most units one step
@@ -304,6 +310,13 @@ gs::SymArgs sym_args(gs_stepper* s, int cur) {
   a.defer_grid = 2 * s->cus;  // resident force workgroups: 2 per CU
   a.defer_index = 0;
   a.gate_probe = s->emulate ? s->gate_probe : 0;
+  a.utrace = s->utrace;
+  if (s->dyn_cap > 1) {
+    a.work = s->gate_buf + 4;
+    a.unit_cap = s->dyn_cap;
+    a.first_wave = s->sym_first_wave;
+  }
+  a.trace_defer0 = (int32_t)s->utrace_main;
   a.diag_last = s->diag_last;
   a.parity = s->parity;
   return a;
@@ -953,6 +966,7 @@ int gs_stepper_create(const gs_config* cfg, gs_stepper** out) {
   if (const char* v = getenv("GRAVSIM_EMU_COMM_US")) s->emu_lat_us = atof(v);
   if (const char* v = getenv("GRAVSIM_EMU_COMM_WGS")) s->emu_wgs = atoi(v);
   if (const char* v = getenv("GRAVSIM_GATE_PROBE")) s->gate_probe = atoi(v);
+  if (const char* v = getenv("GRAVSIM_SYM_DYN_CAP")) s->dyn_cap = atoi(v);
   if (const char* v = getenv("GRAVSIM_SYM_DIAG_LAST")) s->diag_last = atoi(v);
   if (const char* v = getenv("GRAVSIM_SYM_FUSED_TAIL")) s->fuse_tail = atoi(v) != 0 ? 1 : 0;
   if (const char* v = getenv("GRAVSIM_SYM_PARITY")) s->parity = atoi(v) != 0 ? 1 : 0;
@@ -977,6 +991,12 @@ int gs_stepper_create(const gs_config* cfg, gs_stepper** out) {
     if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, cfg->device) == hipSuccess &&
         khz > 0)
       s->clk_khz = khz;
+  }
+  {
+    const int occ = gs::sym_occupancy(s->esz == 8);
+    s->sym_first_wave = (occ > 0 ? occ : 2) * s->cus;
+    // (tests shrink it so that small runs take the dynamic path too)
+    if (const char* v = getenv("GRAVSIM_SYM_FIRST_WAVE")) s->sym_first_wave = atoi(v);
   }
   for (int fm = 0; fm < 3; ++fm)
     s->occ[fm] = s->esz == 4 ? gs::split_occupancy<float>(s->L.kernel, s->L.ipl, fm)
@@ -1019,8 +1039,9 @@ int gs_stepper_create(const gs_config* cfg, gs_stepper** out) {
   }
   FAIL_CLEAN(hipMalloc(&s->mass_dev, (size_t)s->L.n_pad * sizeof(double)));
   FAIL_CLEAN(hipMalloc(&s->nonfinite, sizeof(unsigned long long)));
-  FAIL_CLEAN(hipMalloc(&s->gate_buf, 4 * sizeof(unsigned)));
-  FAIL_CLEAN(hipMemsetAsync(s->gate_buf, 0, 4 * sizeof(unsigned), s->s_comp));
+  // [0..1] gather gates, [2..3] deferral stats, [4..5] dynamic unit-fetch counters
+  FAIL_CLEAN(hipMalloc(&s->gate_buf, 8 * sizeof(unsigned)));
+  FAIL_CLEAN(hipMemsetAsync(s->gate_buf, 0, 8 * sizeof(unsigned), s->s_comp));
   if (s->L.mode == GS_MODE_SYM) {
     // Deferred-unit list of the gated launch (one band's units) and the local-first order.
     const int rows = s->sym_NC / cfg->nranks;
@@ -1039,6 +1060,12 @@ int gs_stepper_create(const gs_config* cfg, gs_stepper** out) {
       FAIL_CLEAN(hipMemcpy(s->sym_lf, lf.data(), lf.size() * sizeof(int32_t),
                            hipMemcpyHostToDevice));
     }
+  }
+  if (s->L.mode == GS_MODE_SYM && getenv("GRAVSIM_UNIT_TRACE")) {
+    // One entry per unit of a band-wide launch plus as many deferred ones (units 7).
+    s->utrace_main = (int64_t)s->sym_band * (s->sym_S_n + s->sym_D);
+    FAIL_CLEAN(hipMalloc(&s->utrace, (size_t)(2 * s->utrace_main) * 4 * sizeof(unsigned long long)));
+    FAIL_CLEAN(hipMemsetAsync(s->utrace, 0, (size_t)(2 * s->utrace_main) * 4 * 8, s->s_comp));
   }
   if (s->emulate && s->emu_gbps > 0.0) {
     // Scratch destination of the modeled collectives (the larger of the two per step).
@@ -1070,7 +1097,7 @@ int gs_stepper_destroy(gs_stepper* s) {
   for (void* p : {s->X[0], s->X[1], s->vel, s->partial, s->acc, (void*)s->mass_dev,
                   (void*)s->nonfinite, (void*)s->sym_Pi, (void*)s->sym_Pj, (void*)s->sym_Pd,
                   (void*)s->sym_S, (void*)s->sym_R, (void*)s->sym_Ti, (void*)s->gate_buf,
-                  (void*)s->defer, (void*)s->sym_lf, s->emu_buf})
+                  (void*)s->defer, (void*)s->sym_lf, s->emu_buf, (void*)s->utrace})
     if (p) (void)hipFree(p);
   for (hipEvent_t e : {s->ev_ready, s->ev_gathered, s->ev_t0, s->ev_local, s->ev_end,
                        s->ev_remote, s->ev_fork, s->ev_rem2, s->ev_sym})
@@ -1191,6 +1218,18 @@ int gs_stepper_set_overlap(gs_stepper* s, int32_t mode) {
   s->sym_overlap = mode;
   if (s->graph) { (void)hipGraphExecDestroy(s->graph); s->graph = nullptr; }
   return 0;
+}
+
+int64_t gs_stepper_unit_trace(gs_stepper* s, uint64_t* out, int64_t cap) {
+  if (!s->utrace) return 0;
+  const int64_t n = 2 * s->utrace_main;
+  if (!out) return n;
+  GS_HIP(hipSetDevice(s->cfg.device));
+  GS_HIP(hipStreamSynchronize(s->s_comp));
+  const int64_t m = cap < n ? cap : n;
+  GS_HIP(hipMemcpy(out, s->utrace, (size_t)m * 4 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  GS_HIP(hipMemset(s->utrace, 0, (size_t)n * 4 * sizeof(uint64_t)));
+  return m;
 }
 
 int gs_stepper_set_timeout(gs_stepper* s, double step_timeout_s) {

@@ -161,6 +161,11 @@ int gs_stepper_phase_stats(gs_stepper* s, double* out8);
 // units run once the gather is published or are deferred to a second launch behind it
 // (GRAVSIM_SYM_OVERLAP sets the initial value).
 int gs_stepper_set_overlap(gs_stepper* s, int32_t mode);
+// Unit timeline of the last sym force launch (stepper created with GRAVSIM_UNIT_TRACE set):
+// copies up to `cap` entries of 4 words {start, end (100 MHz ticks), HW_ID | XCC_ID << 32,
+// row << 32 | segment} (all zero: the slot ran no unit) and clears them. Returns the count;
+// out = nullptr returns the capacity; 0 when tracing is off.
+int64_t gs_stepper_unit_trace(gs_stepper* s, uint64_t* out, int64_t cap);
 // Bound on the host waiting for the oldest of the enqueued steps when it runs far ahead.
 int gs_stepper_set_timeout(gs_stepper* s, double step_timeout_s);
 // Resolved force path: *exact = 1 for the hard-cutoff select, *eps2 = r^2 offset in use.

@@ -91,6 +91,18 @@ struct SymArgs {
   int32_t gate_probe;   // timing probe of the emulation only (GRAVSIM_GATE_PROBE): 0 acquire
   int32_t diag_last;    // units 0: shell segments first, diagonal parts last (else row by row)
   int32_t parity;       // antipodal chunk pairs split between rows by parity (else A < NC/2)
+  // Unit timeline probe (GRAVSIM_UNIT_TRACE, diagnostics only; nullptr otherwise): per force
+  // workgroup 4 words {start, end (s_memrealtime, 100 MHz), HW_ID | XCC_ID << 32,
+  // row << 32 | segment}, at [blockIdx.x] (units 0/6) or [trace_defer0 + k] (units 7).
+  unsigned long long* utrace;
+  int32_t trace_defer0;
+  // Dynamic unit fetch (units 0 / 6; nullptr: unit = blockIdx.x). Workgroups take unit
+  // indices from work[0] in order, the first `first_wave` workgroups one unit each, the others
+  // up to `unit_cap`, so XCDs that run faster take more units; the last workgroup to finish
+  // (work[1] counts exits) re-arms both counters for the next launch. n_units: set by the
+  // launcher.
+  unsigned* work;
+  int32_t n_units, unit_cap, first_wave;
 };
 
 hipError_t launch_force_sym(const SymArgs& a, hipStream_t s);

@@ -151,6 +151,7 @@ def hip_lib():
         _sig(lib, "gs_stepper_phase_stats", c_int32, [S, _PD])
         _sig(lib, "gs_stepper_set_overlap", c_int32, [S, c_int32])
         _sig(lib, "gs_stepper_set_timeout", c_int32, [S, c_double])
+        _sig(lib, "gs_stepper_unit_trace", c_int64, [S, c_void_p, c_int64])
         _sig(lib, "gs_stepper_compute_stream", c_void_p, [S])
         _sig(lib, "gs_stepper_force_mode", c_int32, [S, POINTER(c_int32), POINTER(c_double)])
         _sig(lib, "gs_group_step", c_int32, [POINTER(S), c_int32, c_int32])

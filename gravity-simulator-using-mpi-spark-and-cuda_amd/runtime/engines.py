@@ -140,6 +140,19 @@ class HipEngine:
                 "deferred_units": int(v[6]), "comm_ms": v[2] + v[3],
                 "exposed_comm_ms": v[4] + v[5]}
 
+    def unit_trace(self) -> np.ndarray:
+        """(entries, 4) uint64 timeline of the last sym force launch (GRAVSIM_UNIT_TRACE set
+        at creation): start, end (100 MHz ticks), HW_ID | XCC_ID << 32, row << 32 | segment.
+        Empty when tracing is off."""
+        cap = int(self.lib.gs_stepper_unit_trace(self._s, None, 0))
+        out = np.zeros((max(cap, 0), 4), dtype=np.uint64)
+        if cap > 0:
+            got = int(self.lib.gs_stepper_unit_trace(self._s, out.ctypes.data, cap))
+            if got < 0:
+                _native.check(self.lib, -1, "unit_trace")
+            out = out[:got]
+        return out
+
     def set_overlap(self, mode: int) -> None:
         """Sym-schedule work beside the all-gather (0..3, see gravsim.h)."""
         _native.check(self.lib, self.lib.gs_stepper_set_overlap(self._s, int(mode)), "overlap")

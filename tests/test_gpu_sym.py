@@ -221,3 +221,30 @@ def test_sym_fused_tail_bitwise(hip, monkeypatch, n, dtype):
     assert np.array_equal(out[0][0], out[1][0])
     assert np.array_equal(out[0][1].pos, out[1][1].pos)
     assert np.array_equal(out[0][1].vel, out[1][1].vel)
+
+
+@pytest.mark.parametrize("n,dtype,P,first_wave", [
+    (262144, "fp32", 1, None),   # default first wave (resident slots), 16,640 units
+    (40000, "fp32", 1, "16"),
+    (40000, "fp32", 2, "16"),    # two virtual ranks
+    (40000, "fp64", 1, "16"),
+])
+def test_sym_dynamic_unit_fetch_bitwise(hip, monkeypatch, n, dtype, P, first_wave):
+    """Workgroups that fetch their units from a device counter (GRAVSIM_SYM_DYN_CAP > 1, the
+    default) run the same units into the same slots as one unit per workgroup (0): same
+    bits, and the counters re-arm themselves launch after launch (graph replay included)."""
+    from gravsim.runtime.engines import VirtualGroup
+
+    if first_wave:
+        monkeypatch.setenv("GRAVSIM_SYM_FIRST_WAVE", first_wave)
+    cfg = SimConfig(n=n, dtype=dtype, device="gpu", mode="sym")
+    out = []
+    for cap in ("0", "4"):
+        monkeypatch.setenv("GRAVSIM_SYM_DYN_CAP", cap)
+        g = VirtualGroup(cfg, P)
+        g.init_ics("solar+random", 23)
+        g.step(5)
+        out.append(g.state())
+        g.close()
+    assert np.array_equal(out[0].pos, out[1].pos)
+    assert np.array_equal(out[0].vel, out[1].vel)
