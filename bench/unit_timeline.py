@@ -64,6 +64,15 @@ def analyse(tr: np.ndarray, S: int, slots_per_cu: int = 2) -> dict:
     shell = dur[seg < S]
     diag = dur[seg >= S]
     xcd_end = {int(x): round(float(t1[xcc == x].max()) * TICK_MS, 3) for x in sorted(set(xcc.tolist()))}
+    # units running at once on one CU (expected: the resident workgroups per CU)
+    cu_key = ((xcc * 8 + se) * 2 + sh) * 16 + cu
+    conc = []
+    for k in np.unique(cu_key):
+        m = cu_key == k
+        e = np.concatenate([np.stack([t0[m], np.ones(m.sum(), np.int64)], 1),
+                            np.stack([t1[m], -np.ones(m.sum(), np.int64)], 1)])
+        e = e[np.lexsort((e[:, 1], e[:, 0]))]
+        conc.append(int(np.cumsum(e[:, 1]).max()))
     return {
         "units": int(len(t)), "cus_seen": cus, "slots": slots,
         "span_ms": round(span * TICK_MS, 3),
@@ -75,6 +84,7 @@ def analyse(tr: np.ndarray, S: int, slots_per_cu: int = 2) -> dict:
         "diag_ms": round(statistics.median(diag.tolist()) * TICK_MS, 4) if len(diag) else None,
         "n_shell": int(len(shell)), "n_diag": int(len(diag)),
         "xcd_end_ms": xcd_end,
+        "max_units_per_cu": max(conc), "median_max_units_per_cu": float(np.median(conc)),
         "xcd_units": {int(x): int((xcc == x).sum()) for x in sorted(set(xcc.tolist()))},
     }
 
