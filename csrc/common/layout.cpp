@@ -49,13 +49,12 @@ extern "C" int gs_layout_compute(const gs_config* cfg, gs_layout* out) {
   const int64_t sym_unit = 8 * (int64_t)(chunk % 2048 == 0 ? chunk : 2 * chunk);
   const int64_t sym_pad = gs::round_up(cfg->n, sym_unit);
   bool sym = cfg->mode == GS_MODE_SYM;
-  // From 64K bodies the sym schedule beats the one-sided split (65536: 1.053 vs 1.082 ms,
-  // 131072: 3.05 vs 3.80, 262144: 11.0 vs 16.4; profiles/r1_sym_sizes.jsonl).
-  if (cfg->mode == GS_MODE_AUTO && sym_ok && cfg->n >= 65536 && sym_pad * 20 <= out->n_pad * 21) {
-    // The partial slots are processed in bands of bounded size (stepper.hip ensure_sym),
-    // so memory does not limit the choice.
-    sym = true;
-  }
+  // From 16K bodies the sym schedule beats the one-sided split/fused kernels, padding
+  // included (all-ghost chunks are skipped): 16384 0.137 vs 0.196 ms, 50000 (cuda.cu's N)
+  // 0.479 vs 0.630, 100000 1.64 vs 2.25, 300000 14.1 vs 21.5 (profiles/r2_sizes_auto_vs_sym.txt).
+  // The partial slots are processed in bands of bounded size (stepper.hip ensure_sym), so
+  // memory does not limit the choice either.
+  if (cfg->mode == GS_MODE_AUTO && sym_ok && cfg->n >= 16384) sym = true;
   if (sym) out->n_pad = sym_pad;
   out->n_local = out->n_pad / cfg->nranks;
   out->local_begin = (int64_t)cfg->rank * out->n_local;
