@@ -426,16 +426,6 @@ __device__ __forceinline__ void force_sym_entry(SymArgs a) {
       force_sym_body<T, EXACT>(a, (int)u);
       __syncthreads();  // next_s and the LDS tiles are rewritten by the next unit
     }
-    if (threadIdx.x == 0) {
-      // The last workgroup out re-arms the counters (every other one has finished fetching:
-      // its fetches precede its exit count, acq_rel).
-      const unsigned e =
-          __hip_atomic_fetch_add(a.work + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-      if (e == gridDim.x - 1) {
-        __hip_atomic_store(a.work, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(a.work + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
   } else {
     const unsigned n = a.defer[0];
     if (blockIdx.x == 0 && threadIdx.x == 0 && n > 0)
@@ -709,6 +699,10 @@ hipError_t launch_force_sym_t(const SymArgs& a, hipStream_t s) {
   b.n_units = units;
   unsigned g = (unsigned)units;
   if (a.work && (a.units == 0 || a.units == 6) && a.unit_cap > 1 && units > a.first_wave) {
+    // the counter starts at 0 for every launch: a stream-ordered memset (a graph node when
+    // captured), not state carried over from the previous launch
+    const hipError_t e = hipMemsetAsync(a.work, 0, sizeof(unsigned), s);
+    if (e != hipSuccess) return e;
     // first wave: one unit per workgroup; the rest: up to unit_cap each, with 25 % slack so
     // a fast XCD can take more than its rotation share
     const int64_t rest = units - a.first_wave;

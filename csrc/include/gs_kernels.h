@@ -98,9 +98,8 @@ struct SymArgs {
   int32_t trace_defer0;
   // Dynamic unit fetch (units 0 / 6; nullptr: unit = blockIdx.x). Workgroups take unit
   // indices from work[0] in order, the first `first_wave` workgroups one unit each, the others
-  // up to `unit_cap`, so XCDs that run faster take more units; the last workgroup to finish
-  // (work[1] counts exits) re-arms both counters for the next launch. n_units: set by the
-  // launcher.
+  // up to `unit_cap`, so XCDs that run faster take more units. The launcher zeroes work[0]
+  // on the stream before every such launch. n_units: set by the launcher.
   unsigned* work;
   int32_t n_units, unit_cap, first_wave;
 };
