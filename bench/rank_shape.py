@@ -21,7 +21,6 @@ import sys
 import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-os.environ["GRAVSIM_EMULATE_RANK"] = "1"
 
 
 def main() -> int:
@@ -55,6 +54,7 @@ def main() -> int:
                     help="comma list; timing probes of the gated launch: 0 acquire (real), "
                          "1 no check (order only), 2 relaxed load")
     a = ap.parse_args()
+    os.environ["GRAVSIM_EMULATE_RANK"] = "1"
     os.environ["GRAVSIM_EMU_COMM_US"] = str(a.comm_us)
     os.environ["GRAVSIM_EMU_COMM_WGS"] = str(a.comm_wgs)
     import torch  # noqa: F401

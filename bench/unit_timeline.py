@@ -28,8 +28,6 @@ import sys
 import numpy as np
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-os.environ["GRAVSIM_EMULATE_RANK"] = "1"
-os.environ["GRAVSIM_UNIT_TRACE"] = "1"
 
 TICK_MS = 1e-5  # s_memrealtime runs at 100 MHz
 
@@ -100,6 +98,9 @@ def main() -> int:
                     help="VAR=v1,v2 axis set while the engine is created (repeatable)")
     ap.add_argument("--out", default=None, help="also save the raw traces here (.npz)")
     a = ap.parse_args()
+    # (set here, not at import: tests import analyse() and must not inherit these)
+    os.environ["GRAVSIM_EMULATE_RANK"] = "1"
+    os.environ["GRAVSIM_UNIT_TRACE"] = "1"
     import torch  # noqa: F401
 
     import gravsim  # noqa: F401

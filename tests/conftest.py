@@ -25,3 +25,17 @@ def hip():
     lib = _native.hip_lib()
     assert lib.gs_hip_device_count() > 0
     return lib
+
+
+# Knobs that change what the native stepper computes (per-rank timing emulation, probes).
+# Tests set them only through monkeypatch; one left in the process environment (e.g. by a
+# module imported at collection) would silently alter every later test.
+_PROCESS_KNOBS = ("GRAVSIM_EMULATE_RANK", "GRAVSIM_UNIT_TRACE", "GRAVSIM_EMU_COMM_GBPS",
+                  "GRAVSIM_SYM_DYN_CAP", "GRAVSIM_SYM_FIRST_WAVE", "GRAVSIM_SYM_BAND_MB")
+
+
+@pytest.fixture(autouse=True)
+def _no_stray_native_knobs():
+    stray = [k for k in _PROCESS_KNOBS if k in os.environ]
+    assert not stray, f"process environment carries stepper knobs {stray}"
+    yield
