@@ -49,12 +49,14 @@ extern "C" int gs_layout_compute(const gs_config* cfg, gs_layout* out) {
   const int64_t sym_unit = 8 * (int64_t)(chunk % 2048 == 0 ? chunk : 2 * chunk);
   const int64_t sym_pad = gs::round_up(cfg->n, sym_unit);
   bool sym = cfg->mode == GS_MODE_SYM;
-  // From 16K bodies the sym schedule beats the one-sided split/fused kernels, padding
-  // included (all-ghost chunks are skipped): 16384 0.137 vs 0.196 ms, 50000 (cuda.cu's N)
-  // 0.479 vs 0.630, 100000 1.64 vs 2.25, 300000 14.1 vs 21.5 (profiles/r2_sizes_auto_vs_sym.txt).
-  // The partial slots are processed in bands of bounded size (stepper.hip ensure_sym), so
-  // memory does not limit the choice either.
-  if (cfg->mode == GS_MODE_AUTO && sym_ok && cfg->n >= 16384) sym = true;
+  // From 16K bodies (fp32) / 32K (fp64) the sym schedule beats the one-sided split/fused
+  // kernels, padding included (all-ghost chunks are skipped). fp32: 16384 0.137 vs 0.196 ms,
+  // 50000 (cuda.cu's N) 0.479 vs 0.630, 100000 1.64 vs 2.25, 300000 14.1 vs 21.5; fp64: 16384
+  // 0.283 vs 0.250 (split wins), 50000 1.21 vs 1.75, 300000 37.5 vs 56.5
+  // (profiles/r2_sizes_auto_vs_sym.txt). The partial slots are processed in bands of bounded
+  // size (stepper.hip ensure_sym), so memory does not limit the choice either.
+  const int64_t sym_min = cfg->dtype == GS_FP32 ? 16384 : 32768;
+  if (cfg->mode == GS_MODE_AUTO && sym_ok && cfg->n >= sym_min) sym = true;
   if (sym) out->n_pad = sym_pad;
   out->n_local = out->n_pad / cfg->nranks;
   out->local_begin = (int64_t)cfg->rank * out->n_local;

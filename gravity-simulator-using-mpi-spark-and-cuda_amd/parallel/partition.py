@@ -95,10 +95,11 @@ def sym_bytes(n_pad: int, nranks: int, esz: int = 4) -> int:
 
 def sym_auto(n: int, nranks: int, chunk: int = 0, dtype: str = "fp32") -> bool:
     """Whether mode=auto picks the sym schedule (mirror of gs_layout_compute)."""
-    del chunk, dtype  # (the choice depends on n and the rank count only)
-    # from 16K bodies sym wins, padding included (profiles/r2_sizes_auto_vs_sym.txt); the
-    # partial slots are processed in bounded bands, so memory does not limit the choice
-    return 8 % nranks == 0 and n >= 16384
+    del chunk  # (the choice depends on n, the rank count and the dtype only)
+    # from 16K (fp32) / 32K (fp64) bodies sym wins, padding included
+    # (profiles/r2_sizes_auto_vs_sym.txt); the partial slots are processed in bounded bands,
+    # so memory does not limit the choice
+    return 8 % nranks == 0 and n >= (16384 if dtype == "fp32" else 32768)
 
 
 def layout(n: int, rank: int = 0, nranks: int = 1, chunk: int = 0, sym: bool = False) -> Layout:

@@ -14,15 +14,18 @@ from gravsim.ops import _native
 from gravsim.parallel import partition
 
 
-@pytest.mark.parametrize("n", [1, 2, 3, 8, 1000, 2048, 2049, 65536, 100_003, 1 << 20, 16_777_216])
+@pytest.mark.parametrize("n", [1, 2, 3, 8, 1000, 2048, 2049, 16383, 16384, 20000, 32768, 65536,
+                               100_003, 1 << 20, 16_777_216])
 @pytest.mark.parametrize("P", [1, 2, 3, 4, 8])
-def test_python_layout_matches_native(n, P):
+@pytest.mark.parametrize("dtype", ["fp32", "fp64"])
+def test_python_layout_matches_native(n, P, dtype):
     lib = _native.cpu_lib()
     for r in sorted({0, P - 1, P // 2}):
-        c = _native.GsConfig(n=n, dtype=0, rank=r, nranks=P, device=0)
+        c = _native.GsConfig(n=n, dtype=_native.GS_FP64 if dtype == "fp64" else _native.GS_FP32,
+                             rank=r, nranks=P, device=0)
         L = _native.GsLayout()
         assert lib.gs_layout_compute(ctypes.byref(c), ctypes.byref(L)) == 0
-        sym = partition.sym_auto(n, P)
+        sym = partition.sym_auto(n, P, dtype=dtype)
         assert (L.mode == _native.MODE_IDS["sym"]) == sym
         p = partition.layout(n, r, P, sym=sym)
         assert (L.n_pad, L.n_local, L.local_begin, L.chunk, L.n_chunks) == \
