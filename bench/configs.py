@@ -55,12 +55,14 @@ def gpu_run(n, dtype, steps, warmup, P=1, rank=0, overlap=None, **kw):
 
 def main() -> int:
     ap = argparse.ArgumentParser()
-    ap.add_argument("--only", default="1,2,3,4,5")
+    ap.add_argument("--only", default="1,2,3,4,5,6")
     ap.add_argument("--md", default=None)
     ap.add_argument("--comm-gbps", type=float, default=64.0,
                     help="modeled per-rank collective rate of the 8-GPU emulations (0: free)")
     ap.add_argument("--comm-us", type=float, default=15.0)
-    ap.add_argument("--overlap", type=int, default=None, help="sym overlap mode (default: built-in)")
+    ap.add_argument("--overlap", type=int, default=3,
+                    help="sym overlap mode of the 8-GPU emulations (default 3: the gated launch "
+                         "bench.py's --overlap auto picks for multi-rank sym runs)")
     a = ap.parse_args()
     want = {int(x) for x in a.only.split(",")}
     rows = []
@@ -105,6 +107,12 @@ def main() -> int:
         rows.append(dict(config="#4 4,194,304 fp64", gpus=8, how=how8,
                          ms_per_step=ms8, body_updates_per_s=n / (ms8 * 1e-3), layout=lay8,
                          phase=ph))
+        print(json.dumps(rows[-1]), flush=True)
+    if 6 in want:
+        # the reference's own CUDA workload (cuda.cu:121-123: N = 50,000, fp32, 1 GPU)
+        ms, lay, _ = gpu_run(50000, "fp32", 200, 10)
+        rows.append(dict(config="cuda.cu's 50,000 fp32", gpus=1, how="measured", ms_per_step=ms,
+                         body_updates_per_s=50000 / (ms * 1e-3), layout=lay))
         print(json.dumps(rows[-1]), flush=True)
     if 5 in want:
         n = 1 << 24
