@@ -21,7 +21,7 @@
 // captured once into a hipGraph (two steps = one ping-pong period) and replayed. With
 // use_graph >= 2 the multi-rank step, collective included, is captured too.
 //
-// Newton-3 sym schedule (GS_MODE_SYM, the default from 64K bodies; nbody_sym.hip):
+// Newton-3 sym schedule (GS_MODE_SYM, the default from 16K bodies fp32 / 32K fp64; nbody_sym.hip):
 //   s_comm : ncclAllGather in place (as above)
 //   s_comp : wait(gathered) -> every unit in one launch (diagonal chunks one-sided, shell
 //            chunks both sides of every pair) -> group reduce
