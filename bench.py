@@ -223,7 +223,8 @@ def main(argv=None) -> int:
             kernel_info = {"kernel": f"sym: register tile (LDS-staged j, DPP carriers), {tile}, "
                                      "cyclic half-shell of 2048-body chunks",
                            "n_pad": lay["n_pad"]}
-            exch = "all-gather + group-sum send/recv"
+            exch = ("ring of P-1 neighbour stages" if a.strategy == "ring" else "all-gather") + \
+                " + group-sum send/recv"
             pairs = cfg.n * (cfg.n - 1) / 2  # unordered pairs, each evaluated once
         else:
             kernel_info = {"kernel": _native.KERNEL_NAMES.get(lay["kernel"]), "ipl": lay["ipl"],

@@ -215,6 +215,64 @@ extern "C" int64_t gs_sym_unit_map(int64_t n_pad, int32_t rank, int32_t nranks, 
   return k;
 }
 
+// The gated sym launch's unit order for the ring strategy: the slice of rank (rank - k) mod P
+// arrives at ring stage k (1 .. P-1), so a remote unit can start once the stage of the latest
+// slice it reads has landed. Entry = bit 31 remote | stage << 28 | row << 16 | unit (rows <
+// 4096). Order: the first `fill` local units as in gs_sym_unit_map, then every other unit by
+// stage (local ones first), row by row within a stage, shell segments before diagonal parts.
+// Returns the entry count, 0 if the fields cannot hold the geometry, -1 on error.
+extern "C" int64_t gs_sym_unit_map_ring(int64_t n_pad, int32_t rank, int32_t nranks,
+                                        int32_t parity, int64_t fill, int32_t* out, int64_t cap) {
+  int32_t NC, H, L, S, D;
+  if (nranks < 1 || rank < 0 || rank >= nranks || gs_sym_geometry(n_pad, &NC, &H, &L, &S, &D))
+    return -1;
+  if (NC % nranks) return -1;
+  const int32_t rows = NC / nranks, per = S + D, a0 = rank * rows;
+  const int64_t total = (int64_t)rows * per;
+  if (rows >= 4096 || per >= 65536 || nranks > 8) return 0;
+  if (!out || cap < total) return -1;
+  // ring stage of every unit (0: reads only the rank's own rows)
+  std::vector<int8_t> stage((size_t)total, 0);
+  for (int32_t r = 0; r < rows; ++r) {
+    const int32_t A = a0 + r;
+    const int32_t segs = (16 * gs_sym_shell_len(A, NC, parity) + L - 1) / L;
+    for (int32_t g = 0; g < S && g < segs; ++g) {
+      const int32_t q0 = g * L, q1 = (g + 1) * L - 1;  // quanta of the shell, 16 per chunk
+      int32_t st = 0;
+      for (int32_t d = 1 + q0 / 16; d <= 1 + q1 / 16; ++d) {
+        const int32_t owner = ((A + d) % NC) / rows;
+        const int32_t k = ((rank - owner) % nranks + nranks) % nranks;
+        if (k > st) st = k;
+      }
+      stage[(size_t)r * per + g] = (int8_t)st;
+    }
+  }
+  std::vector<int32_t> nl(rows);
+  std::vector<char> moved((size_t)total, 0);
+  int64_t k = 0;
+  for (int32_t r = 0; r < rows; ++r) {  // the local prefix, exactly as gs_sym_unit_map
+    nl[r] = sym_local_segs(a0 + r, NC, a0, rows, L, S, parity);
+    for (int32_t q = 0; q < D && (fill < 0 || k < fill); ++q) {
+      out[k++] = (r << 16) | (S + q);
+      moved[(size_t)r * per + S + q] = 1;
+    }
+    for (int32_t g = 0; g < nl[r] && (fill < 0 || k < fill); ++g) {
+      out[k++] = (r << 16) | g;
+      moved[(size_t)r * per + g] = 1;
+    }
+  }
+  for (int32_t st = 0; st < nranks; ++st)
+    for (int pass = 0; pass < 2; ++pass)
+      for (int32_t r = 0; r < rows; ++r)
+        for (int32_t u = pass ? S : 0; u < (pass ? per : S); ++u) {
+          const size_t i = (size_t)r * per + u;
+          if (moved[i] || stage[i] != st) continue;
+          const uint32_t remote = st > 0 ? 0x80000000u : 0u;
+          out[k++] = (int32_t)(remote | ((uint32_t)st << 28) | ((uint32_t)r << 16) | (uint32_t)u);
+        }
+  return k;
+}
+
 // Partial-slot bytes per rank if all of the rank's rows were held at once (one band).
 extern "C" int64_t gs_sym_bytes(int64_t n_pad, int32_t nranks, int32_t esz) {
   int32_t nc, h, l, sg, dp;

@@ -261,10 +261,15 @@ __device__ __forceinline__ void run_tiles(const SymArgs& a, ISetK<T>& is, TileSe
 // the step has been handed out. The order is a host-built map (one uniform load per
 // workgroup: unit -> row << 16 | segment, bit 31 = remote); a search through prefix sums put
 // a chain of dependent loads in front of every workgroup and cost 2 % of the step.
-__device__ __forceinline__ bool local_first_unit(const SymArgs& a, int b, int* br, int* s) {
+// With the ring strategy (gate_n > 1) bits 28-30 hold the ring stage whose slice the unit
+// waits for and rows are < 4096 (layout.cpp gs_sym_unit_map_ring).
+__device__ __forceinline__ bool local_first_unit(const SymArgs& a, int b, int* br, int* s,
+                                                 int* stage) {
   const uint32_t m = (uint32_t)a.lf[b];
-  *br = (int)((m >> 16) & 0x7fffu);
+  const bool ring = a.gate_n > 1;
+  *br = (int)((m >> 16) & (ring ? 0xfffu : 0x7fffu));
   *s = (int)(m & 0xffffu);
+  *stage = ring ? (int)((m >> 28) & 7u) : 0;
   return (m >> 31) != 0u;
 }
 
@@ -273,14 +278,15 @@ __device__ __forceinline__ bool local_first_unit(const SymArgs& a, int b, int* b
 // collective's writes); otherwise append the unit to the deferred list and leave. No
 // workgroup ever waits on the collective, so RCCL's kernels always find CUs; the deferred
 // units run in a second launch (units 7) queued behind the gather event.
-__device__ __forceinline__ bool gate_open_or_defer(const SymArgs& a, int b) {
+__device__ __forceinline__ bool gate_open_or_defer(const SymArgs& a, int b, int stage) {
   __shared__ int open_s;
   if (threadIdx.x == 0) {
+    const unsigned* gate = a.gate + stage;
     // (gate_probe: timing probes only, per-rank emulation: 1 skips the check, 2 loads relaxed)
     const bool open = a.gate_probe == 1 ? true
                       : a.gate_probe == 2
-                          ? __hip_atomic_load(a.gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u
-                          : __hip_atomic_load(a.gate, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+                          ? __hip_atomic_load(gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u
+                          : __hip_atomic_load(gate, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != 0u;
     if (!open) {
       const unsigned k =
           __hip_atomic_fetch_add(a.defer, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -302,12 +308,12 @@ __device__ __forceinline__ void force_sym_body(const SymArgs& a, int b) {
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   // Units per row: S shell segments, then D parts of the diagonal chunk.
   // br: row within the band (index into Pi/Pj/Pd); the rank's row is band0 + br.
-  int br, s;
+  int br, s, stage = 0;
   bool gated = false;
   if (a.units == 6) {
-    gated = local_first_unit(a, b, &br, &s) && a.gate != nullptr;
+    gated = local_first_unit(a, b, &br, &s, &stage) && a.gate != nullptr;
   } else if (a.units == 7) {  // deferred unit a.defer_index of the units-6 launch
-    local_first_unit(a, (int)a.defer[1 + a.defer_index], &br, &s);
+    local_first_unit(a, (int)a.defer[1 + a.defer_index], &br, &s, &stage);
   } else if (a.units == 1) {
     br = b / a.D;
     s = a.S + b % a.D;
@@ -353,7 +359,7 @@ __device__ __forceinline__ void force_sym_body(const SymArgs& a, int b) {
     }
     seq.u = seq.valid(u0);
   }
-  if (gated && !gate_open_or_defer(a, b)) return;
+  if (gated && !gate_open_or_defer(a, b, stage)) return;
   const unsigned long long t_start = a.utrace ? __builtin_amdgcn_s_memrealtime() : 0ull;
   const V4* X4 = static_cast<const V4*>(a.X);
   ISetK<T> is;
@@ -548,10 +554,9 @@ __global__ __launch_bounds__(256) void sym_finalize_kernel(SymArgs a) {
   const int64_t li = (int64_t)blockIdx.x * 256 + threadIdx.x;
   // This step's gated launches have completed (stream order): re-arm the gate for the next
   // all-gather into the same buffer (two steps on) and empty the deferred list.
-  if (a.gate && li == 0) {
-    __hip_atomic_store(a.gate, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(a.defer, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
+  if (a.gate && li < a.gate_n)
+    __hip_atomic_store(a.gate + li, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (a.gate && li == 0) __hip_atomic_store(a.defer, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (li >= a.n_local) return;
   const int64_t gi = a.i_begin + li;
   V4* vel = static_cast<V4*>(a.vel);
@@ -605,10 +610,10 @@ __global__ __launch_bounds__(192) void sym_tail_kernel(SymArgs a) {
   __shared__ T acc_s[3][64];
   const int k = threadIdx.x >> 6, l = threadIdx.x & 63;
   const int64_t li = (int64_t)blockIdx.x * 64 + l;
-  if (a.gate && blockIdx.x == 0 && threadIdx.x == 0) {
-    __hip_atomic_store(a.gate, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (a.gate && blockIdx.x == 0 && (int)threadIdx.x < a.gate_n)
+    __hip_atomic_store(a.gate + threadIdx.x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (a.gate && blockIdx.x == 0 && threadIdx.x == 0)
     __hip_atomic_store(a.defer, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
   const int64_t gi = a.i_begin + li;
   const bool real = li < a.n_local && gi < a.n_real;
   if (real) {

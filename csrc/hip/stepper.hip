@@ -141,6 +141,11 @@ struct gs_stepper {
   unsigned* gate_buf = nullptr;
   unsigned* defer = nullptr;
   int32_t* sym_lf = nullptr;  // units-6 order: unit -> row << 16 | segment (bit 31 remote)
+  // Ring strategy of the sym schedule: P-1 neighbour stages instead of one all-gather; the
+  // gated launch waits per stage (ring_gate[8 * buffer + stage], set after each stage's
+  // receive) and its unit map orders the remote units by stage.
+  bool sym_ring = false;
+  unsigned* ring_gate = nullptr;
   int gate_probe = 0;         // GRAVSIM_GATE_PROBE (emulation timing probes only)
   int diag_last = 1;          // GRAVSIM_SYM_DIAG_LAST=0: row-by-row unit order (A/B only)
   int fuse_tail = -1;         // GRAVSIM_SYM_FUSED_TAIL: -1 by size (<= 256K), 0 off, 1 on
@@ -445,8 +450,13 @@ int choose_groups(gs_stepper* s, int span, bool phi, bool concurrent = false) {
   return best;
 }
 
+int ring_xfer_rccl(gs_stepper* s, int cur, int sub);
+
 // In-place all-gather of X[cur] on s_comm (ev_gathered marks completion). With `gate` the
-// comm stream also publishes completion to a force launch already running (units 6).
+// comm stream also publishes completion to a force launch already running (units 6). The sym
+// schedule's ring strategy moves the slices in P-1 neighbour stages instead and, gated,
+// publishes each stage as it lands (ring_gate[8 * cur + k]), so the units that read only
+// slices already received can start.
 int gather(gs_stepper* s, int cur, bool gate = false) {
   if (!xcomm(s) || s->full[cur]) return 0;
   char* buf = static_cast<char*>(s->X[cur]);
@@ -454,14 +464,25 @@ int gather(gs_stepper* s, int cur, bool gate = false) {
   GS_HIP(hipEventRecord(s->ev_ready, s->s_comp));
   GS_HIP(hipStreamWaitEvent(s->s_comm, s->ev_ready, 0));
   GS_MARK(g0, g, s->s_comm);
-  if (s->emulate) {
+  if (s->sym_ring && use_sym(s)) {
+    const size_t slice = (size_t)s->L.n_local * row_bytes(s);
+    for (int k = 1; k < s->cfg.nranks; ++k) {
+      if (s->emulate) {
+        if (comm_model(s, buf, slice)) return -1;
+      } else if (ring_xfer_rccl(s, cur, k)) {
+        return -1;
+      }
+      if (gate) GS_HIP(gs::launch_gate_set(s->ring_gate + 8 * cur + k, s->s_comm));
+    }
+  } else if (s->emulate) {
     if (comm_model(s, buf, gather_bytes(s))) return -1;
   } else {
     GS_NCCL(ncclAllGather(buf + (size_t)s->cfg.rank * s->L.n_local * row_bytes(s), buf, count,
                           s->esz == 4 ? ncclFloat32 : ncclFloat64, s->comm, s->s_comm));
   }
   GS_MARK(g1, g, s->s_comm);
-  if (gate) GS_HIP(gs::launch_gate_set(s->gate_buf + cur, s->s_comm));
+  if (gate && !(s->sym_ring && use_sym(s)))
+    GS_HIP(gs::launch_gate_set(s->gate_buf + cur, s->s_comm));
   GS_HIP(hipEventRecord(s->ev_gathered, s->s_comm));
   s->full[cur] = true;
   return 0;
@@ -623,7 +644,10 @@ int enqueue_sym(gs_stepper* s, int cur, bool need_gather, bool gathered_external
   // this stepper (RCCL or modeled) and one band (the gated launch covers every unit).
   const bool gated = part == 3 && need_gather && !gathered_externally && xcomm(s) &&
                      s->sym_overlap == 3 && s->sym_band >= a.rows && s->sym_lf;
-  if (gated) a.gate = s->gate_buf + cur;
+  if (gated) {
+    a.gate = s->sym_ring ? s->ring_gate + 8 * cur : s->gate_buf + cur;
+    a.gate_n = s->sym_ring ? 8 : 1;
+  }
   if (part & 1) {
     if (need_gather) {
       if (gathered_externally) s->full[cur] = true;
@@ -1039,6 +1063,8 @@ int gs_stepper_create(const gs_config* cfg, gs_stepper** out) {
   }
   FAIL_CLEAN(hipMalloc(&s->mass_dev, (size_t)s->L.n_pad * sizeof(double)));
   FAIL_CLEAN(hipMalloc(&s->nonfinite, sizeof(unsigned long long)));
+  FAIL_CLEAN(hipMalloc(&s->ring_gate, 16 * sizeof(unsigned)));
+  FAIL_CLEAN(hipMemsetAsync(s->ring_gate, 0, 16 * sizeof(unsigned), s->s_comp));
   // [0..1] gather gates, [2..3] deferral stats, [4..5] dynamic unit-fetch counters
   FAIL_CLEAN(hipMalloc(&s->gate_buf, 8 * sizeof(unsigned)));
   FAIL_CLEAN(hipMemsetAsync(s->gate_buf, 0, 8 * sizeof(unsigned), s->s_comp));
@@ -1052,8 +1078,12 @@ int gs_stepper_create(const gs_config* cfg, gs_stepper** out) {
     long fill = 4L * s->cus;  // two dispatch waves of 2 workgroups per CU
     if (const char* v = getenv("GRAVSIM_SYM_LF_FILL")) fill = atol(v);
     std::vector<int32_t> lf(units - 1);
-    const int64_t got = gs_sym_unit_map(s->L.n_pad, cfg->rank, cfg->nranks, s->parity, fill,
-                                        lf.data(), (int64_t)lf.size());
+    s->sym_ring = cfg->strategy == GS_STRATEGY_RING && cfg->nranks > 1;
+    const int64_t got =
+        s->sym_ring ? gs_sym_unit_map_ring(s->L.n_pad, cfg->rank, cfg->nranks, s->parity, fill,
+                                           lf.data(), (int64_t)lf.size())
+                    : gs_sym_unit_map(s->L.n_pad, cfg->rank, cfg->nranks, s->parity, fill,
+                                      lf.data(), (int64_t)lf.size());
     lf.resize(got > 0 ? (size_t)got : 0);  // 0: geometry too large for the 16-bit fields
     if (!lf.empty()) {
       FAIL_CLEAN(hipMalloc(&s->sym_lf, lf.size() * sizeof(int32_t)));
@@ -1097,7 +1127,8 @@ int gs_stepper_destroy(gs_stepper* s) {
   for (void* p : {s->X[0], s->X[1], s->vel, s->partial, s->acc, (void*)s->mass_dev,
                   (void*)s->nonfinite, (void*)s->sym_Pi, (void*)s->sym_Pj, (void*)s->sym_Pd,
                   (void*)s->sym_S, (void*)s->sym_R, (void*)s->sym_Ti, (void*)s->gate_buf,
-                  (void*)s->defer, (void*)s->sym_lf, s->emu_buf, (void*)s->utrace})
+                  (void*)s->defer, (void*)s->sym_lf, s->emu_buf, (void*)s->utrace,
+                  (void*)s->ring_gate})
     if (p) (void)hipFree(p);
   for (hipEvent_t e : {s->ev_ready, s->ev_gathered, s->ev_t0, s->ev_local, s->ev_end,
                        s->ev_remote, s->ev_fork, s->ev_rem2, s->ev_sym})

@@ -98,6 +98,10 @@ int32_t gs_sym_shell_len(int32_t A, int32_t NC, int32_t parity);
 // Unit order of the gated sym launch for one rank (see layout.cpp); returns the entry count.
 int64_t gs_sym_unit_map(int64_t n_pad, int32_t rank, int32_t nranks, int32_t parity,
                         int64_t fill, int32_t* out, int64_t cap);
+// The same for the ring strategy: entries carry the ring stage (bits 28-30) at which the last
+// slice a unit reads arrives, and units are ordered by stage (rows < 4096, nranks <= 8).
+int64_t gs_sym_unit_map_ring(int64_t n_pad, int32_t rank, int32_t nranks, int32_t parity,
+                             int64_t fill, int32_t* out, int64_t cap);
 
 // ---------------------------------------------------------------- counter-based RNG / ICs (host)
 // Fill bodies [begin, end) of the IC family into fp64 arrays (pos/vel: 3 per body, mass: 1).

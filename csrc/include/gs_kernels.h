@@ -82,7 +82,8 @@ struct SymArgs {
   // that finds it still closed appends itself to defer[1..] (count defer[0]) and exits, and
   // the units-7 launch behind the gather event runs them. Finalize clears gate and count.
   // defer_max: the largest deferred count seen (diagnostics).
-  unsigned* gate;
+  unsigned* gate;        // gate[stage]: all-gather: gate[0]; ring: gate[k] after stage k
+  int32_t gate_n;        // flags finalize re-arms: 1 (all-gather) or 8 (ring stages)
   unsigned* defer;
   unsigned* defer_max;
   const int32_t* lf;    // units 6 order: unit -> row << 16 | segment (bit 31: remote unit)

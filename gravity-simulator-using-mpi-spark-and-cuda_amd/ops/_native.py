@@ -89,6 +89,8 @@ def _declare_common(lib) -> None:
     _sig(lib, "gs_sym_shell_len", c_int32, [c_int32, c_int32, c_int32])
     _sig(lib, "gs_sym_unit_map", c_int64, [c_int64, c_int32, c_int32, c_int32, c_int64,
                                            POINTER(c_int32), c_int64])
+    _sig(lib, "gs_sym_unit_map_ring", c_int64, [c_int64, c_int32, c_int32, c_int32, c_int64,
+                                                POINTER(c_int32), c_int64])
     _sig(lib, "gs_auto_chunk", c_int32, [c_int64])
     _sig(lib, "gs_ic_fill_host", None, [c_int32, c_uint64, c_int64, c_int64, c_int64, _PD, _PD,
                                         _PD])

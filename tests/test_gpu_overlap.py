@@ -16,13 +16,14 @@ from gravsim.config import SimConfig
 pytestmark = pytest.mark.gpu
 
 
-def _emu(monkeypatch, n, P, rank, gbps, overlap):
+def _emu(monkeypatch, n, P, rank, gbps, overlap, strategy="allgather"):
     from gravsim.runtime.engines import HipEngine
 
     monkeypatch.setenv("GRAVSIM_EMULATE_RANK", "1")
     monkeypatch.setenv("GRAVSIM_EMU_COMM_GBPS", str(gbps))
     monkeypatch.setenv("GRAVSIM_EMU_COMM_US", "15")
-    e = HipEngine(SimConfig(n=n, dtype="fp32", device="gpu", mode="sym"), rank, P)
+    e = HipEngine(SimConfig(n=n, dtype="fp32", device="gpu", mode="sym", strategy=strategy),
+                  rank, P)
     e.set_overlap(overlap)
     return e
 
@@ -44,6 +45,30 @@ def test_overlap_modes_same_bits(hip, monkeypatch):
     for pos, vel in res[1:]:
         assert np.array_equal(pos, res[0][0])
         assert np.array_equal(vel, res[0][1])
+
+
+def test_ring_stages_same_bits_and_defer(hip, monkeypatch):
+    """Ring strategy (P-1 modeled neighbour stages, each publishing its own gate): the gated
+    launch equals the ungated one bitwise, and with a slow ring (0.05 GB/s per stage) remote
+    units wait on their own stage's gate or are deferred, with the same bits."""
+    res, deferred = [], []
+    for gbps, ov in ((64, 0), (64, 3), (0.05, 3)):
+        e = _emu(monkeypatch, 262144, 8, 5, gbps, ov, strategy="ring")
+        e.init_ics("solar+random", 2)
+        e.step(2)
+        e.sync()
+        e.set_timing(True)
+        e.step(2)
+        deferred.append(e.phase_stats()["deferred_units"])
+        e.set_timing(False)
+        b = e.state()
+        own = e.layout.real_local
+        res.append((b.pos[own.start:own.stop].copy(), b.vel[own.start:own.stop].copy()))
+        e.close()
+    for pos, vel in res[1:]:
+        assert np.array_equal(pos, res[0][0])
+        assert np.array_equal(vel, res[0][1])
+    assert deferred[0] == 0 and deferred[2] > 0
 
 
 def test_phase_split_reports_modeled_comm(hip, monkeypatch):

@@ -85,6 +85,11 @@ OV3 = {"GRAVSIM_SYM_OVERLAP": "3"}  # one local-first launch, remote units gated
     (4, "allgather", "sym", "fp32", 40000, OV3),
     (8, "allgather", "sym", "fp32", 40000, OV3),
     (2, "allgather", "sym", "fp64", 20000, OV3),
+    # ring strategy of the sym schedule: P-1 neighbour stages, ungated and gated per stage
+    (4, "ring", "sym", "fp32", 20000, None),
+    (2, "ring", "sym", "fp32", 20000, OV3),
+    (4, "ring", "sym", "fp32", 40000, OV3),
+    (8, "ring", "sym", "fp32", 40000, OV3),
     # "sym-graph": capturing the multi-rank step over RCCL's socket transport segfaulted
     # inside a rank in round 1 (profiles/r1_rccl_multi_rank_tests.log); graph capture of the
     # collectives stays opt-in (--graph-comm), is covered on one rank below, and the

@@ -80,3 +80,43 @@ def test_unit_map_permutation_and_locality(n_pad, P, fill):
         if fill != 0:
             first = min(fill if fill > 0 else n, int((~remote).sum()))
             assert not remote[:first].any()  # local units lead the dispatch order
+
+
+@pytest.mark.parametrize("n_pad,P", [(65536, 8), (262144, 4), (1 << 20, 8), (1 << 20, 2),
+                                     (1 << 24, 8)])
+@pytest.mark.parametrize("fill", [-1, 1024, 0])
+def test_ring_unit_map_stages(n_pad, P, fill):
+    """Ring strategy of the sym schedule: the slice of rank (r - k) mod P lands at stage k.
+    Every unit carries the stage of the last slice it reads (0: own rows only), units are a
+    permutation, the local prefix comes first and the rest is ordered by stage."""
+    lib, g = _geo(n_pad)
+    NC, L, S, D = g["NC"], g["L"], g["S"], g["D"]
+    rows = NC // P
+    for rank in (0, P - 1):
+        out = (ctypes.c_int32 * (rows * (S + D)))()
+        n = lib.gs_sym_unit_map_ring(n_pad, rank, P, 1, fill, out, len(out))
+        assert n == rows * (S + D)
+        m = np.frombuffer(out, dtype=np.uint32)
+        remote = (m >> 31).astype(bool)
+        stage = ((m >> 28) & 7).astype(np.int64)
+        row = ((m >> 16) & 0xFFF).astype(np.int64)
+        unit = (m & 0xFFFF).astype(np.int64)
+        key = row * (S + D) + unit
+        assert np.array_equal(np.sort(key), np.arange(rows * (S + D)))
+        assert np.array_equal(remote, stage > 0)
+        A = rank * rows + row
+        h = np.array([lib.gs_sym_shell_len(int(x), NC, 1) for x in range(NC)])[A]
+        want = np.zeros(len(m), dtype=np.int64)
+        for i in np.nonzero((unit < S) & (unit * L < 16 * h))[0]:
+            q0, q1 = unit[i] * L, (unit[i] + 1) * L - 1
+            for d in range(1 + q0 // 16, 2 + q1 // 16):
+                owner = ((A[i] + d) % NC) // rows
+                want[i] = max(want[i], (rank - owner) % P)
+        assert np.array_equal(stage, want)
+        local_prefix = int(np.argmax(stage > 0)) if (stage > 0).any() else len(stage)
+        assert (np.diff(stage[local_prefix:]) >= 0).all()  # stage order after the prefix
+        if fill != 0:
+            assert not remote[:min(fill if fill > 0 else n, int((~remote).sum()))].any()
+    # too many rows for the 12-bit row field: no gated ring map (the launch stays ungated)
+    big = 1 << 25
+    assert lib.gs_sym_unit_map_ring(big, 0, 1, 1, -1, None, 0) == 0
