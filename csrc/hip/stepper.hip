@@ -1065,7 +1065,7 @@ int gs_stepper_create(const gs_config* cfg, gs_stepper** out) {
   FAIL_CLEAN(hipMalloc(&s->nonfinite, sizeof(unsigned long long)));
   FAIL_CLEAN(hipMalloc(&s->ring_gate, 16 * sizeof(unsigned)));
   FAIL_CLEAN(hipMemsetAsync(s->ring_gate, 0, 16 * sizeof(unsigned), s->s_comp));
-  // [0..1] gather gates, [2..3] deferral stats, [4..5] dynamic unit-fetch counters
+  // [0..1] gather gates, [2..3] deferral stats, [4] dynamic unit-fetch counter
   FAIL_CLEAN(hipMalloc(&s->gate_buf, 8 * sizeof(unsigned)));
   FAIL_CLEAN(hipMemsetAsync(s->gate_buf, 0, 8 * sizeof(unsigned), s->s_comp));
   if (s->L.mode == GS_MODE_SYM) {
