@@ -94,7 +94,8 @@ OV3 = {"GRAVSIM_SYM_OVERLAP": "3"}  # one local-first launch, remote units gated
     # inside a rank in round 1 (profiles/r1_rccl_multi_rank_tests.log); graph capture of the
     # collectives stays opt-in (--graph-comm), is covered on one rank below, and the
     # multi-process case runs only on request (GRAVSIM_TEST_GRAPH_COMM=1).
-    *([(2, "allgather", "sym-graph", "fp32", 20000, None),
+    *([(2, "allgather", "auto-graph", "fp32", 5000, None),  # split: all-gather only
+       (2, "allgather", "sym-graph", "fp32", 20000, None),
        (4, "allgather", "sym-graph", "fp32", 20000, None),
        (4, "allgather", "sym-graph", "fp32", 40000, OV3)]
       if os.environ.get("GRAVSIM_TEST_GRAPH_COMM") == "1" else []),
