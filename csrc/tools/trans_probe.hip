@@ -1,0 +1,105 @@
+// Probe: does v_rsq_f32 overlap with packed-f32 VALU work on gfx950, and does the answer
+// depend on where the rsq sits in the stream (burst vs spaced) and on waves per SIMD?
+// The sym force tile issues 2 v_rsq_f32 per 16 v_pk_* (gs_sym_tile.h::meet_jp) in bursts
+// of 8; this measures the same mix with exact instruction order (inline asm, so the
+// compiler cannot re-schedule it) at 1, 2 and 4 waves per SIMD.
+//   mode 0: 64 v_pk_fma_f32 only
+//   mode 1: 8 v_rsq_f32 only
+//   mode 2: 8 rsq burst, then 64 pk_fma          (today's shape)
+//   mode 3: (1 rsq + 8 pk_fma) x 8               (spaced)
+//   mode 4: (2 rsq + 16 pk_fma) x 4              (pairs spaced)
+// Output: one JSON line per (mode, waves/SIMD): ns per wave-iteration per SIMD.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+#define PK(k) "v_pk_fma_f32 %" #k ", %" #k ", %[m], %[c]\n"
+#define RSQ(k) "v_rsq_f32 %" #k ", %" #k "\n"
+#define PK8A PK(0) PK(1) PK(2) PK(3) PK(4) PK(5) PK(6) PK(7)
+#define PK8B PK(8) PK(9) PK(10) PK(11) PK(12) PK(13) PK(14) PK(15)
+#define PK16 PK8A PK8B
+#define OPS                                                                                  \
+  "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7), "+v"(a8), \
+      "+v"(a9), "+v"(a10), "+v"(a11), "+v"(a12), "+v"(a13), "+v"(a14), "+v"(a15), "+v"(r0), \
+      "+v"(r1), "+v"(r2), "+v"(r3), "+v"(r4), "+v"(r5), "+v"(r6), "+v"(r7)
+#define INS [m] "v"(m), [c] "v"(c)
+
+template <int MODE>
+__global__ __launch_bounds__(256) void probe(float* out, int iters, float s) {
+  f2 a0 = s + threadIdx.x, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5,
+     a6 = a0 + 6, a7 = a0 + 7, a8 = a0 + 8, a9 = a0 + 9, a10 = a0 + 10, a11 = a0 + 11,
+     a12 = a0 + 12, a13 = a0 + 13, a14 = a0 + 14, a15 = a0 + 15;
+  float r0 = s + 1, r1 = s + 2, r2 = s + 3, r3 = s + 4, r4 = s + 5, r5 = s + 6, r6 = s + 7,
+        r7 = s + 8;
+  const f2 m = f2(0.999f), c = f2(1e-3f);
+  for (int it = 0; it < iters; ++it) {
+    if constexpr (MODE == 0) {
+      asm volatile(PK16 PK16 PK16 PK16 : OPS : INS);
+    } else if constexpr (MODE == 1) {
+      asm volatile(RSQ(16) RSQ(17) RSQ(18) RSQ(19) RSQ(20) RSQ(21) RSQ(22) RSQ(23) : OPS : INS);
+    } else if constexpr (MODE == 2) {
+      asm volatile(RSQ(16) RSQ(17) RSQ(18) RSQ(19) RSQ(20) RSQ(21) RSQ(22) RSQ(23)
+                   PK16 PK16 PK16 PK16 : OPS : INS);
+    } else if constexpr (MODE == 3) {
+      asm volatile(RSQ(16) PK8A RSQ(17) PK8B RSQ(18) PK8A RSQ(19) PK8B RSQ(20) PK8A RSQ(21)
+                   PK8B RSQ(22) PK8A RSQ(23) PK8B : OPS : INS);
+    } else {
+      asm volatile(RSQ(16) RSQ(17) PK16 RSQ(18) RSQ(19) PK16 RSQ(20) RSQ(21) PK16 RSQ(22)
+                   RSQ(23) PK16 : OPS : INS);
+    }
+  }
+  f2 t = a0 + a1 + a2 + a3 + a4 + a5 + a6 + a7 + a8 + a9 + a10 + a11 + a12 + a13 + a14 + a15;
+  out[blockIdx.x * blockDim.x + threadIdx.x] = t.x + t.y + r0 + r1 + r2 + r3 + r4 + r5 + r6 + r7;
+}
+
+#define CHECK(x)                                                              \
+  do {                                                                        \
+    hipError_t e_ = (x);                                                      \
+    if (e_ != hipSuccess) {                                                   \
+      fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e_));                 \
+      exit(1);                                                                \
+    }                                                                         \
+  } while (0)
+
+template <int MODE>
+static void run(const char* name, float* out, int cus, int iters) {
+  for (int wps = 1; wps <= 4; wps *= 2) {
+    const int blocks = cus * wps;  // 256 threads = one wave per SIMD per block
+    hipEvent_t e0, e1;
+    CHECK(hipEventCreate(&e0));
+    CHECK(hipEventCreate(&e1));
+    probe<MODE><<<blocks, 256>>>(out, iters / 10, 1.0f);  // warm-up
+    CHECK(hipGetLastError());
+    CHECK(hipEventRecord(e0));
+    probe<MODE><<<blocks, 256>>>(out, iters, 1.0f);
+    CHECK(hipEventRecord(e1));
+    CHECK(hipEventSynchronize(e1));
+    float ms = 0;
+    CHECK(hipEventElapsedTime(&ms, e0, e1));
+    // ns per wave-iteration per SIMD: every SIMD runs wps waves x iters iterations.
+    const double ns = ms * 1e6 / (double(iters) * wps);
+    printf("{\"mode\": \"%s\", \"waves_per_simd\": %d, \"ms\": %.4f, \"ns_per_iter\": %.3f}\n",
+           name, wps, ms, ns);
+    CHECK(hipEventDestroy(e0));
+    CHECK(hipEventDestroy(e1));
+  }
+}
+
+int main(int argc, char** argv) {
+  int iters = argc > 1 ? atoi(argv[1]) : 20000;
+  hipDeviceProp_t p;
+  CHECK(hipGetDeviceProperties(&p, 0));
+  const int cus = p.multiProcessorCount;
+  float* out;
+  CHECK(hipMalloc(&out, sizeof(float) * cus * 4 * 256));
+  run<0>("64 pk_fma", out, cus, iters);
+  run<1>("8 rsq", out, cus, iters);
+  run<2>("8 rsq burst + 64 pk_fma", out, cus, iters);
+  run<3>("(rsq + 8 pk_fma) x8", out, cus, iters);
+  run<4>("(2 rsq + 16 pk_fma) x4", out, cus, iters);
+  CHECK(hipFree(out));
+  return 0;
+}
