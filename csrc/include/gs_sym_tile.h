@@ -132,6 +132,13 @@ __device__ __forceinline__ f2 pk_fma(f2 a, f2 b, f2 c) { return __builtin_elemen
 #ifndef GS_SYM_U
 #define GS_SYM_U 2
 #endif
+// r^-3 from rsq cubed (0) or rcp(r^2) * rsq(r^2) (1), fp32 tiles. 1 trades a v_pk_mul for a
+// second transcendental and measured 7.9 % slower (1M 177.2 vs 164.3 ms, 65K 0.788 vs
+// 0.726 ms, alternating runs, profiles/r2_rcp_ab.jsonl): the trans pipe is not free here,
+// although an isolated stream hides 8 rsq behind 64 v_pk_fma (profiles/r2_trans_probe.jsonl).
+#ifndef GS_SYM_RCP
+#define GS_SYM_RCP 0
+#endif
 // All I i-bodies of the lane against one j-body (xj, yj, zj, mj): i-side accumulators updated;
 // with SYM the j side's sum over the lane's i-bodies is returned as t (two packed halves).
 // EXACT: the reference hard cutoff (cuda.cu:39, mpi.c:64), r^-3 := 0 when r^2 < cut2, so
@@ -168,10 +175,21 @@ __device__ __forceinline__ void meet_j(ISet<I>& a, float xj, float yj, float zj,
       y[u].y = __builtin_amdgcn_rsqf(r2[u].y);
 #endif
     }
+#if GS_SYM_RCP
+    // r^-3 = rcp(r^2) * rsq(r^2) (A/B variant, see GS_SYM_RCP)
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      y3[u].x = __builtin_amdgcn_rcpf(r2[u].x);
+      y3[u].y = __builtin_amdgcn_rcpf(r2[u].y);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) y3[u] = y3[u] * y[u];
+#else
 #pragma unroll
     for (int u = 0; u < U; ++u) y3[u] = y[u] * y[u];
 #pragma unroll
     for (int u = 0; u < U; ++u) y3[u] = y3[u] * y[u];
+#endif
     if constexpr (EXACT) {
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -404,10 +422,21 @@ __device__ __forceinline__ void meet_jp(ISetP<I>& a, f2 xj, f2 yj, f2 zj, f2 mj,
       y[u].x = __builtin_amdgcn_rsqf(r2[u].x);
       y[u].y = __builtin_amdgcn_rsqf(r2[u].y);
     }
+#if GS_SYM_RCP
+    // r^-3 = rcp(r^2) * rsq(r^2) (A/B variant, see GS_SYM_RCP)
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      y3[u].x = __builtin_amdgcn_rcpf(r2[u].x);
+      y3[u].y = __builtin_amdgcn_rcpf(r2[u].y);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) y3[u] = y3[u] * y[u];
+#else
 #pragma unroll
     for (int u = 0; u < U; ++u) y3[u] = y[u] * y[u];
 #pragma unroll
     for (int u = 0; u < U; ++u) y3[u] = y3[u] * y[u];
+#endif
     if constexpr (EXACT) {
 #pragma unroll
       for (int u = 0; u < U; ++u) {

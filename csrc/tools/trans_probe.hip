@@ -8,7 +8,11 @@
 //   mode 2: 8 rsq burst, then 64 pk_fma          (today's shape)
 //   mode 3: (1 rsq + 8 pk_fma) x 8               (spaced)
 //   mode 4: (2 rsq + 16 pk_fma) x 4              (pairs spaced)
+//   mode 5: 120 v_fma_f32 (24 chains): the same lane-FMA count unpacked
 // Output: one JSON line per (mode, waves/SIMD): ns per wave-iteration per SIMD.
+// Result (profiles/r2_trans_probe.jsonl, 2 waves/SIMD): 64 pk_fma 136 ns, + 8 rsq in any
+// placement 140-143 ns, 120 fma 191 ns. In the sym tile a second transcendental per pair
+// (GS_SYM_RCP) still cost 7.9 %: there the trans results feed the next instructions.
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -55,6 +59,31 @@ __global__ __launch_bounds__(256) void probe(float* out, int iters, float s) {
   out[blockIdx.x * blockDim.x + threadIdx.x] = t.x + t.y + r0 + r1 + r2 + r3 + r4 + r5 + r6 + r7;
 }
 
+#define F(k) "v_fma_f32 %" #k ", %" #k ", %[m], %[c]\n"
+#define F24                                                                                  \
+  F(0) F(1) F(2) F(3) F(4) F(5) F(6) F(7) F(8) F(9) F(10) F(11) F(12) F(13) F(14) F(15) F(16) \
+      F(17) F(18) F(19) F(20) F(21) F(22) F(23)
+
+__global__ __launch_bounds__(256) void probe_fma(float* out, int iters, float s) {
+  float v[24];
+#pragma unroll
+  for (int k = 0; k < 24; ++k) v[k] = s + k + threadIdx.x;
+  const float m = 0.999f, c = 1e-3f;
+  for (int it = 0; it < iters; ++it) {
+    asm volatile(F24 F24 F24 F24 F24
+                 : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]),
+                   "+v"(v[6]), "+v"(v[7]), "+v"(v[8]), "+v"(v[9]), "+v"(v[10]), "+v"(v[11]),
+                   "+v"(v[12]), "+v"(v[13]), "+v"(v[14]), "+v"(v[15]), "+v"(v[16]),
+                   "+v"(v[17]), "+v"(v[18]), "+v"(v[19]), "+v"(v[20]), "+v"(v[21]),
+                   "+v"(v[22]), "+v"(v[23])
+                 : [m] "v"(m), [c] "v"(c));
+  }
+  float t = 0;
+#pragma unroll
+  for (int k = 0; k < 24; ++k) t += v[k];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = t;
+}
+
 #define CHECK(x)                                                              \
   do {                                                                        \
     hipError_t e_ = (x);                                                      \
@@ -65,16 +94,24 @@ __global__ __launch_bounds__(256) void probe(float* out, int iters, float s) {
   } while (0)
 
 template <int MODE>
+static void launch(int blocks, float* out, int iters) {
+  if constexpr (MODE == 5)
+    probe_fma<<<blocks, 256>>>(out, iters, 1.0f);
+  else
+    probe<MODE><<<blocks, 256>>>(out, iters, 1.0f);
+}
+
+template <int MODE>
 static void run(const char* name, float* out, int cus, int iters) {
   for (int wps = 1; wps <= 4; wps *= 2) {
     const int blocks = cus * wps;  // 256 threads = one wave per SIMD per block
     hipEvent_t e0, e1;
     CHECK(hipEventCreate(&e0));
     CHECK(hipEventCreate(&e1));
-    probe<MODE><<<blocks, 256>>>(out, iters / 10, 1.0f);  // warm-up
+    launch<MODE>(blocks, out, iters);  // warm-up at full length (clock settles)
     CHECK(hipGetLastError());
     CHECK(hipEventRecord(e0));
-    probe<MODE><<<blocks, 256>>>(out, iters, 1.0f);
+    launch<MODE>(blocks, out, iters);
     CHECK(hipEventRecord(e1));
     CHECK(hipEventSynchronize(e1));
     float ms = 0;
@@ -95,11 +132,14 @@ int main(int argc, char** argv) {
   const int cus = p.multiProcessorCount;
   float* out;
   CHECK(hipMalloc(&out, sizeof(float) * cus * 4 * 256));
-  run<0>("64 pk_fma", out, cus, iters);
-  run<1>("8 rsq", out, cus, iters);
-  run<2>("8 rsq burst + 64 pk_fma", out, cus, iters);
-  run<3>("(rsq + 8 pk_fma) x8", out, cus, iters);
-  run<4>("(2 rsq + 16 pk_fma) x4", out, cus, iters);
+  for (int rep = 0; rep < 2; ++rep) {  // two passes: the second is on a warm clock
+    run<0>("64 pk_fma", out, cus, iters);
+    run<5>("120 fma", out, cus, iters);
+    run<1>("8 rsq", out, cus, iters);
+    run<2>("8 rsq burst + 64 pk_fma", out, cus, iters);
+    run<3>("(rsq + 8 pk_fma) x8", out, cus, iters);
+    run<4>("(2 rsq + 16 pk_fma) x4", out, cus, iters);
+  }
   CHECK(hipFree(out));
   return 0;
 }
