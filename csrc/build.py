@@ -40,6 +40,8 @@ MICRO_SRC = CSRC / "tools" / "microbench.hip"
 MICRO_BIN = OUT / "microbench"
 PROBE_SRC = CSRC / "tools" / "sym_probe.hip"
 PROBE_BIN = OUT / "sym_probe"
+TRANS_SRC = CSRC / "tools" / "trans_probe.hip"
+TRANS_BIN = OUT / "trans_probe"
 
 
 def _stale(target: Path, deps: list[Path]) -> bool:
@@ -122,18 +124,31 @@ def build_sym_probe(force: bool = False) -> Path:
     return PROBE_BIN
 
 
+def build_trans_probe(force: bool = False) -> Path:
+    """Transcendental / packed-VALU issue probe (csrc/tools/trans_probe.hip)."""
+    OUT.mkdir(parents=True, exist_ok=True)
+    if TRANS_SRC.exists() and (force or _stale(TRANS_BIN, [TRANS_SRC])):
+        tmp = TRANS_BIN.with_suffix(".tmp")
+        _run([hipcc(), "-O3", "-std=c++17", f"--offload-arch={ARCH}", str(TRANS_SRC), "-o",
+              str(tmp)])
+        os.replace(tmp, TRANS_BIN)
+    return TRANS_BIN
+
+
 def build_all(force: bool = False) -> None:
     build_cpu(force)
     build_hip(force)
     build_tool(force)
     build_microbench(force)
     build_sym_probe(force)
+    build_trans_probe(force)
 
 
 def main(argv: list[str] | None = None) -> int:
     ap = argparse.ArgumentParser(description=__doc__)
     ap.add_argument("--force", action="store_true")
-    ap.add_argument("--only", choices=["cpu", "hip", "tool", "microbench", "sym_probe"])
+    ap.add_argument("--only", choices=["cpu", "hip", "tool", "microbench", "sym_probe",
+                                          "trans_probe"])
     a = ap.parse_args(argv)
     if a.only == "cpu":
         build_cpu(a.force)
@@ -145,6 +160,8 @@ def main(argv: list[str] | None = None) -> int:
         build_microbench(a.force)
     elif a.only == "sym_probe":
         build_sym_probe(a.force)
+    elif a.only == "trans_probe":
+        build_trans_probe(a.force)
     else:
         build_all(a.force)
     return 0
