@@ -691,7 +691,10 @@ int enqueue_step(gs_stepper* s, bool capturing, bool gathered_externally) {
     GS_HIP(hipEventRecord(s->ev_fork, s->s_comp));
     GS_HIP(hipStreamWaitEvent(s->s_rem, s->ev_fork, 0));
     GS_HIP(hipStreamWaitEvent(s->s_rem2, s->ev_fork, 0));
-    if (s->have_comm) GS_HIP(hipStreamWaitEvent(s->s_comm, s->ev_fork, 0));
+    if (s->have_comm) {
+      GS_HIP(hipStreamWaitEvent(s->s_comm, s->ev_fork, 0));
+      GS_MARK(g0, g, s->s_comm);  // the ring's P-1 transfers are the step's gather span
+    }
     if (ring_compute<T>(s, a, 0, nullptr)) return -1;
     for (int sub = 1; sub < s->cfg.nranks; ++sub) {
       hipEvent_t ready = nullptr;
@@ -702,6 +705,7 @@ int enqueue_step(gs_stepper* s, bool capturing, bool gathered_externally) {
       }
       if (ring_compute<T>(s, a, sub, ready)) return -1;
     }
+    if (s->have_comm) GS_MARK(g1, g, s->s_comm);
     if (ring_finish<T>(s, a)) return -1;
     if (timed) GS_HIP(hipEventRecord(s->ev_end, s->s_comp));
     if (s->pe) GS_HIP(hipEventRecord(s->pe->end, s->s_comp));

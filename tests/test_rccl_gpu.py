@@ -63,6 +63,15 @@ def _worker(rank, world, port, out_dir, n, steps, strategy="allgather", mode="au
                 np.save(os.path.join(out_dir, "pos.npy"), b.pos)
                 with open(os.path.join(out_dir, "mode.txt"), "w") as f:
                     f.write(str(eng.native_layout["mode"]))
+            # two more steps with phase events (after the saved state; state() gathered the
+            # current buffer, so the second step is the one that runs the collectives)
+            eng.set_timing(True)
+            eng.step(2)
+            ps = eng.phase_stats()
+            eng.set_timing(False)
+            if rank == 0:
+                with open(os.path.join(out_dir, "comm_ms.txt"), "w") as f:
+                    f.write(repr(ps["comm_ms"]))
         eng.close()
     finally:
         if rank == 0:
@@ -124,6 +133,8 @@ def test_rccl_multi_rank_match_single_rank(hip, tmp_path, world, strategy, mode,
     assert np.array_equal(np.load(tmp_path / "pos.npy"), ref.pos)
     vel = np.concatenate([np.load(tmp_path / f"vel{r}.npy") for r in range(world)])
     assert np.array_equal(vel, ref.vel)
+    # every multi-rank schedule times its collectives (all-gather or ring stages + exchange)
+    assert float(open(tmp_path / "comm_ms.txt").read()) > 0.0
 
 
 @pytest.mark.parametrize("graph,strategy", [(1, "allgather"), (2, "allgather"), (1, "ring"),
