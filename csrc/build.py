@@ -75,6 +75,12 @@ def build_cpu(force: bool = False) -> Path:
 # SLP vectorisation packs the per-lane i-bodies into v_pk_{add,mul,fma}_f32; GRAVSIM_SLP=0
 # builds the scalar-VALU variant for A/B runs.
 HIP_FLAGS = ["-O3", "-std=c++17", f"--offload-arch={ARCH}", "-ffp-contract=off", "-fPIC"]
+# The backend's max-ILP machine scheduler: same instructions (same bits), better interleaving
+# of the packed-f32 / v_rsq streams. Alternating builds: 1M sym 164.9-165.2 vs 165.5 ms, 65K
+# 0.717-0.718 vs 0.721-0.722 ms, 256K split 15.07-15.09 vs 16.56 ms, 512K fp64 sym even
+# (profiles/r2_sched_strategy_ab.jsonl, r2_sched_max_ilp_fp64_split_ab.jsonl).
+if os.environ.get("GRAVSIM_SCHED", "max-ilp") != "default":
+    HIP_FLAGS += ["-mllvm", f"-amdgpu-sched-strategy={os.environ.get('GRAVSIM_SCHED', 'max-ilp')}"]
 if os.environ.get("GRAVSIM_SLP", "1") == "0":
     HIP_FLAGS.append("-fno-slp-vectorize")
 HIP_FLAGS += os.environ.get("GRAVSIM_HIP_EXTRA", "").split()
