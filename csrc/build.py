@@ -77,8 +77,10 @@ def build_cpu(force: bool = False) -> Path:
 HIP_FLAGS = ["-O3", "-std=c++17", f"--offload-arch={ARCH}", "-ffp-contract=off", "-fPIC"]
 # The backend's max-ILP machine scheduler: same instructions (same bits), better interleaving
 # of the packed-f32 / v_rsq streams. Alternating builds: 1M sym 164.9-165.2 vs 165.5 ms, 65K
-# 0.717-0.718 vs 0.721-0.722 ms, 256K split 15.07-15.09 vs 16.56 ms, 512K fp64 sym even
-# (profiles/r2_sched_strategy_ab.jsonl, r2_sched_max_ilp_fp64_split_ab.jsonl).
+# 0.717-0.718 vs 0.721-0.722 ms, 256K split 15.07-15.09 vs 16.56 ms, 8K fused 0.165 vs
+# 0.198 ms, 128K sym -0.5 %, 256K fp64 split -1.8 %, 512K fp64 sym even
+# (profiles/r2_sched_strategy_ab.jsonl, r2_sched_max_ilp_*_ab.jsonl). The auto schedule
+# thresholds still hold with it (profiles/r2_s4_sizes_maxilp.txt).
 if os.environ.get("GRAVSIM_SCHED", "max-ilp") != "default":
     HIP_FLAGS += ["-mllvm", f"-amdgpu-sched-strategy={os.environ.get('GRAVSIM_SCHED', 'max-ilp')}"]
 if os.environ.get("GRAVSIM_SLP", "1") == "0":
