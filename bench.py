@@ -274,7 +274,7 @@ def main(argv=None) -> int:
                 **kernel_info,
                 "cutoff_path": "exact-select" if fmode["exact"] else
                 f"fast (core^2={fmode['eps2']:.3g} m^2; bit-identical to the 1e-10 m hard cutoff "
-                "for separations above ~mm)",
+                "for separations above ~1 cm)",
                 "graph": bool(a.graph and (world == 1 or a.graph_comm)),
                 "overlap": overlap,
                 "overlap_check": overlap_check,

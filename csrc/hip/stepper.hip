@@ -411,10 +411,16 @@ void resolve_force_mode(gs_stepper* s) {
   const double core2 = fmax(pow(mu_max / big, 2.0 / 3.0), floor2);
   const double soft2 = s->cfg.softening * s->cfg.softening;
   const double cut2 = s->cfg.cutoff * s->cfg.cutoff;
-  const double fast_eps2 = fmax(soft2, core2);
+  // fp64: the core is ~1e-190 m^2, far inside the cutoff, so the fast path softens at the
+  // cutoff scale instead (eps2 = cut^2): r^2 + eps2 rounds to r^2 for every pair with
+  // r^2 >= 2^53 eps2, i.e. r >= ~1 cm at the reference's 1e-10 m, the same guarantee fp32's
+  // core gives. auto takes it while that radius is <= 1 cm (the select costs 7 % at 512K
+  // fp64: 106.9 vs 99.2 ms, profiles/r2_fp64_fast_cutoff.txt).
+  const double fast_eps2 = s->esz == 8 ? fmax(fmax(soft2, core2), cut2) : fmax(soft2, core2);
   bool exact;
   if (s->cfg.cutoff_mode == 1) exact = true;
   else if (s->cfg.cutoff_mode == 2) exact = false;
+  else if (s->esz == 8) exact = fast_eps2 * 0x1p53 > 1e-4;
   else exact = cut2 > fast_eps2;
   s->exact = exact;
   s->eps2 = exact ? soft2 : fast_eps2;

@@ -32,8 +32,8 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--cutoff", type=float, default=d.cutoff)
     p.add_argument("--softening", type=float, default=d.softening)
     p.add_argument("--cutoff-mode", choices=["auto", "exact", "fast"], default=d.cutoff_mode,
-                   help="GPU force path: exact hard-cutoff select, or fast (cutoff inside an "
-                        "overflow-safe core; bit-identical for separations above ~mm)")
+                   help="GPU force path: exact hard-cutoff select, or fast (r^2 + a core of "
+                        "the cutoff scale, no select; bit-identical for separations above ~1 cm)")
     p.add_argument("--integrator", choices=["kd", "leapfrog"], default=d.integrator,
                    help="kd: the reference's kick-drift update; leapfrog: the same kernel on "
                         "half-step-staggered velocities (second order)")

@@ -252,6 +252,16 @@ def test_auto_cutoff_mode_resolution(hip):
     eng.init_ics("solar+random", 1)
     assert eng.force_mode()["exact"]
     eng.close()
+    # fp64: the fast path softens at the cutoff scale (bit-identical above ~1 cm)
+    eng = _engine(100, "fp64")
+    eng.init_ics("solar+random", 1)
+    fm = eng.force_mode()
+    assert not fm["exact"] and fm["eps2"] == pytest.approx(1e-20)
+    eng.close()
+    eng = _engine(100, "fp64", cutoff=1e3)
+    eng.init_ics("solar+random", 1)
+    assert eng.force_mode()["exact"]
+    eng.close()
 
 
 def test_fast_path_self_term_zero_with_coincident_bodies(hip):
