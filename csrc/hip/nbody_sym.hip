@@ -614,6 +614,10 @@ __global__ __launch_bounds__(192) void sym_tail_kernel(SymArgs a) {
     __hip_atomic_store(a.gate + threadIdx.x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (a.gate && blockIdx.x == 0 && threadIdx.x == 0)
     __hip_atomic_store(a.defer, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // re-arm the dynamic unit counter of the force launch that preceded this kernel (the
+  // stepper then skips the next launch's memset: SymArgs::work_zero)
+  if (a.work && blockIdx.x == 0 && threadIdx.x == 0)
+    __hip_atomic_store(a.work, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const int64_t gi = a.i_begin + li;
   const bool real = li < a.n_local && gi < a.n_real;
   if (real) {
@@ -705,9 +709,12 @@ hipError_t launch_force_sym_t(const SymArgs& a, hipStream_t s) {
   unsigned g = (unsigned)units;
   if (a.work && (a.units == 0 || a.units == 6) && a.unit_cap > 1 && units > a.first_wave) {
     // the counter starts at 0 for every launch: a stream-ordered memset (a graph node when
-    // captured), not state carried over from the previous launch
-    const hipError_t e = hipMemsetAsync(a.work, 0, sizeof(unsigned), s);
-    if (e != hipSuccess) return e;
+    // captured), unless the fused tail kernel that ran after the previous launch on this
+    // stream already re-armed it (work_zero; saves a launch per step at small N)
+    if (!a.work_zero) {
+      const hipError_t e = hipMemsetAsync(a.work, 0, sizeof(unsigned), s);
+      if (e != hipSuccess) return e;
+    }
     // first wave: one unit per workgroup; the rest: up to unit_cap each, with 25 % slack so
     // a fast XCD can take more than its rotation share
     const int64_t rest = units - a.first_wave;

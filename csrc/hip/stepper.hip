@@ -164,6 +164,7 @@ struct gs_stepper {
   int64_t prog_rec = 0, prog_done = 0;
   double step_timeout_s = 0.0;  // 0: unbounded
   bool graph_failed = false;    // multi-rank capture refused: eager fallback
+  bool work_zero = true;        // sym dynamic unit counter (gate_buf[4]) known to be 0
 };
 
 namespace {
@@ -578,6 +579,15 @@ int ring_finish(gs_stepper* s, const gs::KArgs<T>& a) {
 // (profiles/r2_fused_tail_ab.jsonl): 65K 0.707 vs 0.708 ms, 256K 10.51 vs 10.57 ms, but 1M
 // 166.8 vs 166.1 ms, where the fused kernel's 8x fewer threads for the group sums lose.
 // GRAVSIM_SYM_FUSED_TAIL=0 / 1 forces the three-kernel / fused tail at any size.
+// Every sym force launch goes through here: it tells the launcher whether the dynamic unit
+// counter is known to be 0 (re-armed by the fused tail kernel enqueued after the previous
+// launch on this stream), then marks it dirty until the next fused tail.
+hipError_t force_sym_launch(gs_stepper* s, gs::SymArgs a, hipStream_t st) {
+  a.work_zero = s->work_zero ? 1 : 0;
+  s->work_zero = false;
+  return gs::launch_force_sym(a, st);
+}
+
 bool fused_tail(const gs_stepper* s) {
   const bool size_ok = s->fuse_tail > 0 || (s->fuse_tail < 0 && s->sym_NC <= 128);
   return size_ok && s->cfg.nranks == 1 && !multi(s) && s->sym_band >= s->sym_NC;
@@ -594,20 +604,20 @@ int sym_force(gs_stepper* s, gs::SymArgs a, bool overlap_gather, bool exchange =
       // 3: one launch with the local units first; remote units run in it once the gather is
       // published, or are deferred to a second launch queued behind the gather event.
       a.units = 6;
-      GS_HIP(gs::launch_force_sym(a, s->s_comp));
+      GS_HIP(force_sym_launch(s, a, s->s_comp));
       GS_MARK(w0, w, s->s_comp);
       GS_HIP(hipStreamWaitEvent(s->s_comp, s->ev_gathered, 0));
       GS_MARK(w1, w, s->s_comp);
       a.units = 7;
-      GS_HIP(gs::launch_force_sym(a, s->s_comp));
+      GS_HIP(force_sym_launch(s, a, s->s_comp));
       a.units = 0;
     } else if (overlap_gather && b0 == 0 && one_band && ov == 1) {
       gs::SymArgs d = a;
       d.units = 1;  // diagonal chunks beside the gather
-      GS_HIP(gs::launch_force_sym(d, s->s_comp));
+      GS_HIP(force_sym_launch(s, d, s->s_comp));
       GS_HIP(hipStreamWaitEvent(s->s_comp, s->ev_gathered, 0));
       a.units = 2;
-      GS_HIP(gs::launch_force_sym(a, s->s_comp));
+      GS_HIP(force_sym_launch(s, a, s->s_comp));
     } else if (overlap_gather && b0 == 0 && one_band && ov == 2) {
       // fork: s_rem starts after everything already on s_comp (X[cur] written) and the gather
       GS_HIP(hipEventRecord(s->ev_fork, s->s_comp));
@@ -615,10 +625,10 @@ int sym_force(gs_stepper* s, gs::SymArgs a, bool overlap_gather, bool exchange =
       GS_HIP(hipStreamWaitEvent(s->s_rem, s->ev_gathered, 0));
       gs::SymArgs r = a;
       r.units = 4;  // shell segments that read gathered rows
-      GS_HIP(gs::launch_force_sym(r, s->s_rem));
+      GS_HIP(force_sym_launch(s, r, s->s_rem));
       GS_HIP(hipEventRecord(s->ev_remote, s->s_rem));
       a.units = 5;  // diagonal + rank-local shell units, beside the gather
-      GS_HIP(gs::launch_force_sym(a, s->s_comp));
+      GS_HIP(force_sym_launch(s, a, s->s_comp));
       GS_HIP(hipStreamWaitEvent(s->s_comp, s->ev_remote, 0));  // join
     } else {
       if (overlap_gather && b0 == 0) {
@@ -626,7 +636,7 @@ int sym_force(gs_stepper* s, gs::SymArgs a, bool overlap_gather, bool exchange =
         GS_HIP(hipStreamWaitEvent(s->s_comp, s->ev_gathered, 0));
         GS_MARK(w1, w, s->s_comp);
       }
-      GS_HIP(gs::launch_force_sym(a, s->s_comp));
+      GS_HIP(force_sym_launch(s, a, s->s_comp));
     }
     if (fused_tail(s)) continue;  // reductions + integrate in sym_tail_kernel (one band)
     GS_HIP(gs::launch_sym_group_reduce(a, s->s_comp));
@@ -663,8 +673,12 @@ int enqueue_sym(gs_stepper* s, int cur, bool need_gather, bool gathered_external
     if (timed) GS_HIP(hipEventRecord(s->ev_local, s->s_comp));
   }
   if (part & 2) {
-    if (fused_tail(s)) GS_HIP(gs::launch_sym_tail(a, s->s_comp));
-    else GS_HIP(gs::launch_sym_finalize(a, s->s_comp));
+    if (fused_tail(s)) {
+      GS_HIP(gs::launch_sym_tail(a, s->s_comp));
+      s->work_zero = true;  // the tail re-armed the unit counter
+    } else {
+      GS_HIP(gs::launch_sym_finalize(a, s->s_comp));
+    }
   }
   return 0;
 }
@@ -875,8 +889,12 @@ int accel_impl(gs_stepper* s, double* acc4, bool step_path) {
       sa.acc_out = s->acc;
       if (sym_force(s, sa, false)) return -1;
       if (xcomm(s) && sym_exchange_rccl(s)) return -1;
-      if (fused_tail(s)) GS_HIP(gs::launch_sym_tail(sa, s->s_comp));
-      else GS_HIP(gs::launch_sym_finalize(sa, s->s_comp));
+      if (fused_tail(s)) {
+        GS_HIP(gs::launch_sym_tail(sa, s->s_comp));
+        s->work_zero = true;
+      } else {
+        GS_HIP(gs::launch_sym_finalize(sa, s->s_comp));
+      }
       GS_HIP(hipStreamSynchronize(s->s_comp));
       std::vector<T> A((size_t)s->L.n_local * 4);
       GS_HIP(hipMemcpy(A.data(), s->acc, A.size() * sizeof(T), hipMemcpyDeviceToHost));
