@@ -790,6 +790,10 @@ int build_graph(gs_stepper* s) {
   const int64_t k0 = s->k;
   const bool f0 = s->full[0], f1 = s->full[1];
   hipGraph_t g = nullptr;
+  // A replayed graph cannot rely on the counter state at capture time: its first sym force
+  // launch always re-zeroes the unit counter (a later one may skip it after a fused tail
+  // inside the graph; the flag left by the capture then matches every replay's end state).
+  s->work_zero = false;
   GS_HIP(hipStreamBeginCapture(s->s_comp, hipStreamCaptureModeThreadLocal));
   int rc = enqueue_step_any(s, true);
   if (rc == 0) rc = enqueue_step_any(s, true);

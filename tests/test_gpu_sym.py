@@ -248,3 +248,23 @@ def test_sym_dynamic_unit_fetch_bitwise(hip, monkeypatch, n, dtype, P, first_wav
         g.close()
     assert np.array_equal(out[0].pos, out[1].pos)
     assert np.array_equal(out[0].vel, out[1].vel)
+
+
+@pytest.mark.parametrize("fused", ["0", "1"])
+def test_sym_graph_replays_rezero_unit_counter(hip, monkeypatch, fused):
+    """A fresh engine whose first steps are hipGraph replays (no eager step or accel query
+    before) must match eager steps bitwise: every replay starts with the dynamic unit counter
+    re-zeroed, whether the graph ends in the fused tail (which re-arms it) or not."""
+    from gravsim.runtime.engines import HipEngine
+
+    monkeypatch.setenv("GRAVSIM_SYM_FUSED_TAIL", fused)
+    out = []
+    for graph in (True, False):
+        e = HipEngine(SimConfig(n=32768, dtype="fp32", device="gpu", mode="sym", graph=graph))
+        e.init_ics("solar+random", 3)
+        e.step(6)
+        e.sync()
+        out.append(e.state())
+        e.close()
+    assert np.array_equal(out[0].pos, out[1].pos)
+    assert np.array_equal(out[0].vel, out[1].vel)
