@@ -21,15 +21,29 @@ anything touches the GPU. Under a launcher, WORLD_SIZE must equal --gpus.
 A step is the full simulation step: all-gather + force + exchange + integrate (no work
 skipped). Data: synthetic Sun/Earth/Mars + uniform random bodies generated on device
 (seeded). Rank 0 prints ONE JSON line; value is the whole-job body-updates/s =
-N * K / max_rank(wall). Outside the timed region: a sampled accuracy check of the step's own
-accelerations (before the warmup) and a few eager steps with phase events for the comm split.
+N * K / max_rank(wall).
+
+Audits of the timed work (outside the timed region; the run exits non-zero if one fails):
+  * unit count: the sym force kernels count every unit they run on device; after the loop
+    each rank must have run exactly rows x (S + D) units per timed step;
+  * replay: the same warmup + K steps are re-run from the same ICs on an independent
+    schedule (eager launches, one static unit per workgroup, ungated) and must give the
+    same bits on every rank.
+Also outside it: the sampled accuracy of the step's own accelerations at step 0 and after
+the last timed step, the relative drift of total momentum over the run, a few eager steps
+with phase events for the comm split, and the reference's exact hard-cutoff select timed
+on its own (exact_cutoff_ms_per_step). Multi-rank runs record per rank the device it bound
+and the RCCL transports its connections used (parsed from RCCL's INFO log, sent to a file).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import re
+import shutil
 import sys
+import tempfile
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -68,7 +82,75 @@ def parse(argv=None) -> argparse.Namespace:
                          "sum on the host (0 = skip)")
     ap.add_argument("--phase-steps", type=int, default=3,
                     help="eager steps with phase events after the timed loop (comm split)")
+    ap.add_argument("--no-replay-audit", dest="replay_audit", action="store_false",
+                    help="skip the independent-schedule re-run of the timed steps")
+    ap.add_argument("--exact-steps", type=int, default=3,
+                    help="steps timed with the reference's exact cutoff select after the "
+                         "headline (0 = skip)")
     return ap.parse_args(argv)
+
+
+def rccl_log_setup() -> str | None:
+    """Route RCCL's INFO log to a private per-rank file (before any RCCL call; stdout stays
+    rank 0's JSON line) so the transport each connection used can be reported. Left alone
+    when the user already configured NCCL_DEBUG."""
+    if "NCCL_DEBUG" in os.environ or "NCCL_DEBUG_FILE" in os.environ:
+        return None
+    d = tempfile.mkdtemp(prefix="gravsim_rccl_")
+    os.environ["NCCL_DEBUG"] = "INFO"
+    os.environ["NCCL_DEBUG_SUBSYS"] = "INIT,P2P,NET"
+    os.environ["NCCL_DEBUG_FILE"] = os.path.join(d, "rccl.log")
+    return os.environ["NCCL_DEBUG_FILE"]
+
+
+def rccl_transports(path: str | None) -> dict:
+    """Transports of this rank's RCCL connections ("Channel .. via P2P/IPC", "NET/Socket",
+    "SHM"...) and the RCCL version, from the INFO log; the file is removed afterwards."""
+    out = {"transports": None, "rccl_version": None, "net": None}
+    if not path or not os.path.exists(path):
+        return out
+    seen, net = set(), set()
+    with open(path, errors="replace") as f:
+        for line in f:
+            m = re.search(r" via (\S+)", line)
+            if m and "Channel" in line:
+                seen.add(re.sub(r"/\d+$", "", m.group(1)))
+            m = re.search(r"(?:RCCL|NCCL) version[ :]+(\S+)", line)
+            if m and out["rccl_version"] is None:
+                out["rccl_version"] = m.group(1)
+            m = re.search(r"Using network (\S+)", line)
+            if m:
+                net.add(m.group(1))
+    out["transports"] = sorted(seen)
+    out["net"] = sorted(net) or None
+    shutil.rmtree(os.path.dirname(path), ignore_errors=True)
+    return out
+
+
+def device_record(dev: int) -> dict:
+    import torch
+
+    p = torch.cuda.get_device_properties(dev)
+    return {"device": dev, "pci": f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}",
+            "arch": p.gcnArchName, "cus": p.multi_processor_count}
+
+
+def own_state(eng):
+    """(positions, velocities) of this rank's real bodies (collective for P > 1)."""
+    b = eng.state()
+    own = eng.layout.real_local
+    return b.pos[own.start:own.stop].copy(), b.vel[own.start:own.stop].copy(), \
+        b.mass[own.start:own.stop].copy()
+
+
+def momentum(dist, comm, vel, mass):
+    """(total momentum vector, sum of m |v|) over all ranks' own bodies."""
+    import numpy as np
+
+    p = (mass[:, None] * vel).sum(axis=0)
+    scale = float((mass * np.linalg.norm(vel, axis=1)).sum())
+    return np.array([comm.allreduce_sum(dist, float(x)) for x in p]), \
+        comm.allreduce_sum(dist, scale)
 
 
 def sampled_error(eng, cfg, samples: int, seed: int = 7) -> float:
@@ -162,12 +244,13 @@ def main(argv=None) -> int:
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE {world_env}: run one rank per GPU "
                          "(torch.distributed.run --nproc-per-node must equal --gpus)")
 
+    import numpy as np
     import torch
 
     import gravsim  # noqa: F401
     from gravsim.config import SimConfig
     from gravsim.ops import _native
-    from gravsim.parallel import comm
+    from gravsim.parallel import comm, launch
     from gravsim.runtime.engines import HipEngine
 
     dist = comm.init()
@@ -185,10 +268,14 @@ def main(argv=None) -> int:
     cfg = SimConfig(n=a.n, dt=a.dt, dtype=a.dtype, device="gpu", kernel=a.kernel, mode=a.mode,
                     ipl=a.ipl, graph=a.graph, graph_comm=a.graph_comm,
                     cutoff_mode=a.cutoff_mode, strategy=a.strategy).validate()
+    rccl_log = rccl_log_setup() if world > 1 else None  # before the first RCCL call
     eng = HipEngine(cfg, rank, world, device=dev, dist=dist)
+    ranks_info = None
     if world > 1:
         uid = HipEngine.unique_id() if rank == 0 else None
         eng.comm_init(comm.broadcast_bytes(dist, uid))
+        rec = {"rank": rank, **device_record(dev), **rccl_transports(rccl_log)}
+        ranks_info = comm.allgather_object(dist, rec)
     sym = _native.MODE_NAMES.get(eng.native_layout["mode"]) == "sym"
     overlap, overlap_check = (0, None)
     if a.overlap != "auto":
@@ -199,13 +286,16 @@ def main(argv=None) -> int:
     eng.init_ics("solar+random", cfg.seed)
     eng.sync()
 
-    # Accuracy of the step's own force path at step 0 (untimed).
+    # Accuracy of the step's own force path at step 0, and the initial momentum (untimed).
     err = sampled_error(eng, cfg, a.check_samples) if a.check_samples > 0 else None
     if err is not None:
         err = comm.allreduce_max(dist, err)
+    _, vel0, mass = own_state(eng)
+    p0, pscale = momentum(dist, comm, vel0, mass)
 
     eng.step(a.warmup)
     eng.sync()
+    eng.audit_reset()
     torch.cuda.synchronize()
     comm.barrier(dist)
     torch.cuda.synchronize()
@@ -217,7 +307,27 @@ def main(argv=None) -> int:
     t1 = time.perf_counter()
     wall = comm.allreduce_max(dist, t1 - t0)
 
+    # ---- audits of the timed work (untimed) --------------------------------------------
+    failures = []
+    done, per_step = eng.audit()
+    if per_step:
+        short = comm.allreduce_sum(dist, 0.0 if done == per_step * a.steps else 1.0)
+        units = {"units_per_step_rank0": per_step,
+                 "units_done_rank0": done, "ranks_short": int(short)}
+        if short:
+            failures.append(f"unit count: {int(short)} rank(s) did not run rows x (S + D) "
+                            f"units per timed step (rank {rank}: {done} of "
+                            f"{per_step * a.steps})")
+    else:
+        units = None  # one-sided schedules: no unit counter, the replay audit still runs
     bad = comm.allreduce_sum(dist, eng.nonfinite())
+    pos_t, vel_t, _ = own_state(eng)
+    p1, _ = momentum(dist, comm, vel_t, mass)
+    drift = float(np.linalg.norm(p1 - p0)) / max(pscale, 1e-300)
+    err_end = sampled_error(eng, cfg, a.check_samples) if a.check_samples > 0 else None
+    if err_end is not None:
+        err_end = comm.allreduce_max(dist, err_end)
+
     # Comm/compute split (untimed): a few eager steps with per-step phase events.
     phase = None
     if a.phase_steps > 0:
@@ -227,8 +337,40 @@ def main(argv=None) -> int:
         eng.set_timing(False)
         for k in ("step_ms", "comm_ms", "exposed_comm_ms", "gather_ms", "exchange_ms"):
             phase[k] = comm.allreduce_max(dist, phase[k])
+
+    # Replay: warmup + K steps from the same ICs on an independent schedule must give the
+    # timed run's bits (eager launches, one static unit per workgroup, no gating).
+    replay = None
+    if a.replay_audit:
+        eng.set_schedule(0, 0)
+        eng.set_overlap(0)
+        eng.init_ics("solar+random", cfg.seed)
+        eng.step(a.warmup + a.steps)
+        eng.sync()
+        pos_r, vel_r, _ = own_state(eng)
+        same = np.array_equal(pos_r, pos_t) and np.array_equal(vel_r, vel_t)
+        diff = comm.allreduce_sum(dist, 0.0 if same else 1.0)
+        replay = "bitwise" if not diff else f"differs on {int(diff)} rank(s)"
+        if diff:
+            failures.append(f"replay: the independent schedule differs on {int(diff)} rank(s)")
+        eng.set_schedule((2 if a.graph_comm else 1) if a.graph else 0,
+                         int(os.environ.get("GRAVSIM_SYM_DYN_CAP", "4")))
+        eng.set_overlap(overlap)
+
+    # The reference's exact hard-cutoff select (cuda.cu:39, mpi.c:64), timed on its own.
     lay = eng.native_layout
     fmode = eng.force_mode()
+    exact_ms = None
+    if a.exact_steps > 0:
+        eng.set_cutoff_mode("exact")
+        eng.step(2)
+        eng.sync()
+        comm.barrier(dist)
+        t0 = time.perf_counter()
+        eng.step(a.exact_steps)
+        eng.sync()
+        comm.barrier(dist)
+        exact_ms = 1e3 * comm.allreduce_max(dist, time.perf_counter() - t0) / a.exact_steps
     eng.close()
     if rank == 0:
         value = cfg.n * a.steps / wall
@@ -283,9 +425,22 @@ def main(argv=None) -> int:
                 # ... and the pair evaluations actually performed (sym: N(N-1)/2 per step)
                 "pair_evals_per_s": pairs * a.steps / wall,
                 "sampled_rel_err": err,
+                "sampled_rel_err_final": err_end,
+                "momentum_rel_drift": drift,
+                "exact_cutoff_ms_per_step": exact_ms,
                 "nonfinite": int(bad),
             },
+            "work_audit": "ok" if not failures else "; ".join(failures),
+            "audit": {"units": units, "replay": replay},
         }
+        if world > 1:
+            out["config"]["launch"] = {
+                "probe_devices": int(os.environ[launch.PROBE_ENV])
+                if os.environ.get(launch.PROBE_ENV) else None,
+                "rehearsal_rank_hosts": os.environ.get("GRAVSIM_RCCL_RANK_HOSTS") == "1",
+                "HSA_ENABLE_IPC_MODE_LEGACY": os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY"),
+            }
+            out["config"]["ranks"] = ranks_info
         if phase is not None:
             out["comm_ms"] = phase["comm_ms"]
             out["exposed_comm_ms"] = phase["exposed_comm_ms"]
@@ -294,6 +449,9 @@ def main(argv=None) -> int:
                 "exposed_exchange_ms", "deferred_units")}
         print(json.dumps(out), flush=True)
     comm.shutdown(dist)
+    if failures:
+        print("bench.py: work audit FAILED: " + "; ".join(failures), file=sys.stderr, flush=True)
+        return 1
     return 0
 
 

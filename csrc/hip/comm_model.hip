@@ -8,9 +8,9 @@
 //   reference times its whole loop, MPI_Allgatherv included (mpi.c:189,227-247); round-1
 //   emulations treated the exchange as free.
 // * gate_set_kernel: publishes "the all-gather into X[cur] is complete" to the force launch
-//   that may already be running (GRAVSIM_SYM_OVERLAP=3, nbody_sym.hip): one agent-scope
-//   release store after the collective on the comm stream. Force units only test it (no
-//   spinning), so the collective never competes with waiting workgroups for CUs.
+//   that may already be running (overlap 3, the multi-rank default, nbody_sym.hip): one
+//   system-scope release store after the collective on the comm stream. Force units only
+//   test it (no spinning), so the collective never competes with waiting workgroups for CUs.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -31,8 +31,16 @@ __global__ __launch_bounds__(256) void comm_model_kernel(const uint4* __restrict
   __syncthreads();
 }
 
+// System-scope release to pair with the force units' system-scope acquire (nbody_sym.hip
+// gate_open_or_defer): the gathered rows come from peer GPUs. The kernel writes nothing
+// before the flag (the collective's writes precede it by the stream order), and the explicit
+// vmcnt wait keeps the flag behind the L2 write-back whatever the compiler decides.
 __global__ void gate_set_kernel(unsigned* gate) {
-  if (threadIdx.x == 0) __hip_atomic_store(gate, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(gate, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
 }
 
 }  // namespace

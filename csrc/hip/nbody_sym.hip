@@ -274,19 +274,26 @@ __device__ __forceinline__ bool local_first_unit(const SymArgs& a, int b, int* b
 }
 
 // Remote unit of the local-first launch (units 6): go ahead if the comm stream has already
-// published the all-gather (the agent-scope acquire orders the position reads after the
-// collective's writes); otherwise append the unit to the deferred list and leave. No
+// published the all-gather; otherwise append the unit to the deferred list and leave. No
 // workgroup ever waits on the collective, so RCCL's kernels always find CUs; the deferred
 // units run in a second launch (units 7) queued behind the gather event.
+// The acquire is SYSTEM scope (global_load sc0 sc1 + buffer_inv sc0 sc1: this CU's L1 and the
+// XCD's L2). On a real node the remote rows of X are written by peer GPUs over xGMI, which
+// are not agent-scope writers: an agent-scope acquire (buffer_inv sc1) invalidates only the
+// L1 and could leave stale L2 lines of X in place. The ungated schedule gets the same
+// system-scope acquire from the dispatch of the kernel queued behind the gather event;
+// gate_set_kernel publishes with the matching system-scope release (comm_model.hip).
 __device__ __forceinline__ bool gate_open_or_defer(const SymArgs& a, int b, int stage) {
   __shared__ int open_s;
   if (threadIdx.x == 0) {
     const unsigned* gate = a.gate + stage;
-    // (gate_probe: timing probes only, per-rank emulation: 1 skips the check, 2 loads relaxed)
-    const bool open = a.gate_probe == 1 ? true
-                      : a.gate_probe == 2
-                          ? __hip_atomic_load(gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u
-                          : __hip_atomic_load(gate, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+    // (gate_probe, timing probes of the per-rank emulation only: 1 skips the check, 2 loads
+    // relaxed, 3 acquires at agent scope)
+    const bool open =
+        a.gate_probe == 1   ? true
+        : a.gate_probe == 2 ? __hip_atomic_load(gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u
+        : a.gate_probe == 3 ? __hip_atomic_load(gate, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != 0u
+                            : __hip_atomic_load(gate, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != 0u;
     if (!open) {
       const unsigned k =
           __hip_atomic_fetch_add(a.defer, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -296,6 +303,15 @@ __device__ __forceinline__ bool gate_open_or_defer(const SymArgs& a, int b, int 
   }
   __syncthreads();
   return open_s != 0;
+}
+
+// Work audit (SymArgs::audit): one relaxed device-scope add per unit that completed (or
+// was empty), from one lane, after the unit's partial stores. The host compares the count
+// with rows x (S + D) per step (bench.py work_audit), so a launch that silently skipped
+// units (a stale dynamic-fetch counter, a lost deferred unit) cannot pass as a fast step.
+__device__ __forceinline__ void audit_unit(const SymArgs& a) {
+  if (threadIdx.x == 0)
+    __hip_atomic_fetch_add(a.audit, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // One unit b (row a, segment s) per call; s == S is the row's diagonal chunk. b is the
@@ -338,7 +354,14 @@ __device__ __forceinline__ void force_sym_body(const SymArgs& a, int b) {
     s = b % (a.S + a.D);
   }
   const int A = a.a0 + a.band0 + br;
-  if ((int64_t)A * kSymC >= a.n_real) return;  // all-ghost row: never read
+  // Empty units (all-ghost row, segment past the row's shell) count as done for the work
+  // audit, in exactly one of the launches that list them (units 4 and 5 both list shell
+  // segments: the units-5 launch counts the empty ones).
+  const bool count_empty = a.audit && a.units != 4;
+  if ((int64_t)A * kSymC >= a.n_real) {  // all-ghost row: never read
+    if (count_empty) audit_unit(a);
+    return;
+  }
   const bool diag = s >= a.S;
   const int seg_tiles = a.L * G::kTilesPerQuantum;
   TileSeq<T> seq{A, a.NC, a.real_chunks, 0, 0, diag};
@@ -349,7 +372,10 @@ __device__ __forceinline__ void force_sym_body(const SymArgs& a, int b) {
   } else {
     const int h_tiles = shell_len(A, a.NC, a.parity) * G::kTilesPerChunk;
     const int u0 = s * seg_tiles;
-    if (u0 >= h_tiles) return;  // past this row's shell: never read
+    if (u0 >= h_tiles) {  // past this row's shell: never read
+      if (count_empty) audit_unit(a);
+      return;
+    }
     seq.u1 = min(u0 + seg_tiles, h_tiles);
     if (a.units == 4 || a.units == 5) {
       // Rank-local: every j-chunk of the segment is one of the rank's own rows, so it needs
@@ -359,7 +385,7 @@ __device__ __forceinline__ void force_sym_body(const SymArgs& a, int b) {
     }
     seq.u = seq.valid(u0);
   }
-  if (gated && !gate_open_or_defer(a, b, stage)) return;
+  if (gated && !gate_open_or_defer(a, b, stage)) return;  // counted when units 7 runs it
   const unsigned long long t_start = a.utrace ? __builtin_amdgcn_s_memrealtime() : 0ull;
   const V4* X4 = static_cast<const V4*>(a.X);
   ISetK<T> is;
@@ -393,6 +419,7 @@ __device__ __forceinline__ void force_sym_body(const SymArgs& a, int b) {
       out[2 * kSymC + b] = is.az[i];
     }
   }
+  if (a.audit) audit_unit(a);
   if (a.utrace && threadIdx.x == 0) {
     // hwreg(HW_ID) whole register, hwreg(XCC_ID) bits 3:0 (ids 4 and 20 on gfx9.4+)
     const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);

@@ -165,6 +165,13 @@ struct gs_stepper {
   double step_timeout_s = 0.0;  // 0: unbounded
   bool graph_failed = false;    // multi-rank capture refused: eager fallback
   bool work_zero = true;        // sym dynamic unit counter (gate_buf[4]) known to be 0
+  // Work audit of the sym force launches: +1 per unit run (nbody_sym.hip audit_unit); a step
+  // runs rows x (S + D) units on this rank whatever the launch split or fetch order.
+  unsigned long long* audit = nullptr;
+  // Fault injection for the audit's own test (GRAVSIM_FAULT_SKIP_UNITS=k): every dynamic
+  // force launch starts its unit counter at k instead of 0, so units 0 .. k-1 never run,
+  // exactly the failure class of a stale re-armed counter (a memset node when captured).
+  unsigned fault_skip = 0;
 };
 
 namespace {
@@ -325,6 +332,7 @@ gs::SymArgs sym_args(gs_stepper* s, int cur) {
   a.trace_defer0 = (int32_t)s->utrace_main;
   a.diag_last = s->diag_last;
   a.parity = s->parity;
+  a.audit = s->audit;
   return a;
 }
 
@@ -560,17 +568,23 @@ int ring_finish(gs_stepper* s, const gs::KArgs<T>& a) {
 // exchange by device copies, then part 2 (gs_group_step).
 // Force + reductions over the rank's rows, band by band: the force units, the group reduce
 // (the first band starts S_g, later ones continue it) and the row reduce (Ti). With one band
-// and a pending all-gather (sym_overlap, GRAVSIM_SYM_OVERLAP):
-//   0 (default): wait for the gather, then one launch of every unit;
+// and a pending all-gather (sym_overlap: the multi-rank default is 3, GRAVSIM_SYM_OVERLAP or
+// gs_stepper_set_overlap choose another):
+//   3: ONE launch whose grid lists the rank-local units first; a remote unit runs if the
+//     gather has been published (gate flag set on the comm stream), else it defers itself to
+//     a second small launch queued behind the gather event. No launch boundary and no
+//     waiting workgroup: per-rank emulation of 1M / 8 with the collectives modeled at
+//     64 GB/s + 15 us, 22.42-22.59 ms against 22.74-22.87 ms for 0 (docs/DESIGN.md §7,
+//     profiles/r2_overlap_fill_ab.jsonl);
+//   0: wait for the gather, then one launch of every unit;
 //   1: the diagonal-chunk units (own rows only) run beside the gather, then the shell units
 //     after it;
 //   2: the diagonal units and the shell segments whose j-chunks are all own rows (1M, P = 8:
 //     2080 of 16448 units) run on s_comp beside the gather and the other shell units on
 //     s_rem after it, concurrently.
-// A unit is ~0.6 ms of work at 1M, so every extra launch boundary drains the GPU for about
-// that long, while the gather it would hide is ~0.1 ms (14.7 MB per rank over xGMI).
-// Per-rank emulation of 1M, P = 8 (gather treated as done), alternating runs: 0: 21.0-21.2 ms,
-// 1: 21.4-21.6, 2: 22.4-22.6 (profiles/r1_sym_overlap_ab.txt).
+// Modes 1 and 2 pay a launch boundary (a unit is ~0.6 ms of work at 1M) to hide a ~0.1 ms
+// gather and lost to 0 in round 1's emulation with free collectives (0: 21.0-21.2 ms,
+// 1: 21.4-21.6, 2: 22.4-22.6; profiles/r1_sym_overlap_ab.txt); they are kept for A/B runs.
 // With `exchange` the RCCL group-sum exchange starts right
 // after the last group reduce and runs beside the last row reduce; the compute stream joins
 // it afterwards.
@@ -585,6 +599,11 @@ int ring_finish(gs_stepper* s, const gs::KArgs<T>& a) {
 hipError_t force_sym_launch(gs_stepper* s, gs::SymArgs a, hipStream_t st) {
   a.work_zero = s->work_zero ? 1 : 0;
   s->work_zero = false;
+  if (s->fault_skip && a.work && (a.units == 0 || a.units == 6)) {
+    const hipError_t e = hipMemsetD32Async(a.work, (int)s->fault_skip, 1, st);
+    if (e != hipSuccess) return e;
+    a.work_zero = 1;  // the launcher must not re-zero it
+  }
   return gs::launch_force_sym(a, st);
 }
 
@@ -683,10 +702,19 @@ int enqueue_sym(gs_stepper* s, int cur, bool need_gather, bool gathered_external
   return 0;
 }
 
+// Clears the phase-event pointer on every exit path of an enqueue (an error return included),
+// so gather() from download_state / accel_impl never records into a stale PhaseEv (pev may
+// reallocate on the next phase_begin).
+struct PhaseScope {
+  gs_stepper* s;
+  ~PhaseScope() { s->pe = nullptr; }
+};
+
 // Enqueue one step. `capturing` disables timing events.
 template <typename T>
 int enqueue_step(gs_stepper* s, bool capturing, bool gathered_externally) {
   Range range("gs.step");
+  PhaseScope pscope{s};
   const int cur = (int)(s->k & 1);
   gs::KArgs<T> a = base_args<T>(s, cur);
   const int kernel = s->L.kernel, ipl = s->L.ipl;
@@ -1017,6 +1045,9 @@ int gs_stepper_create(const gs_config* cfg, gs_stepper** out) {
   s->esz = cfg->dtype == GS_FP64 ? 8 : 4;
   s->timed = getenv("GRAVSIM_PHASE_TIMING") != nullptr;
   s->emulate = getenv("GRAVSIM_EMULATE_RANK") != nullptr && cfg->nranks > 1;
+  // Multi-rank sym steps default to the gated local-first launch (3): remote units start as
+  // soon as the gather lands, nothing waits on it (see sym_force).
+  s->sym_overlap = cfg->nranks > 1 ? 3 : 0;
   if (const char* ov = getenv("GRAVSIM_SYM_OVERLAP")) s->sym_overlap = atoi(ov);
   if (const char* v = getenv("GRAVSIM_EMU_COMM_GBPS")) s->emu_gbps = atof(v);
   if (const char* v = getenv("GRAVSIM_EMU_COMM_US")) s->emu_lat_us = atof(v);
@@ -1026,6 +1057,7 @@ int gs_stepper_create(const gs_config* cfg, gs_stepper** out) {
   if (const char* v = getenv("GRAVSIM_SYM_DIAG_LAST")) s->diag_last = atoi(v);
   if (const char* v = getenv("GRAVSIM_SYM_FUSED_TAIL")) s->fuse_tail = atoi(v) != 0 ? 1 : 0;
   if (const char* v = getenv("GRAVSIM_SYM_PARITY")) s->parity = atoi(v) != 0 ? 1 : 0;
+  if (const char* v = getenv("GRAVSIM_FAULT_SKIP_UNITS")) s->fault_skip = (unsigned)atoi(v);
   const int64_t own_first = s->L.local_begin / s->L.chunk;
   const int64_t own_last = (s->L.local_begin + s->L.n_local) / s->L.chunk;
   s->own_c0 = (int)(own_first < s->L.n_chunks ? own_first : s->L.n_chunks);
@@ -1101,6 +1133,10 @@ int gs_stepper_create(const gs_config* cfg, gs_stepper** out) {
   FAIL_CLEAN(hipMalloc(&s->gate_buf, 8 * sizeof(unsigned)));
   FAIL_CLEAN(hipMemsetAsync(s->gate_buf, 0, 8 * sizeof(unsigned), s->s_comp));
   if (s->L.mode == GS_MODE_SYM) {
+    FAIL_CLEAN(hipMalloc(&s->audit, sizeof(unsigned long long)));
+    FAIL_CLEAN(hipMemsetAsync(s->audit, 0, sizeof(unsigned long long), s->s_comp));
+  }
+  if (s->L.mode == GS_MODE_SYM) {
     // Deferred-unit list of the gated launch (one band's units) and the local-first order.
     const int rows = s->sym_NC / cfg->nranks;
     const size_t units = (size_t)rows * (s->sym_S_n + s->sym_D) + 1;
@@ -1160,7 +1196,7 @@ int gs_stepper_destroy(gs_stepper* s) {
                   (void*)s->nonfinite, (void*)s->sym_Pi, (void*)s->sym_Pj, (void*)s->sym_Pd,
                   (void*)s->sym_S, (void*)s->sym_R, (void*)s->sym_Ti, (void*)s->gate_buf,
                   (void*)s->defer, (void*)s->sym_lf, s->emu_buf, (void*)s->utrace,
-                  (void*)s->ring_gate})
+                  (void*)s->ring_gate, (void*)s->audit})
     if (p) (void)hipFree(p);
   for (hipEvent_t e : {s->ev_ready, s->ev_gathered, s->ev_t0, s->ev_local, s->ev_end,
                        s->ev_remote, s->ev_fork, s->ev_rem2, s->ev_sym})
@@ -1241,8 +1277,10 @@ int gs_stepper_step(gs_stepper* s, int32_t nsteps) {
   // collectives modeled (GRAVSIM_EMU_COMM_GBPS > 0) or free; remote slices hold stale data,
   // so the numbers are timings, not physics.
   // hipGraph replay of a two-step ping-pong period. Multi-rank (RCCL or emulated) steps are
-  // captured collectives included when use_graph >= 2 (the default for multi-rank runs);
-  // a capture the runtime refuses falls back to eager steps.
+  // captured collectives included only when use_graph >= 2 (opt-in: --graph-comm). Over
+  // RCCL's socket transport that capture crashes inside hipStreamEndCapture
+  // (profiles/r2_graph_comm_root_cause.txt), which no fallback here can catch; a capture
+  // the runtime refuses with an error code falls back to eager steps.
   const bool graph_ok =
       s->cfg.use_graph >= (xcomm(s) ? 2 : 1) && !s->timed && !(xcomm(s) && s->graph_failed);
   int32_t left = nsteps;
@@ -1283,6 +1321,48 @@ int gs_stepper_set_overlap(gs_stepper* s, int32_t mode) {
   return 0;
 }
 
+int gs_stepper_set_schedule(gs_stepper* s, int32_t use_graph, int32_t dyn_cap) {
+  if (use_graph < 0 || use_graph > 2) { gs_set_error("set_schedule: use_graph must be 0..2"); return -1; }
+  s->cfg.use_graph = use_graph;
+  if (dyn_cap >= 0) s->dyn_cap = dyn_cap;
+  s->graph_failed = false;
+  s->work_zero = false;  // (a dynamic launch after a static one re-zeroes its counter)
+  if (s->graph) { (void)hipGraphExecDestroy(s->graph); s->graph = nullptr; }
+  return 0;
+}
+
+int gs_stepper_set_cutoff_mode(gs_stepper* s, int32_t mode) {
+  if (mode < 0 || mode > 2) { gs_set_error("set_cutoff_mode: mode must be 0..2"); return -1; }
+  s->cfg.cutoff_mode = mode;
+  resolve_force_mode(s);
+  if (s->graph) { (void)hipGraphExecDestroy(s->graph); s->graph = nullptr; }
+  return 0;
+}
+
+int gs_stepper_audit(gs_stepper* s, uint64_t* units_done, uint64_t* units_per_step) {
+  if (units_done) *units_done = 0;
+  if (units_per_step) *units_per_step = 0;
+  if (!s->audit) return 0;  // one-sided schedules: no unit audit
+  GS_HIP(hipSetDevice(s->cfg.device));
+  const uint64_t rows = (uint64_t)(s->sym_NC / s->cfg.nranks);
+  if (units_per_step) *units_per_step = rows * (uint64_t)(s->sym_S_n + s->sym_D);
+  if (units_done) {
+    GS_HIP(hipStreamSynchronize(s->s_comp));
+    unsigned long long h = 0;
+    GS_HIP(hipMemcpy(&h, s->audit, sizeof(h), hipMemcpyDeviceToHost));
+    *units_done = h;
+  }
+  return 0;
+}
+
+int gs_stepper_audit_reset(gs_stepper* s) {
+  if (!s->audit) return 0;
+  GS_HIP(hipSetDevice(s->cfg.device));
+  GS_HIP(hipMemsetAsync(s->audit, 0, sizeof(unsigned long long), s->s_comp));
+  GS_HIP(hipStreamSynchronize(s->s_comp));
+  return 0;
+}
+
 int64_t gs_stepper_unit_trace(gs_stepper* s, uint64_t* out, int64_t cap) {
   if (!s->utrace) return 0;
   const int64_t n = 2 * s->utrace_main;
@@ -1291,7 +1371,8 @@ int64_t gs_stepper_unit_trace(gs_stepper* s, uint64_t* out, int64_t cap) {
   GS_HIP(hipStreamSynchronize(s->s_comp));
   const int64_t m = cap < n ? cap : n;
   GS_HIP(hipMemcpy(out, s->utrace, (size_t)m * 4 * sizeof(uint64_t), hipMemcpyDeviceToHost));
-  GS_HIP(hipMemset(s->utrace, 0, (size_t)n * 4 * sizeof(uint64_t)));
+  GS_HIP(hipMemsetAsync(s->utrace, 0, (size_t)n * 4 * sizeof(uint64_t), s->s_comp));
+  GS_HIP(hipStreamSynchronize(s->s_comp));
   return m;
 }
 
@@ -1346,7 +1427,10 @@ int gs_stepper_phase_stats(gs_stepper* s, double* out8) {
   GS_HIP(hipMemcpy(d, s->gate_buf + 2, sizeof(d), hipMemcpyDeviceToHost));
   out8[6] = d[1];
   out8[7] = 0.0;
-  GS_HIP(hipMemset(s->gate_buf + 2, 0, sizeof(d)));
+  // (on s_comp: a legacy-stream memset is not ordered against the non-blocking compute
+  // stream, so the next gated launch could race it)
+  GS_HIP(hipMemsetAsync(s->gate_buf + 2, 0, sizeof(d), s->s_comp));
+  GS_HIP(hipStreamSynchronize(s->s_comp));
   s->pev_used = 0;
   return 0;
 }

@@ -163,8 +163,19 @@ int gs_stepper_phase_stats(gs_stepper* s, double* out8);
 // Sym schedule work beside the all-gather: 0 wait then one launch, 1 diagonal units first,
 // 2 local units + remote units on a second stream, 3 one local-first launch whose remote
 // units run once the gather is published or are deferred to a second launch behind it
-// (GRAVSIM_SYM_OVERLAP sets the initial value).
+// (the default for nranks > 1; GRAVSIM_SYM_OVERLAP sets another initial value).
 int gs_stepper_set_overlap(gs_stepper* s, int32_t mode);
+// Schedule knobs for an independent re-run (bench.py's replay audit): use_graph 0 eager,
+// 1 single-rank graphs, 2 multi-rank capture too; dyn_cap <= 1 static units (one per
+// workgroup), > 1 dynamic fetch with that many units per workgroup, < 0 unchanged.
+int gs_stepper_set_schedule(gs_stepper* s, int32_t use_graph, int32_t dyn_cap);
+// Re-resolve the force path with a new cutoff mode (0 auto, 1 exact select, 2 fast core).
+int gs_stepper_set_cutoff_mode(gs_stepper* s, int32_t mode);
+// Work audit of the sym schedule: force units completed since the last reset (waits for the
+// compute stream) and the units one step must run on this rank (rows x (S + D)); both 0 for
+// the one-sided schedules.
+int gs_stepper_audit(gs_stepper* s, uint64_t* units_done, uint64_t* units_per_step);
+int gs_stepper_audit_reset(gs_stepper* s);
 // Unit timeline of the last sym force launch (stepper created with GRAVSIM_UNIT_TRACE set):
 // copies up to `cap` entries of 4 words {start, end (100 MHz ticks), HW_ID | XCC_ID << 32,
 // row << 32 | segment} (all zero: the slot ran no unit) and clears them. Returns the count;
@@ -188,6 +199,21 @@ int gs_stepper_comm_check(gs_stepper* s);
 
 int gs_hip_device_count(void);
 const char* gs_hip_kernel_info(void);
+
+// ---------------------------------------------------------------- HIP IPC (ipc.hip)
+// Cross-process sharing of device memory and events on one node: what RCCL's intra-node P2P
+// transport builds on (tests/test_ipc_gpu.py). Handles are HIP_IPC_HANDLE_SIZE (64) bytes.
+int gs_dev_alloc(int32_t device, uint64_t bytes, void** out);
+int gs_dev_free(void* p);
+int gs_dev_copy(void* dst, const void* src, uint64_t bytes, int32_t to_device);
+int gs_ipc_mem_handle(void* p, void* out64);
+int gs_ipc_mem_open(int32_t device, const void* h64, void** out);
+int gs_ipc_mem_close(void* p);
+int gs_ipc_event_create(int32_t device, void** ev, void* out64);
+int gs_ipc_event_open(int32_t device, const void* h64, void** ev);
+int gs_event_record_sync(void* ev);
+int gs_event_wait_sync(void* ev);
+int gs_event_destroy(void* ev);
 
 // ---------------------------------------------------------------- errors
 const char* gs_last_error(void);

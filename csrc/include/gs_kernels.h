@@ -106,6 +106,9 @@ struct SymArgs {
   // work[0] is already 0 on this stream (the fused tail kernel that ran after the previous
   // dynamic launch re-armed it): the launcher skips its memset.
   int32_t work_zero;
+  // Work audit (nullptr: off): +1 per force unit that ran to completion (or was empty), so a
+  // step's count must be rows x (S + D) whatever the launch split, deferral or fetch order.
+  unsigned long long* audit;
 };
 
 hipError_t launch_force_sym(const SymArgs& a, hipStream_t s);

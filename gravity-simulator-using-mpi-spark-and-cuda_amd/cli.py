@@ -47,7 +47,8 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--no-graph", dest="graph", action="store_false")
     p.add_argument("--graph-comm", dest="graph_comm", action="store_true",
                    help="replay multi-rank steps from a hipGraph that captures them, RCCL "
-                        "collectives included (default: eager multi-rank steps)")
+                        "collectives included (opt-in: over RCCL's socket transport the capture "
+                        "is known to crash with a SIGSEGV inside hipStreamEndCapture)")
     p.add_argument("--no-graph-comm", dest="graph_comm", action="store_false",
                    help=argparse.SUPPRESS)
     p.add_argument("--step-timeout", dest="step_timeout_s", type=float, default=d.step_timeout_s,
@@ -55,7 +56,8 @@ def build_parser() -> argparse.ArgumentParser:
                         "completes for this many seconds (0 = wait forever)")
     p.add_argument("--overlap", type=int, choices=[-1, 0, 1, 2, 3], default=d.overlap,
                    help="multi-rank sym schedule: work beside the all-gather (3: one launch, "
-                        "rank-local units first, remote units once the gather is published; "
+                        "rank-local units first, remote units once the gather is published, "
+                        "the built-in default for P > 1; 0: wait for the gather, one launch; "
                         "-1: built-in default)")
     p.add_argument("--strategy", choices=["allgather", "ring"], default=d.strategy,
                    help="multi-rank GPU exchange: one all-gather overlapped with the local "

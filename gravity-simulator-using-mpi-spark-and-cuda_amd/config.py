@@ -41,14 +41,16 @@ class SimConfig:
     chunk: int = 0                # canonical j-chunk (0 = auto from n)
     split_groups: int = 0
     graph: bool = True            # hipGraph replay of the step loop (single rank)
-    graph_comm: bool = False      # also capture the multi-rank step (RCCL collectives included;
-                                  # eager fallback if the runtime refuses the capture). Off by
-                                  # default: docs/DESIGN.md "hipGraph and RCCL".
+    graph_comm: bool = False      # also capture the multi-rank step, RCCL collectives included.
+                                  # Off by default: over RCCL's socket transport the capture
+                                  # crashes inside hipStreamEndCapture (a SIGSEGV no fallback
+                                  # can catch; docs/DESIGN.md "hipGraph and RCCL").
     comm: str = "auto"            # rccl (GPU) | gloo (CPU) | none
     strategy: str = "allgather"   # multi-rank exchange: allgather | ring (pipelined send/recv)
     overlap: int = -1             # sym work beside the all-gather: 0 none, 1 diagonal units
                                   # first, 2 two streams, 3 gated local-first launch; -1 native
-                                  # default (GRAVSIM_SYM_OVERLAP or 0)
+                                  # default (3 for P > 1, as bench.py runs; GRAVSIM_SYM_OVERLAP
+                                  # overrides)
     threads: int = 0              # CPU engine OpenMP threads (0 = default)
     step_timeout_s: float = 600.0 # multi-rank hang detection: abort RCCL when no step completes
                                   # for this long

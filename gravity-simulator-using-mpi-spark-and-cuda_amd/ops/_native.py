@@ -152,6 +152,10 @@ def hip_lib():
         _sig(lib, "gs_stepper_set_timing", c_int32, [S, c_int32])
         _sig(lib, "gs_stepper_phase_stats", c_int32, [S, _PD])
         _sig(lib, "gs_stepper_set_overlap", c_int32, [S, c_int32])
+        _sig(lib, "gs_stepper_set_schedule", c_int32, [S, c_int32, c_int32])
+        _sig(lib, "gs_stepper_set_cutoff_mode", c_int32, [S, c_int32])
+        _sig(lib, "gs_stepper_audit", c_int32, [S, POINTER(c_uint64), POINTER(c_uint64)])
+        _sig(lib, "gs_stepper_audit_reset", c_int32, [S])
         _sig(lib, "gs_stepper_set_timeout", c_int32, [S, c_double])
         _sig(lib, "gs_stepper_unit_trace", c_int64, [S, c_void_p, c_int64])
         _sig(lib, "gs_stepper_compute_stream", c_void_p, [S])
@@ -161,6 +165,17 @@ def hip_lib():
         _sig(lib, "gs_stepper_comm_init", c_int32, [S, c_void_p, c_int32, c_int32])
         _sig(lib, "gs_stepper_comm_check", c_int32, [S])
         _sig(lib, "gs_hip_device_count", c_int32, [])
+        VP = POINTER(c_void_p)
+        _sig(lib, "gs_dev_alloc", c_int32, [c_int32, c_uint64, VP])
+        _sig(lib, "gs_dev_free", c_int32, [c_void_p])
+        _sig(lib, "gs_dev_copy", c_int32, [c_void_p, c_void_p, c_uint64, c_int32])
+        _sig(lib, "gs_ipc_mem_handle", c_int32, [c_void_p, c_void_p])
+        _sig(lib, "gs_ipc_mem_open", c_int32, [c_int32, c_void_p, VP])
+        _sig(lib, "gs_ipc_mem_close", c_int32, [c_void_p])
+        _sig(lib, "gs_ipc_event_create", c_int32, [c_int32, VP, c_void_p])
+        _sig(lib, "gs_ipc_event_open", c_int32, [c_int32, c_void_p, VP])
+        for f in ("gs_event_record_sync", "gs_event_wait_sync", "gs_event_destroy"):
+            _sig(lib, f, c_int32, [c_void_p])
         _sig(lib, "gs_hip_kernel_info", ctypes.c_char_p, [])
         _hip = lib
         return lib

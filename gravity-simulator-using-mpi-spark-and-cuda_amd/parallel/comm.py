@@ -98,6 +98,17 @@ def broadcast_bytes(info: DistInfo, payload: bytes | None, src: int = 0) -> byte
     return bytes(buf.numpy().tobytes())
 
 
+def allgather_object(info: DistInfo, obj) -> list:
+    """Every rank's picklable `obj`, in rank order (control plane only: small records)."""
+    if info.world <= 1:
+        return [obj]
+    import torch.distributed as dist
+
+    out = [None] * info.world
+    dist.all_gather_object(out, obj)
+    return out
+
+
 def allreduce_max(info: DistInfo, value: float) -> float:
     if info.world <= 1:
         return float(value)

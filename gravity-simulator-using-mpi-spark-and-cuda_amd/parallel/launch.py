@@ -70,18 +70,24 @@ def torchrun_cmd(nproc: int, target: list[str], argv: Iterable[str], port: int,
             str(nproc), "--master-addr", "127.0.0.1", "--master-port", str(port), *target, *rest]
 
 
-def check_device_count(nproc: int) -> None:
-    """Refuse more ranks than visible GPUs (one rank per GPU), except in the one-GPU RCCL
-    rehearsal (GRAVSIM_RCCL_RANK_HOSTS=1: every rank on device 0 over loopback sockets).
-    torch.cuda.device_count() does not initialise the GPU on this image."""
-    if os.environ.get("GRAVSIM_RCCL_RANK_HOSTS") == "1":
-        return
+PROBE_ENV = "GRAVSIM_LAUNCH_PROBE"  # the parent's device count, handed to the ranks
+
+
+def check_device_count(nproc: int) -> int:
+    """Count the visible HIP devices (torch.cuda.device_count() does not initialise the GPU
+    on this image) and refuse more ranks than devices: one rank per GPU. The one-GPU RCCL
+    rehearsal (GRAVSIM_RCCL_RANK_HOSTS=1: every rank on device 0 over loopback sockets) runs
+    the same probe and skips only the refusal, so it executes the production parent sequence
+    probe -> torchrun child -> RCCL. Returns the count and exports it to the children
+    (GRAVSIM_LAUNCH_PROBE; bench.py reports it)."""
     import torch
 
     have = torch.cuda.device_count()
-    if nproc > have:
+    os.environ[PROBE_ENV] = str(have)
+    if nproc > have and os.environ.get("GRAVSIM_RCCL_RANK_HOSTS") != "1":
         raise SystemExit(f"--gpus {nproc} but only {have} HIP device(s) are visible "
                          "(set GRAVSIM_RCCL_RANK_HOSTS=1 to rehearse several ranks on one GPU)")
+    return have
 
 
 def spawn(nproc: int, target: list[str], argv: Iterable[str], keep_gpus: bool = False,

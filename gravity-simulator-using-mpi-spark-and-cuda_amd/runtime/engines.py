@@ -154,8 +154,32 @@ class HipEngine:
         return out
 
     def set_overlap(self, mode: int) -> None:
-        """Sym-schedule work beside the all-gather (0..3, see gravsim.h)."""
+        """Sym-schedule work beside the all-gather (0..3, see gravsim.h; 3 is the native
+        default for P > 1)."""
         _native.check(self.lib, self.lib.gs_stepper_set_overlap(self._s, int(mode)), "overlap")
+
+    def set_schedule(self, graph: int, dyn_cap: int = -1) -> None:
+        """graph: 0 eager, 1 single-rank hipGraph replay, 2 multi-rank capture too;
+        dyn_cap: <= 1 static force units (one per workgroup), > 1 dynamic unit fetch,
+        < 0 unchanged. Same bits in every combination (an independent schedule for audits)."""
+        _native.check(self.lib, self.lib.gs_stepper_set_schedule(self._s, int(graph),
+                                                                 int(dyn_cap)), "schedule")
+
+    def set_cutoff_mode(self, mode: str) -> None:
+        """Re-resolve the force path: auto | exact (reference hard-cutoff select) | fast."""
+        _native.check(self.lib, self.lib.gs_stepper_set_cutoff_mode(
+            self._s, _native.CUTOFF_IDS[mode]), "cutoff mode")
+
+    def audit(self) -> tuple[int, int]:
+        """(force units completed since the last audit_reset, units per step on this rank);
+        (0, 0) for the one-sided schedules, which have no unit audit. Waits for the GPU."""
+        done, per = ctypes.c_uint64(), ctypes.c_uint64()
+        _native.check(self.lib, self.lib.gs_stepper_audit(self._s, ctypes.byref(done),
+                                                          ctypes.byref(per)), "audit")
+        return int(done.value), int(per.value)
+
+    def audit_reset(self) -> None:
+        _native.check(self.lib, self.lib.gs_stepper_audit_reset(self._s), "audit reset")
 
     def state(self) -> BodySet:
         """Full positions (collective for P > 1), own velocity rows, masses."""

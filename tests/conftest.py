@@ -31,7 +31,8 @@ def hip():
 # Tests set them only through monkeypatch; one left in the process environment (e.g. by a
 # module imported at collection) would silently alter every later test.
 _PROCESS_KNOBS = ("GRAVSIM_EMULATE_RANK", "GRAVSIM_UNIT_TRACE", "GRAVSIM_EMU_COMM_GBPS",
-                  "GRAVSIM_SYM_DYN_CAP", "GRAVSIM_SYM_FIRST_WAVE", "GRAVSIM_SYM_BAND_MB")
+                  "GRAVSIM_SYM_DYN_CAP", "GRAVSIM_SYM_FIRST_WAVE", "GRAVSIM_SYM_BAND_MB",
+                  "GRAVSIM_FAULT_SKIP_UNITS")
 
 
 @pytest.fixture(autouse=True)

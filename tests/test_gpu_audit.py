@@ -1,0 +1,139 @@
+"""Work audit of the sym force launches and pinned cutoff semantics (GPU).
+
+bench.py must not be able to print a fast headline for steps that skipped work (round 2:
+graph replays after the first ran no units until commit 8fdec84). The force kernels count
+every unit they run (nbody_sym.hip audit_unit); a step must run rows x (S + D) units per
+rank whatever the launch split, band count, fetch order or graph replay. A skipped-unit fault
+(GRAVSIM_FAULT_SKIP_UNITS: the dynamic counter starts past 0, the failure class of a stale
+re-armed counter) must be caught by bench.py's unit count and by its independent replay.
+
+The reference times its whole loop with the work in it (cuda.cu:154-171, mpi.c:189-247).
+"""
+from __future__ import annotations
+
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from gravsim.config import SimConfig
+from gravsim.models import initial_conditions as ic
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.parametrize("n,dtype,P,band_mb,graph", [
+    (65536, "fp32", 1, None, True),     # fused tail re-arms the counter, graph replay
+    (65536, "fp32", 1, None, False),    # eager
+    (40000, "fp32", 1, "1", True),      # one 2048-body row per band, static launches
+    (40000, "fp64", 2, None, False),    # virtual ranks: each shard counts its own rows
+])
+def test_unit_audit_counts_every_unit(hip, monkeypatch, n, dtype, P, band_mb, graph):
+    from gravsim.runtime.engines import VirtualGroup
+
+    if band_mb:
+        monkeypatch.setenv("GRAVSIM_SYM_BAND_MB", band_mb)
+    g = VirtualGroup(SimConfig(n=n, dtype=dtype, device="gpu", mode="sym", graph=graph), P)
+    try:
+        g.init_ics("solar+random", 5)
+        for s in g.shards:
+            s.audit_reset()
+        steps = 5
+        g.step(steps)
+        g.sync()
+        per = []
+        for s in g.shards:
+            done, per_step = s.audit()
+            assert per_step > 0
+            assert done == per_step * steps, (done, per_step)
+            per.append(per_step)
+        # every rank's rows together: all NC rows x (S + D)
+        NC = g.shards[0].layout.n_pad // 2048
+        assert sum(per) % NC == 0
+        # the step-path acceleration query runs every unit once more
+        if P == 1:
+            s = g.shards[0]
+            s.audit_reset()
+            s.accel(step_path=True)
+            assert s.audit() == (per[0], per[0])
+    finally:
+        g.close()
+
+
+def _bench(args, env_extra=None):
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    env.update(env_extra or {})
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], env=env,
+                       capture_output=True, text=True, timeout=240, cwd=ROOT)
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    return r, (json.loads(lines[-1]) if lines else None)
+
+
+def test_bench_audit_ok_and_reports_physics(hip):
+    r, out = _bench(["--n", "65536", "--steps", "6", "--warmup", "2", "--exact-steps", "2"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert out["work_audit"] == "ok"
+    assert out["audit"]["replay"] == "bitwise"
+    u = out["audit"]["units"]
+    assert u["units_done_rank0"] == 6 * u["units_per_step_rank0"] and u["ranks_short"] == 0
+    c = out["config"]
+    assert c["sampled_rel_err"] < 1e-4 and c["sampled_rel_err_final"] < 1e-4
+    assert c["momentum_rel_drift"] < 1e-5
+    assert c["exact_cutoff_ms_per_step"] > 0
+
+
+def test_bench_audit_catches_skipped_units(hip):
+    """The dynamic counter starts at 64 in every force launch: 64 units per step never run.
+    The step is slightly faster and wrong; bench.py must say so and exit non-zero."""
+    r, out = _bench(["--n", "65536", "--steps", "4", "--warmup", "1", "--exact-steps", "0",
+                     "--phase-steps", "0"], {"GRAVSIM_FAULT_SKIP_UNITS": "64"})
+    assert r.returncode == 1, (r.returncode, r.stderr[-3000:])
+    assert "work audit FAILED" in r.stderr
+    assert out is not None and out["work_audit"] != "ok"
+    assert "unit count" in out["work_audit"] and "replay" in out["work_audit"]
+    u = out["audit"]["units"]
+    assert u["units_done_rank0"] == 4 * (u["units_per_step_rank0"] - 64)
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "fp64"])
+def test_cutoff_paths_below_the_cutoff_pinned(hip, dtype):
+    """A pair closer than the reference's 1e-10 m cutoff: the exact path (the reference's
+    select, cuda.cu:39, mpi.c:64) gives it zero force; the fast path (the default) adds the
+    core c^2 instead, so the pair gets mu r / (r^2 + c^2)^1.5: finite, huge, never NaN.
+    Every other pair is the same in both paths (bit-identical above ~1 cm)."""
+    from gravsim.runtime.engines import HipEngine
+
+    n = 4096
+    b = ic.solar_random(n, seed=21)
+    b.pos[101] = b.pos[100] + np.array([5e-11, 0.0, 0.0])  # 0.5 cutoff apart
+    out = {}
+    for mode in ("exact", "fast"):
+        e = HipEngine(SimConfig(n=n, dtype=dtype, device="gpu", mode="sym", cutoff_mode=mode))
+        try:
+            e.load(b)
+            out[mode] = (e.accel(step_path=True)[:n, :3], e.force_mode())
+        finally:
+            e.close()
+    a_ex, fm_ex = out["exact"]
+    a_fa, fm_fa = out["fast"]
+    assert fm_ex["exact"] and not fm_fa["exact"]
+    c2 = fm_fa["eps2"]
+    mu = 6.67430e-11 * b.mass
+    d = b.pos[101] - b.pos[100]
+    r2 = float(d @ d)
+    want_100 = mu[101] * d / (r2 + c2) ** 1.5  # the pair's term on body 100 (fast path)
+    got_100 = a_fa[100] - a_ex[100]
+    assert np.all(np.isfinite(a_fa)) and np.all(np.isfinite(a_ex))
+    np.testing.assert_allclose(got_100, want_100, rtol=1e-4 if dtype == "fp32" else 1e-9,
+                               atol=1e-6 * np.abs(want_100).max())
+    # far bodies see both paths alike
+    far = np.setdiff1d(np.arange(n), [100, 101])
+    rel = np.abs(a_fa[far] - a_ex[far]).max() / np.abs(a_ex[far]).max()
+    assert rel < (1e-5 if dtype == "fp32" else 1e-12), rel

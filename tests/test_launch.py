@@ -40,10 +40,14 @@ def test_device_count_guard(monkeypatch):
     import torch
 
     have = torch.cuda.device_count()
+    monkeypatch.delenv(launch.PROBE_ENV, raising=False)
     with pytest.raises(SystemExit, match="HIP device"):
         launch.check_device_count(have + 1)
     monkeypatch.setenv("GRAVSIM_RCCL_RANK_HOSTS", "1")
-    launch.check_device_count(have + 8)  # rehearsal: every rank on one GPU
+    monkeypatch.delenv(launch.PROBE_ENV, raising=False)
+    # rehearsal: every rank on one GPU; the probe still runs and is handed to the ranks
+    assert launch.check_device_count(have + 8) == have
+    assert os.environ[launch.PROBE_ENV] == str(have)
 
 
 def _bench(args, env_extra):
