@@ -7,8 +7,9 @@ the Newton-3 schedule: every unordered pair is evaluated once and applied to bot
 (csrc/hip/nbody_sym.hip). Each rank owns N/P bodies (a block of 2048-body chunk rows), joins
 an in-place RCCL all-gather of positions, evaluates its rows' cyclic half-shell of chunk
 pairs, exchanges the group sums of the far sides with ncclSend/ncclRecv, and integrates its
-own bodies (kick-drift). Single-rank steps replay a hipGraph; multi-rank steps run eagerly
-(--graph-comm captures them, collectives included).
+own bodies (kick-drift). Single-rank steps replay a hipGraph; multi-rank steps replay a
+segmented plan: the compute work between two collectives as graph segments, the RCCL calls
+issued eagerly between them (--graph-comm captures the collectives too, opt-in).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--n BODIES] [--dtype fp32|fp64]
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
@@ -92,11 +93,13 @@ def parse(argv=None) -> argparse.Namespace:
 
 def rccl_log_setup() -> str | None:
     """Route RCCL's INFO log to a private per-rank file (before any RCCL call; stdout stays
-    rank 0's JSON line) so the transport each connection used can be reported. Left alone
-    when the user already configured NCCL_DEBUG."""
-    if "NCCL_DEBUG" in os.environ or "NCCL_DEBUG_FILE" in os.environ:
+    rank 0's JSON line) so the transport each connection used can be reported. A level the
+    user set (NCCL_DEBUG=WARN...) is raised to INFO for the file; its WARN lines are echoed
+    to stderr afterwards. Left alone when the user already chose a log file."""
+    if "NCCL_DEBUG_FILE" in os.environ:
         return None
     d = tempfile.mkdtemp(prefix="gravsim_rccl_")
+    os.environ["GRAVSIM_USER_NCCL_DEBUG"] = os.environ.get("NCCL_DEBUG", "")
     os.environ["NCCL_DEBUG"] = "INFO"
     os.environ["NCCL_DEBUG_SUBSYS"] = "INIT,P2P,NET"
     os.environ["NCCL_DEBUG_FILE"] = os.path.join(d, "rccl.log")
@@ -107,11 +110,19 @@ def rccl_transports(path: str | None) -> dict:
     """Transports of this rank's RCCL connections ("Channel .. via P2P/IPC", "NET/Socket",
     "SHM"...) and the RCCL version, from the INFO log; the file is removed afterwards."""
     out = {"transports": None, "rccl_version": None, "net": None}
-    if not path or not os.path.exists(path):
+    if not path:
+        out["rccl_log"] = "NCCL_DEBUG_FILE set by the user: not parsed"
+        return out
+    if not os.path.exists(path):
+        out["rccl_log"] = f"no RCCL log written at {path}"
         return out
     seen, net = set(), set()
+    lines = 0
     with open(path, errors="replace") as f:
         for line in f:
+            lines += 1
+            if " WARN " in line:
+                sys.stderr.write(line)
             m = re.search(r" via (\S+)", line)
             if m and "Channel" in line:
                 seen.add(re.sub(r"/\d+$", "", m.group(1)))
@@ -123,6 +134,7 @@ def rccl_transports(path: str | None) -> dict:
                 net.add(m.group(1))
     out["transports"] = sorted(seen)
     out["net"] = sorted(net) or None
+    out["rccl_log"] = f"{lines} lines"
     shutil.rmtree(os.path.dirname(path), ignore_errors=True)
     return out
 
@@ -306,6 +318,7 @@ def main(argv=None) -> int:
     comm.barrier(dist)
     t1 = time.perf_counter()
     wall = comm.allreduce_max(dist, t1 - t0)
+    ginfo = eng.graph_info()
 
     # ---- audits of the timed work (untimed) --------------------------------------------
     failures = []
@@ -417,7 +430,10 @@ def main(argv=None) -> int:
                 "cutoff_path": "exact-select" if fmode["exact"] else
                 f"fast (core^2={fmode['eps2']:.3g} m^2; bit-identical to the 1e-10 m hard cutoff "
                 "for separations above ~1 cm)",
-                "graph": bool(a.graph and (world == 1 or a.graph_comm)),
+                # eager | graph (one hipGraph per two steps) | segmented (multi-rank: compute
+                # segments as graphs, RCCL collectives eager between them)
+                "graph": ginfo["mode"],
+                "graph_segments": ginfo["segments"] or None,
                 "overlap": overlap,
                 "overlap_check": overlap_check,
                 # N^2 ordered pair terms per step (what a one-sided sum evaluates) ...

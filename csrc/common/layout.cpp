@@ -39,11 +39,12 @@ extern "C" int gs_layout_compute(const gs_config* cfg, gs_layout* out) {
   out->n = cfg->n;
   out->chunk = chunk;
   out->n_pad = gs::round_up(cfg->n, (int64_t)cfg->nranks * chunk);
-  // Newton-3 symmetric schedule (fp32, fast cutoff, P | 8). Its chunk/row/group structure
-  // must not depend on P, so the padding is the one an 8-rank run would use.
-  const bool sym_ok = 8 % cfg->nranks == 0 && cfg->kernel != GS_KERNEL_MFMA;
+  // Newton-3 symmetric schedule, any P from 1 to 8. Its chunk/row/block structure must not
+  // depend on P, so the padding is the one an 8-rank run would use; ranks own whole row
+  // blocks (gs_common.h sym_blk_lo: mpi.c's remainder rule over the B blocks).
+  const bool sym_ok = cfg->nranks <= 8 && cfg->kernel != GS_KERNEL_MFMA;
   if (cfg->mode == GS_MODE_SYM && !sym_ok) {
-    gs_set_error("layout: the sym schedule needs nranks dividing 8 (and not the mfma kernel)");
+    gs_set_error("layout: the sym schedule needs nranks <= 8 (and not the mfma kernel)");
     return -1;
   }
   const int64_t sym_unit = 8 * (int64_t)(chunk % 2048 == 0 ? chunk : 2 * chunk);
@@ -57,9 +58,16 @@ extern "C" int gs_layout_compute(const gs_config* cfg, gs_layout* out) {
   // size (stepper.hip ensure_sym), so memory does not limit the choice either.
   const int64_t sym_min = cfg->dtype == GS_FP32 ? 16384 : 32768;
   if (cfg->mode == GS_MODE_AUTO && sym_ok && cfg->n >= sym_min) sym = true;
-  if (sym) out->n_pad = sym_pad;
-  out->n_local = out->n_pad / cfg->nranks;
-  out->local_begin = (int64_t)cfg->rank * out->n_local;
+  if (sym) {
+    out->n_pad = sym_pad;
+    int32_t a0 = 0, rows = 0;
+    if (gs_sym_rank_rows(sym_pad, cfg->nranks, cfg->rank, &a0, &rows)) return -1;
+    out->local_begin = (int64_t)a0 * 2048;
+    out->n_local = (int64_t)rows * 2048;
+  } else {
+    out->n_local = out->n_pad / cfg->nranks;
+    out->local_begin = (int64_t)cfg->rank * out->n_local;
+  }
   out->n_chunks = (int32_t)((cfg->n + chunk - 1) / chunk);
   // j source and i-bodies per lane, from in-process sweeps on MI355X with the explicit
   // 2-vector fp32 loop (profiles/r1_tune2_*.log):
@@ -148,6 +156,52 @@ extern "C" int gs_sym_geometry(int64_t n_pad, int32_t* NC, int32_t* H, int32_t* 
   return 0;
 }
 
+// Rows [a0, a0 + rows) of rank `rank` of `nranks` in the sym schedule: whole row blocks by
+// mpi.c's remainder rule (gs_common.h sym_blk_lo). Equal for every P dividing 8.
+extern "C" int gs_sym_rank_rows(int64_t n_pad, int32_t nranks, int32_t rank, int32_t* a0,
+                                int32_t* rows) {
+  if (n_pad % (8 * 2048) != 0) { gs_set_error("sym: n_pad must be a multiple of 16384"); return -1; }
+  const int32_t NC = (int32_t)(n_pad / 2048), B = gs::sym_blocks(NC), RB = NC / B;
+  if (nranks < 1 || nranks > B || rank < 0 || rank >= nranks) {
+    gs_set_error("sym: nranks must be 1 .. the row-block count (>= 8)");
+    return -1;
+  }
+  const int32_t lo = gs::sym_blk_lo(B, nranks, rank), hi = gs::sym_blk_lo(B, nranks, rank + 1);
+  if (a0) *a0 = lo * RB;
+  if (rows) *rows = (hi - lo) * RB;
+  return 0;
+}
+
+// Row blocks and reduction-tree nodes: B blocks of RB rows; rank `rank` sends nn dyadic
+// nodes (sub-trees of its block range); nodes of lower ranks come first (nb of them); NN
+// nodes in all.
+extern "C" int gs_sym_nodes(int64_t n_pad, int32_t nranks, int32_t rank, int32_t* B, int32_t* RB,
+                            int32_t* nn, int32_t* nb, int32_t* NN) {
+  if (gs_sym_rank_rows(n_pad, nranks, rank, nullptr, nullptr)) return -1;
+  const int32_t NC = (int32_t)(n_pad / 2048), b = gs::sym_blocks(NC);
+  int32_t before = 0, total = 0, mine = 0;
+  for (int32_t q = 0; q < nranks; ++q) {
+    const int32_t k = gs::sym_node_count(gs::sym_blk_lo(b, nranks, q), gs::sym_blk_lo(b, nranks, q + 1));
+    if (q < rank) before += k;
+    if (q == rank) mine = k;
+    total += k;
+  }
+  if (B) *B = b;
+  if (RB) *RB = NC / b;
+  if (nn) *nn = mine;
+  if (nb) *nb = before;
+  if (NN) *NN = total;
+  return 0;
+}
+
+// Owner rank of chunk row A.
+static int32_t sym_row_owner(int32_t A, int32_t NC, int32_t nranks) {
+  const int32_t B = gs::sym_blocks(NC), blk = A / (NC / B);
+  int32_t q = 0;
+  while (q + 1 < nranks && gs::sym_blk_lo(B, nranks, q + 1) <= blk) ++q;
+  return q;
+}
+
 // Chunk rows of the sym schedule: row A pairs with the next h(A) chunks cyclically. Distances
 // 1 .. NC/2 - 1 belong to the row below; each antipodal pair {A, A + NC/2} to one of its two
 // rows, by parity (A < NC/2 takes it iff A is even; NC/2 is a multiple of 4, so A + NC/2 has
@@ -183,11 +237,11 @@ static int32_t sym_local_segs(int32_t A, int32_t NC, int32_t a0, int32_t rows, i
 // geometry, -1 on error (cap too small, bad arguments).
 extern "C" int64_t gs_sym_unit_map(int64_t n_pad, int32_t rank, int32_t nranks, int32_t parity,
                                    int64_t fill, int32_t* out, int64_t cap) {
-  int32_t NC, H, L, S, D;
-  if (nranks < 1 || rank < 0 || rank >= nranks || gs_sym_geometry(n_pad, &NC, &H, &L, &S, &D))
+  int32_t NC, H, L, S, D, a0, rows;
+  if (nranks < 1 || rank < 0 || rank >= nranks || gs_sym_geometry(n_pad, &NC, &H, &L, &S, &D) ||
+      gs_sym_rank_rows(n_pad, nranks, rank, &a0, &rows))
     return -1;
-  if (NC % nranks) return -1;
-  const int32_t rows = NC / nranks, per = S + D, a0 = rank * rows;
+  const int32_t per = S + D;
   const int64_t total = (int64_t)rows * per;
   if (rows >= 32768 || per >= 65536) return 0;
   if (!out || cap < total) return -1;
@@ -223,11 +277,11 @@ extern "C" int64_t gs_sym_unit_map(int64_t n_pad, int32_t rank, int32_t nranks, 
 // Returns the entry count, 0 if the fields cannot hold the geometry, -1 on error.
 extern "C" int64_t gs_sym_unit_map_ring(int64_t n_pad, int32_t rank, int32_t nranks,
                                         int32_t parity, int64_t fill, int32_t* out, int64_t cap) {
-  int32_t NC, H, L, S, D;
-  if (nranks < 1 || rank < 0 || rank >= nranks || gs_sym_geometry(n_pad, &NC, &H, &L, &S, &D))
+  int32_t NC, H, L, S, D, a0, rows;
+  if (nranks < 1 || rank < 0 || rank >= nranks || gs_sym_geometry(n_pad, &NC, &H, &L, &S, &D) ||
+      gs_sym_rank_rows(n_pad, nranks, rank, &a0, &rows))
     return -1;
-  if (NC % nranks) return -1;
-  const int32_t rows = NC / nranks, per = S + D, a0 = rank * rows;
+  const int32_t per = S + D;
   const int64_t total = (int64_t)rows * per;
   if (rows >= 4096 || per >= 65536 || nranks > 8) return 0;
   if (!out || cap < total) return -1;
@@ -240,7 +294,7 @@ extern "C" int64_t gs_sym_unit_map_ring(int64_t n_pad, int32_t rank, int32_t nra
       const int32_t q0 = g * L, q1 = (g + 1) * L - 1;  // quanta of the shell, 16 per chunk
       int32_t st = 0;
       for (int32_t d = 1 + q0 / 16; d <= 1 + q1 / 16; ++d) {
-        const int32_t owner = ((A + d) % NC) / rows;
+        const int32_t owner = sym_row_owner((A + d) % NC, NC, nranks);
         const int32_t k = ((rank - owner) % nranks + nranks) % nranks;
         if (k > st) st = k;
       }
@@ -273,13 +327,18 @@ extern "C" int64_t gs_sym_unit_map_ring(int64_t n_pad, int32_t rank, int32_t nra
   return k;
 }
 
-// Partial-slot bytes per rank if all of the rank's rows were held at once (one band).
+// Partial-slot bytes of rank 0 (the largest share) if all of its rows were held at once (one
+// band): Pi + Pj + Pd (3 elements per body per slot), the node sums it sends (nn x 3 per
+// body of the run) and the ones it receives (NN x 3 per own body).
 extern "C" int64_t gs_sym_bytes(int64_t n_pad, int32_t nranks, int32_t esz) {
-  int32_t nc, h, l, sg, dp;
-  if (gs_sym_geometry(n_pad, &nc, &h, &l, &sg, &dp)) return -1;
-  const int64_t n_local = n_pad / nranks;
-  // Pi + Pj + Pd (3 elements per body per slot) + two group-sum buffers (8 groups x 3)
-  return n_local * 3 * esz * ((int64_t)sg + h + dp) + 2 * n_local * 8 * 3 * esz;
+  int32_t nc, h, l, sg, dp, a0, rows, nn, NN;
+  if (gs_sym_geometry(n_pad, &nc, &h, &l, &sg, &dp) ||
+      gs_sym_rank_rows(n_pad, nranks, 0, &a0, &rows) ||
+      gs_sym_nodes(n_pad, nranks, 0, nullptr, nullptr, &nn, nullptr, &NN))
+    return -1;
+  const int64_t n_local = (int64_t)rows * 2048;
+  return n_local * 3 * esz * ((int64_t)sg + h + dp) +
+         ((int64_t)nn * n_pad + (int64_t)NN * n_local) * 3 * esz;
 }
 
 extern "C" void gs_ic_fill_host(int32_t ic, uint64_t seed, int64_t n, int64_t begin, int64_t end,

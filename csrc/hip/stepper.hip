@@ -44,6 +44,7 @@
 #include <string.h>
 
 #include <chrono>
+#include <functional>
 #include <string>
 #include <thread>
 #include <vector>
@@ -172,6 +173,20 @@ struct gs_stepper {
   // force launch starts its unit counter at k instead of 0, so units 0 .. k-1 never run,
   // exactly the failure class of a stale re-armed counter (a memset node when captured).
   unsigned fault_skip = 0;
+  // Segmented step graph of multi-rank runs (use_graph 1): the compute stream's work between
+  // two cross-stream points is captured as one graph segment; the collectives (RCCL, or the
+  // emulation's modeled ones) and the event record/wait that order them against the compute
+  // stream are issued eagerly between the segments on replay. RCCL is never captured, so the
+  // socket-transport capture crash (profiles/r2_graph_comm_root_cause.txt) cannot occur.
+  struct PlanOp {
+    enum Kind { kGraph, kRecord, kWait, kHost } kind;
+    hipGraphExec_t g;
+    hipEvent_t ev;
+    std::function<int()> fn;
+  };
+  std::vector<PlanOp> plan;  // one ping-pong period (two steps)
+  bool rec = false;          // recording a plan: s_comp is capturing a segment
+  int plan_graphs = 0;       // graph segments per period (diagnostics)
 };
 
 namespace {
@@ -210,6 +225,73 @@ struct Range {
 };
 
 size_t row_bytes(const gs_stepper* s) { return 4 * s->esz; }
+
+// ---- compute-stream ordering points (eager, or cut points of a recorded plan) ----------
+// End the open capture segment and keep it as a graph if it holds any node.
+int seg_cut(gs_stepper* s) {
+  hipGraph_t g = nullptr;
+  GS_HIP(hipStreamEndCapture(s->s_comp, &g));
+  size_t nodes = 0;
+  hipError_t e = hipGraphGetNodes(g, nullptr, &nodes);
+  if (e == hipSuccess && nodes > 0) {
+    hipGraphExec_t x = nullptr;
+    e = hipGraphInstantiate(&x, g, nullptr, nullptr, 0);
+    if (e == hipSuccess) {
+      s->plan.push_back({gs_stepper::PlanOp::kGraph, x, nullptr, {}});
+      ++s->plan_graphs;
+    }
+  }
+  (void)hipGraphDestroy(g);
+  GS_HIP(e);
+  return 0;
+}
+
+int seg_open(gs_stepper* s) {
+  GS_HIP(hipStreamBeginCapture(s->s_comp, hipStreamCaptureModeThreadLocal));
+  return 0;
+}
+
+// hipEventRecord(ev, s_comp) for another stream to wait on.
+int comp_record(gs_stepper* s, hipEvent_t ev) {
+  if (!s->rec) {
+    GS_HIP(hipEventRecord(ev, s->s_comp));
+    return 0;
+  }
+  if (seg_cut(s)) return -1;
+  s->plan.push_back({gs_stepper::PlanOp::kRecord, nullptr, ev, {}});
+  return seg_open(s);
+}
+
+// hipStreamWaitEvent(s_comp, ev) on an event another stream records.
+int comp_wait(gs_stepper* s, hipEvent_t ev) {
+  if (!s->rec) {
+    GS_HIP(hipStreamWaitEvent(s->s_comp, ev, 0));
+    return 0;
+  }
+  if (seg_cut(s)) return -1;
+  s->plan.push_back({gs_stepper::PlanOp::kWait, nullptr, ev, {}});
+  return seg_open(s);
+}
+
+// Work on the comm stream (a collective and its event bookkeeping): run now, or replayed
+// eagerly at this point of the plan.
+int comm_do(gs_stepper* s, std::function<int()> fn) {
+  if (!s->rec) return fn();
+  if (seg_cut(s)) return -1;
+  s->plan.push_back({gs_stepper::PlanOp::kHost, nullptr, nullptr, std::move(fn)});
+  return seg_open(s);
+}
+
+void drop_graphs(gs_stepper* s) {
+  if (s->graph) {
+    (void)hipGraphExecDestroy(s->graph);
+    s->graph = nullptr;
+  }
+  for (auto& op : s->plan)
+    if (op.g) (void)hipGraphExecDestroy(op.g);
+  s->plan.clear();
+  s->plan_graphs = 0;
+}
 
 // A multi-rank exchange is active: a real communicator, or the per-rank emulation.
 bool xcomm(const gs_stepper* s) { return s->have_comm || s->emulate; }
@@ -341,31 +423,35 @@ gs::SymArgs sym_args(gs_stepper* s, int cur) {
 // With join = false the compute stream does not wait for it yet (the caller joins with
 // hipStreamWaitEvent(s_comp, ev_sym) after work that does not read Rbuf).
 int sym_exchange_rccl(gs_stepper* s, bool join = true) {
-  const int P = s->cfg.nranks, r = s->cfg.rank;
-  const size_t cnt = (size_t)(gs::kSymGroups / P) * 3 * s->L.n_local;  // elements
-  const size_t bytes = cnt * s->esz;
-  const ncclDataType_t dt = s->esz == 8 ? ncclFloat64 : ncclFloat32;
-  GS_HIP(hipEventRecord(s->ev_ready, s->s_comp));
-  GS_HIP(hipStreamWaitEvent(s->s_comm, s->ev_ready, 0));
-  GS_MARK(x0, x, s->s_comm);
-  GS_HIP(hipMemcpyAsync(s->sym_R + (size_t)r * bytes, s->sym_S + (size_t)r * bytes, bytes,
-                        hipMemcpyDeviceToDevice, s->s_comm));
-  if (s->emulate) {
-    if (comm_model(s, s->sym_S, exchange_bytes(s))) return -1;
-  } else if (P > 1) {
-    GS_NCCL(ncclGroupStart());
-    for (int q = 0; q < P; ++q) {
-      if (q == r) continue;
-      GS_NCCL(ncclSend(s->sym_S + (size_t)q * bytes, cnt, dt, q, s->comm, s->s_comm));
-      GS_NCCL(ncclRecv(s->sym_R + (size_t)q * bytes, cnt, dt, q, s->comm, s->s_comm));
-    }
-    GS_NCCL(ncclGroupEnd());
-  }
-  GS_MARK(x1, x, s->s_comm);
-  GS_HIP(hipEventRecord(s->ev_sym, s->s_comm));
+  if (comp_record(s, s->ev_ready)) return -1;
+  if (comm_do(s, [s]() -> int {
+        const int P = s->cfg.nranks, r = s->cfg.rank;
+        const size_t cnt = (size_t)(gs::kSymGroups / P) * 3 * s->L.n_local;  // elements
+        const size_t bytes = cnt * s->esz;
+        const ncclDataType_t dt = s->esz == 8 ? ncclFloat64 : ncclFloat32;
+        GS_HIP(hipStreamWaitEvent(s->s_comm, s->ev_ready, 0));
+        GS_MARK(x0, x, s->s_comm);
+        GS_HIP(hipMemcpyAsync(s->sym_R + (size_t)r * bytes, s->sym_S + (size_t)r * bytes, bytes,
+                              hipMemcpyDeviceToDevice, s->s_comm));
+        if (s->emulate) {
+          if (comm_model(s, s->sym_S, exchange_bytes(s))) return -1;
+        } else if (P > 1) {
+          GS_NCCL(ncclGroupStart());
+          for (int q = 0; q < P; ++q) {
+            if (q == r) continue;
+            GS_NCCL(ncclSend(s->sym_S + (size_t)q * bytes, cnt, dt, q, s->comm, s->s_comm));
+            GS_NCCL(ncclRecv(s->sym_R + (size_t)q * bytes, cnt, dt, q, s->comm, s->s_comm));
+          }
+          GS_NCCL(ncclGroupEnd());
+        }
+        GS_MARK(x1, x, s->s_comm);
+        GS_HIP(hipEventRecord(s->ev_sym, s->s_comm));
+        return 0;
+      }))
+    return -1;
   if (join) {
     GS_MARK(j0, j, s->s_comp);
-    GS_HIP(hipStreamWaitEvent(s->s_comp, s->ev_sym, 0));
+    if (comp_wait(s, s->ev_sym)) return -1;
     GS_MARK(j1, j, s->s_comp);
   }
   return 0;
@@ -474,33 +560,35 @@ int ring_xfer_rccl(gs_stepper* s, int cur, int sub);
 // slices already received can start.
 int gather(gs_stepper* s, int cur, bool gate = false) {
   if (!xcomm(s) || s->full[cur]) return 0;
-  char* buf = static_cast<char*>(s->X[cur]);
-  const size_t count = (size_t)s->L.n_local * 4;
-  GS_HIP(hipEventRecord(s->ev_ready, s->s_comp));
-  GS_HIP(hipStreamWaitEvent(s->s_comm, s->ev_ready, 0));
-  GS_MARK(g0, g, s->s_comm);
-  if (s->sym_ring && use_sym(s)) {
-    const size_t slice = (size_t)s->L.n_local * row_bytes(s);
-    for (int k = 1; k < s->cfg.nranks; ++k) {
-      if (s->emulate) {
-        if (comm_model(s, buf, slice)) return -1;
-      } else if (ring_xfer_rccl(s, cur, k)) {
-        return -1;
-      }
-      if (gate) GS_HIP(gs::launch_gate_set(s->ring_gate + 8 * cur + k, s->s_comm));
-    }
-  } else if (s->emulate) {
-    if (comm_model(s, buf, gather_bytes(s))) return -1;
-  } else {
-    GS_NCCL(ncclAllGather(buf + (size_t)s->cfg.rank * s->L.n_local * row_bytes(s), buf, count,
-                          s->esz == 4 ? ncclFloat32 : ncclFloat64, s->comm, s->s_comm));
-  }
-  GS_MARK(g1, g, s->s_comm);
-  if (gate && !(s->sym_ring && use_sym(s)))
-    GS_HIP(gs::launch_gate_set(s->gate_buf + cur, s->s_comm));
-  GS_HIP(hipEventRecord(s->ev_gathered, s->s_comm));
+  if (comp_record(s, s->ev_ready)) return -1;
   s->full[cur] = true;
-  return 0;
+  return comm_do(s, [s, cur, gate]() -> int {
+    char* buf = static_cast<char*>(s->X[cur]);
+    const size_t count = (size_t)s->L.n_local * 4;
+    GS_HIP(hipStreamWaitEvent(s->s_comm, s->ev_ready, 0));
+    GS_MARK(g0, g, s->s_comm);
+    if (s->sym_ring && use_sym(s)) {
+      const size_t slice = (size_t)s->L.n_local * row_bytes(s);
+      for (int k = 1; k < s->cfg.nranks; ++k) {
+        if (s->emulate) {
+          if (comm_model(s, buf, slice)) return -1;
+        } else if (ring_xfer_rccl(s, cur, k)) {
+          return -1;
+        }
+        if (gate) GS_HIP(gs::launch_gate_set(s->ring_gate + 8 * cur + k, s->s_comm));
+      }
+    } else if (s->emulate) {
+      if (comm_model(s, buf, gather_bytes(s))) return -1;
+    } else {
+      GS_NCCL(ncclAllGather(buf + (size_t)s->cfg.rank * s->L.n_local * row_bytes(s), buf, count,
+                            s->esz == 4 ? ncclFloat32 : ncclFloat64, s->comm, s->s_comm));
+    }
+    GS_MARK(g1, g, s->s_comm);
+    if (gate && !(s->sym_ring && use_sym(s)))
+      GS_HIP(gs::launch_gate_set(s->gate_buf + cur, s->s_comm));
+    GS_HIP(hipEventRecord(s->ev_gathered, s->s_comm));
+    return 0;
+  });
 }
 
 // ---- ring pass (strategy 1) ------------------------------------------------------------
@@ -625,7 +713,7 @@ int sym_force(gs_stepper* s, gs::SymArgs a, bool overlap_gather, bool exchange =
       a.units = 6;
       GS_HIP(force_sym_launch(s, a, s->s_comp));
       GS_MARK(w0, w, s->s_comp);
-      GS_HIP(hipStreamWaitEvent(s->s_comp, s->ev_gathered, 0));
+      if (comp_wait(s, s->ev_gathered)) return -1;
       GS_MARK(w1, w, s->s_comp);
       a.units = 7;
       GS_HIP(force_sym_launch(s, a, s->s_comp));
@@ -634,7 +722,7 @@ int sym_force(gs_stepper* s, gs::SymArgs a, bool overlap_gather, bool exchange =
       gs::SymArgs d = a;
       d.units = 1;  // diagonal chunks beside the gather
       GS_HIP(force_sym_launch(s, d, s->s_comp));
-      GS_HIP(hipStreamWaitEvent(s->s_comp, s->ev_gathered, 0));
+      if (comp_wait(s, s->ev_gathered)) return -1;
       a.units = 2;
       GS_HIP(force_sym_launch(s, a, s->s_comp));
     } else if (overlap_gather && b0 == 0 && one_band && ov == 2) {
@@ -652,7 +740,7 @@ int sym_force(gs_stepper* s, gs::SymArgs a, bool overlap_gather, bool exchange =
     } else {
       if (overlap_gather && b0 == 0) {
         GS_MARK(w0, w, s->s_comp);
-        GS_HIP(hipStreamWaitEvent(s->s_comp, s->ev_gathered, 0));
+        if (comp_wait(s, s->ev_gathered)) return -1;
         GS_MARK(w1, w, s->s_comp);
       }
       GS_HIP(force_sym_launch(s, a, s->s_comp));
@@ -664,7 +752,7 @@ int sym_force(gs_stepper* s, gs::SymArgs a, bool overlap_gather, bool exchange =
     GS_HIP(gs::launch_sym_row_reduce(a, s->s_comp));
     if (exchange && last) {
       GS_MARK(j0, j, s->s_comp);
-      GS_HIP(hipStreamWaitEvent(s->s_comp, s->ev_sym, 0));
+      if (comp_wait(s, s->ev_sym)) return -1;
       GS_MARK(j1, j, s->s_comp);
     }
   }
@@ -833,6 +921,53 @@ int build_graph(gs_stepper* s) {
   GS_HIP(e);
   GS_HIP(hipGraphInstantiate(&s->graph, g, nullptr, nullptr, 0));
   GS_HIP(hipGraphDestroy(g));
+  return 0;
+}
+
+// Multi-rank steps whose cross-stream points all go through comp_record / comp_wait /
+// comm_do: the sym schedule except overlap 2 (a second compute stream forked per step).
+bool plan_ok(const gs_stepper* s) {
+  return xcomm(s) && use_sym(s) && s->sym_overlap != 2 && s->cfg.use_graph == 1 && !s->timed;
+}
+
+// Record one ping-pong period (two steps, from an even step whose buffer needs its gather)
+// as a plan: compute segments captured on s_comp, the collectives kept as eager host ops.
+int build_plan(gs_stepper* s) {
+  const int64_t k0 = s->k;
+  const bool f0 = s->full[0], f1 = s->full[1];
+  drop_graphs(s);
+  s->work_zero = false;  // (as build_graph: a replay re-zeroes the dynamic unit counter)
+  if (seg_open(s)) return -1;
+  s->rec = true;
+  int rc = enqueue_step_any(s, true);
+  if (rc == 0) rc = enqueue_step_any(s, true);
+  s->rec = false;
+  const int cut = rc == 0 ? seg_cut(s) : 0;
+  if (rc != 0) {  // abandon the open capture
+    hipGraph_t g = nullptr;
+    if (hipStreamEndCapture(s->s_comp, &g) == hipSuccess && g) (void)hipGraphDestroy(g);
+  }
+  s->k = k0;
+  s->full[0] = f0;
+  s->full[1] = f1;
+  if (rc || cut) {
+    drop_graphs(s);
+    return -1;
+  }
+  return 0;
+}
+
+int run_plan(gs_stepper* s) {
+  for (auto& op : s->plan) {
+    switch (op.kind) {
+      case gs_stepper::PlanOp::kGraph: GS_HIP(hipGraphLaunch(op.g, s->s_comp)); break;
+      case gs_stepper::PlanOp::kRecord: GS_HIP(hipEventRecord(op.ev, s->s_comp)); break;
+      case gs_stepper::PlanOp::kWait: GS_HIP(hipStreamWaitEvent(s->s_comp, op.ev, 0)); break;
+      case gs_stepper::PlanOp::kHost:
+        if (op.fn()) return -1;
+        break;
+    }
+  }
   return 0;
 }
 
@@ -1132,7 +1267,8 @@ int gs_stepper_create(const gs_config* cfg, gs_stepper** out) {
   // [0..1] gather gates, [2..3] deferral stats, [4] dynamic unit-fetch counter
   FAIL_CLEAN(hipMalloc(&s->gate_buf, 8 * sizeof(unsigned)));
   FAIL_CLEAN(hipMemsetAsync(s->gate_buf, 0, 8 * sizeof(unsigned), s->s_comp));
-  if (s->L.mode == GS_MODE_SYM) {
+  if (s->L.mode == GS_MODE_SYM && !(getenv("GRAVSIM_AUDIT") && atoi(getenv("GRAVSIM_AUDIT")) == 0)) {
+    // (GRAVSIM_AUDIT=0: no unit counter, for A/B timing of its cost only)
     FAIL_CLEAN(hipMalloc(&s->audit, sizeof(unsigned long long)));
     FAIL_CLEAN(hipMemsetAsync(s->audit, 0, sizeof(unsigned long long), s->s_comp));
   }
@@ -1189,7 +1325,7 @@ int gs_stepper_destroy(gs_stepper* s) {
   if (s->s_comm) (void)hipStreamSynchronize(s->s_comm);
   if (s->s_rem) (void)hipStreamSynchronize(s->s_rem);
   if (s->s_rem2) (void)hipStreamSynchronize(s->s_rem2);
-  if (s->graph) (void)hipGraphExecDestroy(s->graph);
+  drop_graphs(s);
   if (s->have_comm) (void)ncclCommDestroy(s->comm);
   if (s->sym_R == s->sym_S) s->sym_R = nullptr;
   for (void* p : {s->X[0], s->X[1], s->vel, s->partial, s->acc, (void*)s->mass_dev,
@@ -1250,13 +1386,13 @@ int gs_stepper_init_ics(gs_stepper* s, int32_t ic, uint64_t seed) {
                           hipMemcpyDeviceToDevice, s->s_comp));
     GS_HIP(hipStreamSynchronize(s->s_comp));
   }
-  if (s->graph) { (void)hipGraphExecDestroy(s->graph); s->graph = nullptr; }
+  drop_graphs(s);
   return 0;
 }
 
 int gs_stepper_set_state(gs_stepper* s, const double* pos, const double* vel, const double* mass) {
   GS_HIP(hipSetDevice(s->cfg.device));
-  if (s->graph) { (void)hipGraphExecDestroy(s->graph); s->graph = nullptr; }
+  drop_graphs(s);
   return s->esz == 4 ? upload_state<float>(s, pos, vel, mass)
                      : upload_state<double>(s, pos, vel, mass);
 }
@@ -1281,18 +1417,29 @@ int gs_stepper_step(gs_stepper* s, int32_t nsteps) {
   // RCCL's socket transport that capture crashes inside hipStreamEndCapture
   // (profiles/r2_graph_comm_root_cause.txt), which no fallback here can catch; a capture
   // the runtime refuses with an error code falls back to eager steps.
-  const bool graph_ok =
-      s->cfg.use_graph >= (xcomm(s) ? 2 : 1) && !s->timed && !(xcomm(s) && s->graph_failed);
+  // Multi-rank runs with use_graph 1 (the default) replay a segmented plan instead: compute
+  // segments as graphs, collectives eager between them (plan_ok, build_plan).
+  const bool seg = plan_ok(s);
+  const bool graph_ok = seg || (s->cfg.use_graph >= (xcomm(s) ? 2 : 1) && !s->timed &&
+                                !(xcomm(s) && s->graph_failed));
   int32_t left = nsteps;
   while (left > 0) {
     const bool period_start = (s->k & 1) == 0 && (xcomm(s) ? !s->full[0] : true);
     if (graph_ok && left >= 2 && period_start && !s->graph_failed) {
-      if (!s->graph && build_graph(s)) {
-        if (!xcomm(s)) return -1;
-        s->graph_failed = true;  // eager from here on (the error text is kept for inspection)
-        continue;
+      if (seg) {
+        if (s->plan.empty() && build_plan(s)) {
+          s->graph_failed = true;  // eager from here on (the error text is kept)
+          continue;
+        }
+        if (run_plan(s)) return -1;
+      } else {
+        if (!s->graph && build_graph(s)) {
+          if (!xcomm(s)) return -1;
+          s->graph_failed = true;  // eager from here on (the error text is kept for inspection)
+          continue;
+        }
+        GS_HIP(hipGraphLaunch(s->graph, s->s_comp));
       }
-      GS_HIP(hipGraphLaunch(s->graph, s->s_comp));
       s->k += 2;
       // After one period: X[1] was gathered in the second step, X[0] holds only the own slice.
       s->full[0] = !xcomm(s);
@@ -1317,7 +1464,7 @@ int gs_stepper_set_timing(gs_stepper* s, int32_t on) {
 int gs_stepper_set_overlap(gs_stepper* s, int32_t mode) {
   if (mode < 0 || mode > 3) { gs_set_error("set_overlap: mode must be 0..3"); return -1; }
   s->sym_overlap = mode;
-  if (s->graph) { (void)hipGraphExecDestroy(s->graph); s->graph = nullptr; }
+  drop_graphs(s);
   return 0;
 }
 
@@ -1327,7 +1474,7 @@ int gs_stepper_set_schedule(gs_stepper* s, int32_t use_graph, int32_t dyn_cap) {
   if (dyn_cap >= 0) s->dyn_cap = dyn_cap;
   s->graph_failed = false;
   s->work_zero = false;  // (a dynamic launch after a static one re-zeroes its counter)
-  if (s->graph) { (void)hipGraphExecDestroy(s->graph); s->graph = nullptr; }
+  drop_graphs(s);
   return 0;
 }
 
@@ -1335,7 +1482,13 @@ int gs_stepper_set_cutoff_mode(gs_stepper* s, int32_t mode) {
   if (mode < 0 || mode > 2) { gs_set_error("set_cutoff_mode: mode must be 0..2"); return -1; }
   s->cfg.cutoff_mode = mode;
   resolve_force_mode(s);
-  if (s->graph) { (void)hipGraphExecDestroy(s->graph); s->graph = nullptr; }
+  drop_graphs(s);
+  return 0;
+}
+
+int gs_stepper_graph_info(gs_stepper* s, int32_t* mode, int32_t* segments) {
+  if (mode) *mode = !s->plan.empty() ? 2 : (s->graph ? 1 : 0);
+  if (segments) *segments = s->plan_graphs;
   return 0;
 }
 
@@ -1686,7 +1839,7 @@ int gs_stepper_comm_init(gs_stepper* s, const void* id128, int32_t rank, int32_t
     (void)ncclCommDestroy(s->comm);
     s->comm = nullptr;
   }
-  if (s->graph) { (void)hipGraphExecDestroy(s->graph); s->graph = nullptr; }
+  drop_graphs(s);
   if (s->have_comm) {
     // Warm-up: RCCL builds its transports lazily on the first collective and on the first
     // send/recv to each peer. Do both here on scratch memory (the accel buffer holds

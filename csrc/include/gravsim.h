@@ -93,6 +93,12 @@ int32_t gs_auto_chunk(int64_t n);
 int gs_sym_geometry(int64_t n_pad, int32_t* NC, int32_t* H, int32_t* L, int32_t* S,
                     int32_t* D);
 int64_t gs_sym_bytes(int64_t n_pad, int32_t nranks, int32_t esz);
+// Rows [a0, a0 + rows) of one rank (whole row blocks, mpi.c's remainder rule) and the
+// reduction-tree nodes: B blocks of RB rows, nn nodes sent by this rank, nb by lower ranks,
+// NN in all (gs_common.h).
+int gs_sym_rank_rows(int64_t n_pad, int32_t nranks, int32_t rank, int32_t* a0, int32_t* rows);
+int gs_sym_nodes(int64_t n_pad, int32_t nranks, int32_t rank, int32_t* B, int32_t* RB,
+                 int32_t* nn, int32_t* nb, int32_t* NN);
 // Shell length of chunk row A (antipodal pairs split by parity; parity 0: rows A < NC/2).
 int32_t gs_sym_shell_len(int32_t A, int32_t NC, int32_t parity);
 // Unit order of the gated sym launch for one rank (see layout.cpp); returns the entry count.
@@ -176,6 +182,10 @@ int gs_stepper_set_cutoff_mode(gs_stepper* s, int32_t mode);
 // the one-sided schedules.
 int gs_stepper_audit(gs_stepper* s, uint64_t* units_done, uint64_t* units_per_step);
 int gs_stepper_audit_reset(gs_stepper* s);
+// What the last replayed steps ran from: *mode 0 eager, 1 one hipGraph per two steps, 2 a
+// segmented plan (multi-rank: compute segments as graphs, collectives eager between them);
+// *segments = graph segments per two steps (mode 2).
+int gs_stepper_graph_info(gs_stepper* s, int32_t* mode, int32_t* segments);
 // Unit timeline of the last sym force launch (stepper created with GRAVSIM_UNIT_TRACE set):
 // copies up to `cap` entries of 4 words {start, end (100 MHz ticks), HW_ID | XCC_ID << 32,
 // row << 32 | segment} (all zero: the slot ran no unit) and clears them. Returns the count;

@@ -75,6 +75,40 @@ GS_HD int32_t auto_chunk(int64_t n) {
 
 GS_HD int64_t round_up(int64_t a, int64_t b) { return (a + b - 1) / b * b; }
 
+// ---- Newton-3 (sym) schedule: row blocks, rank ownership, canonical reduction tree -------
+// The NC chunk rows are cut into B row blocks (B = the largest power of two <= 64 dividing
+// NC, a function of n_pad only). Rank r of P owns blocks [sym_blk_lo(r), sym_blk_lo(r + 1))
+// by the reference's remainder rule (mpi.c:184-187: the first B mod P ranks hold one more),
+// so every P from 1 to 8 gets a balanced share of whole blocks. The j-side sums reach a body
+// as a binary tree over the B blocks (each leaf a row-ascending sum), so the bits depend on
+// n_pad only: a rank sends the dyadic sub-trees covering its block range, and the receiver
+// completes the same tree (binary-counter merge, left + right).
+GS_HD int32_t sym_blocks(int32_t NC) {
+  int32_t b = 64;
+  while (b > 1 && NC % b) b >>= 1;
+  return b;
+}
+GS_HD int32_t sym_blk_lo(int32_t B, int32_t P, int32_t r) {
+  const int32_t base = B / P, rem = B % P;
+  return r * base + (r < rem ? r : rem);
+}
+// Level of the dyadic node that starts at block lo inside [lo, hi): the largest l with
+// lo % 2^l == 0 and lo + 2^l <= hi.
+GS_HD int32_t sym_dyadic_level(int32_t lo, int32_t hi) {
+  int32_t l = 0;
+  while (l < 30 && ((lo >> l) & 1) == 0 && lo + (2 << l) <= hi) ++l;
+  return l;
+}
+// Dyadic nodes covering [lo, hi).
+GS_HD int32_t sym_node_count(int32_t lo, int32_t hi) {
+  int32_t n = 0;
+  while (lo < hi) {
+    lo += 1 << sym_dyadic_level(lo, hi);
+    ++n;
+  }
+  return n;
+}
+
 // Threads per force-kernel workgroup (i-bodies per workgroup = GS_BLOCK * ipl). 256 = 4
 // waves; other values exist for the block-size sweep (scripts/gpu_block_sweep.sh).
 #ifndef GS_BLOCK

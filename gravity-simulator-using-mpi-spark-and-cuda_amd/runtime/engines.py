@@ -178,6 +178,13 @@ class HipEngine:
                                                           ctypes.byref(per)), "audit")
         return int(done.value), int(per.value)
 
+    def graph_info(self) -> dict:
+        """How replayed steps run: eager, one graph per two steps, or a segmented plan
+        (multi-rank: compute segments as graphs, collectives eagerly between them)."""
+        m, n = ctypes.c_int32(), ctypes.c_int32()
+        self.lib.gs_stepper_graph_info(self._s, ctypes.byref(m), ctypes.byref(n))
+        return {"mode": ("eager", "graph", "segmented")[m.value], "segments": n.value}
+
     def audit_reset(self) -> None:
         _native.check(self.lib, self.lib.gs_stepper_audit_reset(self._s), "audit reset")
 

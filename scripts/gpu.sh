@@ -15,6 +15,8 @@
 #   trace[:<rank_shape args>] rocprofv3 kernel trace of bench/rank_shape.py + overlap report
 #   rankprof[:<rank_shape args>] rocprofv3 kernel-trace stats of bench/rank_shape.py
 #   counters                  rocprofv3 -L (the PMC counters this box offers)
+#   ipc                       two-process HIP IPC with / without HSA_ENABLE_IPC_MODE_LEGACY=0
+#   abaudit[:<bench args>]    interleaved bench.py A/B of the work-audit counter (GRAVSIM_AUDIT)
 # Outputs land in gpurun_out/<task>*.log.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
@@ -75,6 +77,19 @@ for task in "$@"; do
         --output-format csv -- python bench/rank_shape.py $a
       head -8 $out/rankprof/rp_kernel_stats.csv ;;
     counters) step 120 $out/counters.txt rocprofv3 -L ;;
+    ipc)
+      # two-process HIP IPC (memory + event) with the launcher's dmabuf setting and without it
+      step 300 $out/ipc_dmabuf.log env HSA_ENABLE_IPC_MODE_LEGACY=0 python tests/ipc_peer.py pair
+      step 300 $out/ipc_legacy.log env -u HSA_ENABLE_IPC_MODE_LEGACY python tests/ipc_peer.py pair ;;
+    abaudit)
+      # interleaved A/B of the work-audit counter's cost at the headline size (same box)
+      for i in 1 2 3; do
+        for arm in 1 0; do
+          step 600 $out/abaudit_${arm}_$i.log env GRAVSIM_AUDIT=$arm python bench.py --steps 10 \
+            --warmup 2 --exact-steps 0 --phase-steps 0 --check-samples 0 --no-replay-audit $a
+          grep -o '"ms_per_step": [0-9.]*' $out/abaudit_${arm}_$i.log | sed "s/^/audit=$arm /" | tee -a $out/abaudit.txt
+        done
+      done ;;
     *) echo "unknown task $task"; exit 2 ;;
   esac
 done

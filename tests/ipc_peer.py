@@ -78,5 +78,43 @@ def main(argv: list[str]) -> int:
     return 0
 
 
+def pair(nbytes: int) -> int:
+    """Run exporter + importer under this environment and print one JSON verdict line
+    (scripts/gpu.sh ipc runs it with and without HSA_ENABLE_IPC_MODE_LEGACY=0)."""
+    import json
+    import subprocess
+
+    env = dict(os.environ)
+    a = subprocess.Popen([sys.executable, __file__, "export", str(nbytes)], stdin=subprocess.PIPE,
+                         stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, env=env)
+    log, ok = [], False
+    try:
+        line = ""
+        for raw in a.stdout:
+            line = raw.strip()
+            log.append("A: " + line)
+            if line.startswith(("HANDLES ", "FAIL")):
+                break
+        if line.startswith("HANDLES "):
+            _, hm, he = line.split()
+            b = subprocess.run([sys.executable, __file__, "import", str(nbytes), hm, he],
+                               capture_output=True, text=True, timeout=120, env=env)
+            log.append(f"B rc={b.returncode}: " + (b.stdout + b.stderr).strip()[-800:])
+            a.stdin.write("CHECK\n" if b.returncode == 0 else "ABORT\n")
+            a.stdin.flush()
+            out = a.communicate(timeout=120)[0]
+            log.append(f"A rc={a.returncode}: " + out.strip()[-800:])
+            ok = b.returncode == 0 and a.returncode == 0 and "EXPORT OK" in out
+    finally:
+        if a.poll() is None:
+            a.kill()
+            a.wait()
+    print(json.dumps({"HSA_ENABLE_IPC_MODE_LEGACY": env.get("HSA_ENABLE_IPC_MODE_LEGACY"),
+                      "ipc_works": ok, "log": log}), flush=True)
+    return 0
+
+
 if __name__ == "__main__":
+    if sys.argv[1:2] == ["pair"]:
+        sys.exit(pair(int(sys.argv[2]) if len(sys.argv) > 2 else 4 << 20))
     sys.exit(main(sys.argv[1:]))

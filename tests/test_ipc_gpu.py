@@ -31,12 +31,19 @@ def _run_pair(env: dict) -> tuple[bool, str]:
                          cwd=ROOT)
     log = []
     try:
-        line = a.stdout.readline().strip()
-        log.append(f"A: {line}")
+        line = ""
+        while True:  # (the runtime may print warnings first, e.g. a missing amdgpu.ids)
+            line = a.stdout.readline()
+            if not line:
+                break
+            line = line.strip()
+            log.append(f"A: {line}")
+            if line.startswith(("HANDLES ", "FAIL")):
+                break
         if not line.startswith("HANDLES "):
-            a.stdin.close()
+            a.kill()
             rest = a.communicate(timeout=60)[0]
-            return False, "\n".join(log) + "\n" + rest[-2000:]
+            return False, "\n".join(log) + "\n" + (rest or "")[-2000:]
         _, hm, he = line.split()
         b = subprocess.run([sys.executable, PEER, "import", str(NBYTES), hm, he], env=env,
                            capture_output=True, text=True, timeout=120, cwd=ROOT)

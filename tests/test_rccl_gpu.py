@@ -39,11 +39,14 @@ def _worker(rank, world, port, out_dir, n, steps, strategy="allgather", mode="au
     dist = comm.init(timeout_s=120)
     status = "ok"
     try:
-        # "<mode>-graph": the multi-rank step, collectives included, captured in a hipGraph
+        # "<mode>-graph": the multi-rank step, collectives included, captured in a hipGraph;
+        # "<mode>-eager": no graphs at all (the default replays a segmented plan: compute
+        # segments as graphs, collectives eager between them)
         graph_comm = mode.endswith("-graph")
+        eager = mode.endswith("-eager")
         cfg = SimConfig(n=n, dtype=dtype, device="gpu", chunk=1024, step_timeout_s=120,
-                        strategy=strategy, mode=mode.removesuffix("-graph"),
-                        graph_comm=graph_comm)
+                        strategy=strategy, mode=mode.removesuffix("-graph").removesuffix("-eager"),
+                        graph_comm=graph_comm, graph=not eager)
         eng = HipEngine(cfg, rank, world, device=0, dist=dist)
         uid = HipEngine.unique_id() if rank == 0 else None
         uid = comm.broadcast_bytes(dist, uid)
@@ -54,8 +57,13 @@ def _worker(rank, world, port, out_dir, n, steps, strategy="allgather", mode="au
         ok = comm.allreduce_sum(dist, 0.0 if status == "ok" else 1.0)
         if ok == 0:
             eng.init_ics("solar+random", 5)
+            eng.audit_reset()
             eng.step(steps)
             eng.sync(timeout_s=120)
+            done, per = eng.audit()
+            gi = eng.graph_info()
+            with open(os.path.join(out_dir, f"audit{rank}.txt"), "w") as f:
+                f.write(f"{done} {per} {gi['mode']} {gi['segments']}")
             b = eng.state()
             own = eng.layout.real_local  # velocities are rank-local (positions are gathered)
             np.save(os.path.join(out_dir, f"vel{rank}.npy"), b.vel[own.start:own.stop])
@@ -80,7 +88,12 @@ def _worker(rank, world, port, out_dir, n, steps, strategy="allgather", mode="au
         comm.shutdown(dist)
 
 
-OV3 = {"GRAVSIM_SYM_OVERLAP": "3"}  # one local-first launch, remote units gated in-kernel
+OV3 = {"GRAVSIM_SYM_OVERLAP": "3"}  # one local-first launch, remote units gated (the default)
+OV0 = {"GRAVSIM_SYM_OVERLAP": "0"}  # wait for the gather, then one launch
+_GRAPH_COMM_XFAIL = pytest.mark.xfail(
+    reason="capturing RCCL collectives over the socket transport crashes inside "
+           "hipStreamEndCapture (profiles/r2_graph_comm_root_cause.txt); the default "
+           "segmented plan keeps RCCL out of the capture", strict=False)
 
 
 @pytest.mark.parametrize("world,strategy,mode,dtype,n,env", [
@@ -99,12 +112,17 @@ OV3 = {"GRAVSIM_SYM_OVERLAP": "3"}  # one local-first launch, remote units gated
     (2, "ring", "sym", "fp32", 20000, OV3),
     (4, "ring", "sym", "fp32", 40000, OV3),
     (8, "ring", "sym", "fp32", 40000, OV3),
-    # "sym-graph": capturing the multi-rank step over RCCL's socket transport segfaulted
-    # inside a rank in round 1 (profiles/r1_rccl_multi_rank_tests.log); graph capture of the
-    # collectives stays opt-in (--graph-comm), is covered on one rank below, and the
-    # multi-process case runs only on request (GRAVSIM_TEST_GRAPH_COMM=1).
+    # the round-2 default (ungated, eager) and ungated under the segmented plan
+    (4, "allgather", "sym-eager", "fp32", 40000, OV0),
+    (8, "allgather", "sym", "fp32", 40000, OV0),
+    (2, "allgather", "sym-eager", "fp64", 20000, None),
+    # "sym-graph": capturing the multi-rank step, collectives included, over RCCL's socket
+    # transport segfaulted inside a rank (round 1: profiles/r1_rccl_multi_rank_tests.log;
+    # round 2: profiles/r2_graph_comm_root_cause.txt). It stays opt-in (--graph-comm) and is
+    # kept here as an expected failure so its status shows in every run; the remaining
+    # capture cases run on request (GRAVSIM_TEST_GRAPH_COMM=1).
+    pytest.param(2, "allgather", "sym-graph", "fp32", 20000, None, marks=_GRAPH_COMM_XFAIL),
     *([(2, "allgather", "auto-graph", "fp32", 5000, None),  # split: all-gather only
-       (2, "allgather", "sym-graph", "fp32", 20000, None),
        (4, "allgather", "sym-graph", "fp32", 20000, None),
        (4, "allgather", "sym-graph", "fp32", 40000, OV3)]
       if os.environ.get("GRAVSIM_TEST_GRAPH_COMM") == "1" else []),
@@ -121,7 +139,16 @@ def test_rccl_multi_rank_match_single_rank(hip, tmp_path, world, strategy, mode,
     from gravsim.config import SimConfig
     from gravsim.runtime.engines import HipEngine
 
-    mode = mode.removesuffix("-graph")
+    variant = mode
+    mode = mode.removesuffix("-graph").removesuffix("-eager")
+    for r in range(world):  # every rank ran exactly its units, from the expected schedule
+        done, per, gmode, segs = open(tmp_path / f"audit{r}.txt").read().split()
+        if mode == "sym":
+            assert int(done) == int(per) * steps and int(per) > 0, (r, done, per)
+            want = {"-eager": "eager", "-graph": "graph"}.get(variant[len(mode):], "segmented")
+            assert gmode == want, (r, gmode, want)
+            if want == "segmented":
+                assert int(segs) >= 4, segs
     eng = HipEngine(SimConfig(n=n, dtype=dtype, device="gpu", chunk=1024, mode=mode))
     eng.init_ics("solar+random", 5)
     eng.step(steps)
@@ -142,8 +169,10 @@ def test_rccl_multi_rank_match_single_rank(hip, tmp_path, world, strategy, mode,
                                             (2, "sym3")])
 def test_rccl_one_rank_full_schedule_bitwise(hip, monkeypatch, graph, strategy):
     """A live 1-rank RCCL communicator drives the whole multi-rank step (in-place
-    ncclAllGather, concurrent local/remote split, ordered reduce) — eagerly and captured into
-    a hipGraph (use_graph=2 captures the collective) — and must match the plain path."""
+    ncclAllGather, concurrent local/remote split, ordered reduce) — eagerly (one-sided
+    schedule, graph 1), as a segmented plan (sym, graph 1: compute segments captured, the
+    collectives eager between them) and captured whole (use_graph=2 captures the collective
+    too) — and must match the plain path."""
     from gravsim.config import SimConfig
     from gravsim.runtime.engines import HipEngine
 
@@ -172,6 +201,9 @@ def test_rccl_one_rank_full_schedule_bitwise(hip, monkeypatch, graph, strategy):
     eng.init_ics("solar+random", 4)
     eng.step(7)
     eng.sync(timeout_s=60)
+    gi = eng.graph_info()
+    if sym and graph == 1:  # a live communicator: the segmented plan, RCCL outside the graphs
+        assert gi["mode"] == "segmented" and gi["segments"] >= 4, gi
     got = eng.state().pos
     eng.close()
     monkeypatch.delenv("GRAVSIM_FORCE_COMM")
