@@ -13,12 +13,14 @@
 //     every chunk row carries the same amount of work and rank ownership is a plain block
 //     partition of rows;
 //   * both sides land in pre-assigned partial slots and are summed in a fixed order by the
-//     group-reduce and finalize kernels: deterministic, and the same bits for every rank
-//     count P dividing 8 (the group sums are what crosses ranks).
+//     node-reduce and finalize kernels (a binary tree over 64 row blocks): deterministic, and
+//     the same bits for every rank count P from 1 to 8 (the tree nodes are what crosses
+//     ranks; a rank owns whole row blocks by mpi.c:184-187's remainder rule).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "gravsim.h"
+#include "gs_common.h"
 #include "gs_kernels.h"
 #include "gs_sym_tile.h"
 
@@ -481,63 +483,160 @@ __global__ __launch_bounds__(Geo<double>::kThreads) GS_SYM_WPE64 void force_sym_
   force_sym_entry<double, EXACT, DEFER, DYN>(a);
 }
 
-// S_g(x) for this rank's groups and every body x of a real chunk: rows A of group g in
-// ascending order, each contributing Pj[A][d - 1] with d = (X - A) mod NC when X lies in
-// A's shell. Grid: (bodies / 256, groups per rank).
-template <typename T>
-__global__ __launch_bounds__(256) void sym_group_reduce_kernel(SymArgs a) {
-  const int64_t x = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (x >= (int64_t)a.real_chunks * kSymC) return;
-  const int gpr = kSymGroups / a.P;  // groups per rank
-  const int gl = blockIdx.y;
-  const int R = a.NC / kSymGroups;
-  const int g = (a.a0 / R) + gl;
-  const int X = (int)(x / kSymC), c = (int)(x % kSymC);
-  // Rows of group g inside the current band. The first band starts the sums at 0 (it writes
-  // every entry, so Sbuf needs no clearing); later bands continue them, which adds in the
-  // same order as one pass over the group. Entries of bodies past the real chunks are never
-  // read (finalize zeroes ghost bodies without reading Rbuf).
-  const int lo = max(g * R, a.a0 + a.band0);
-  const int hi = min(min((g + 1) * R, a.a0 + a.band0 + a.band_rows), a.real_chunks);
-  const bool first = a.band0 == 0;
-  if (lo >= hi && !first) return;
-  const int q = (int)(x / a.n_local);
-  const int64_t xl = x % a.n_local;
-  T* o = static_cast<T*>(a.Sbuf) + ((int64_t)q * gpr + gl) * 3 * a.n_local + xl;
-  const T* Pj = static_cast<const T*>(a.Pj);
-  T sx = T(0), sy = T(0), sz = T(0);
-  if (!first) {
-    sx = o[0];
-    sy = o[a.n_local];
-    sz = o[2 * a.n_local];
+// ---- canonical j-side reduction ----------------------------------------------------------
+// S(x) = sum over the rows A whose shell holds body x of Pj[A][d - 1] (d = (X - A) mod NC):
+// a binary tree over the B row blocks (gs_common.h sym_blocks), each leaf the row-ascending
+// sum of one block (rows outside X's shell add +0.0, an identity here: a sum started at +0.0
+// never becomes -0.0). A rank reduces the dyadic nodes covering its block range; the
+// receiver completes the tree with a binary-counter merge (left + right), so S(x) has the
+// same bits for every rank count.
+
+// Pending sub-trees of a binary-counter merge: acc[k] holds a finished node of 2^k blocks
+// while bit k of occ is set. Fully unrolled with constant indices (registers, no scratch).
+template <typename T, int C>
+struct TreeAcc {
+  T acc[7][C];
+  unsigned occ;
+  __device__ __forceinline__ void push(int level, T* v) {
+#pragma unroll
+    for (int k = 0; k < 7; ++k) {
+      if (k < level) continue;
+      if (occ & (1u << k)) {
+#pragma unroll
+        for (int c = 0; c < C; ++c) v[c] = acc[k][c] + v[c];  // left + right
+        occ &= ~(1u << k);
+      } else {
+#pragma unroll
+        for (int c = 0; c < C; ++c) acc[k][c] = v[c];
+        occ |= 1u << k;
+        return;
+      }
+    }
   }
-  // 4 rows' loads in flight, added in row order; rows outside X's shell add +0.0, an
-  // identity here (a sum started at +0.0 never becomes -0.0). Validity is wave-uniform.
+  __device__ __forceinline__ void result(T* v) const {  // occ holds exactly one bit
+#pragma unroll
+    for (int k = 0; k < 7; ++k)
+      if (occ == (1u << k)) {
+#pragma unroll
+        for (int c = 0; c < C; ++c) v[c] = acc[k][c];
+      }
+  }
+};
+
+// Row-ascending sum of Pj over rows [A_lo, A_hi) for body (X, c), one component per C:
+// the loads of U rows are issued ahead of their ordered adds; rows outside X's shell add 0.
+template <typename T, int C>
+__device__ __forceinline__ void pj_row_sum(const SymArgs& a, int A_lo, int A_hi, int X,
+                                           const T* pjc, int64_t comp_stride, T* out) {
+#pragma unroll
+  for (int k = 0; k < C; ++k) out[k] = T(0);
   constexpr int U = 4;
-  for (int A0 = lo; A0 < hi; A0 += U) {
-    T vx[U], vy[U], vz[U];
+  for (int A0 = A_lo; A0 < A_hi; A0 += U) {
+    T v[U][C];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int A = A0 + u;
       const int d = (X - A + a.NC) % a.NC;
-      vx[u] = vy[u] = vz[u] = T(0);
-      if (A < hi && d != 0 && d <= shell_len(A, a.NC, a.parity)) {
-        const T* p = Pj + ((int64_t)(A - a.a0 - a.band0) * a.H + (d - 1)) * 3 * kSymC + c;
-        vx[u] = p[0];
-        vy[u] = p[kSymC];
-        vz[u] = p[2 * kSymC];
-      }
+      const bool ok = A < A_hi && d != 0 && d <= shell_len(A, a.NC, a.parity);
+      const T* p = pjc + ((int64_t)(A - a.a0 - a.band0) * a.H + (d - 1)) * 3 * kSymC;
+#pragma unroll
+      for (int k = 0; k < C; ++k) v[u][k] = ok ? p[k * comp_stride] : T(0);
     }
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      sx += vx[u];
-      sy += vy[u];
-      sz += vz[u];
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int k = 0; k < C; ++k) out[k] += v[u][k];
+  }
+}
+
+// Owner rank of chunk row X.
+__device__ __forceinline__ int sym_row_owner(const SymArgs& a, int X) {
+  const int blk = X / a.RB;
+  int q = 0;
+  while (q + 1 < a.P && a.blk_lo[q + 1] <= blk) ++q;
+  return q;
+}
+
+// Multi-band runs: the leaf sum of every block inside the band (bands hold whole blocks),
+// into Bbuf[block - first own block][3][bodies]. Grid: (bodies / 256, blocks in the band).
+template <typename T>
+__global__ __launch_bounds__(256) void sym_block_reduce_kernel(SymArgs a) {
+  const int64_t nb = (int64_t)a.real_chunks * kSymC;
+  const int64_t x = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (x >= nb) return;
+  const int X = (int)(x / kSymC), c = (int)(x % kSymC);
+  const int b = (a.a0 + a.band0) / a.RB + (int)blockIdx.y;
+  const int A_lo = max(b * a.RB, 0), A_hi = min((b + 1) * a.RB, a.real_chunks);
+  T v[3];
+  pj_row_sum<T, 3>(a, A_lo, max(A_lo, A_hi), X, static_cast<const T*>(a.Pj) + c, kSymC, v);
+  T* o = static_cast<T*>(a.Bbuf) + (int64_t)(b - a.blk_lo[a.rank]) * 3 * nb + x;
+  o[0] = v[0];
+  o[nb] = v[1];
+  o[2 * nb] = v[2];
+}
+
+// Node k (blockIdx.y) of this rank's dyadic decomposition, for every body x of a real chunk:
+// the tree over the node's blocks, leaves from Pj directly (one band holds all the rank's
+// rows) or from Bbuf (multi-band runs). Output Sbuf[dest rank q][node k][3][n_local(q)].
+template <typename T>
+__global__ __launch_bounds__(256) void sym_node_reduce_kernel(SymArgs a) {
+  const int64_t nb = (int64_t)a.real_chunks * kSymC;
+  const int64_t x = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (x >= nb) return;
+  const int X = (int)(x / kSymC), c = (int)(x % kSymC);
+  const int own_lo = a.blk_lo[a.rank], own_hi = a.blk_lo[a.rank + 1];
+  int lo = own_lo, l = sym_dyadic_level(lo, own_hi);
+  for (int k = 0; k < (int)blockIdx.y; ++k) {
+    lo += 1 << l;
+    l = sym_dyadic_level(lo, own_hi);
+  }
+  TreeAcc<T, 3> t;
+  t.occ = 0;
+  const T* Bb = static_cast<const T*>(a.Bbuf);
+  for (int b = lo; b < lo + (1 << l); ++b) {
+    T v[3];
+    if (Bb) {
+      const T* p = Bb + (int64_t)(b - own_lo) * 3 * nb + x;
+      v[0] = p[0];
+      v[1] = p[nb];
+      v[2] = p[2 * nb];
+    } else {
+      const int A_lo = b * a.RB, A_hi = min((b + 1) * a.RB, a.real_chunks);
+      pj_row_sum<T, 3>(a, A_lo, max(A_lo, A_hi), X, static_cast<const T*>(a.Pj) + c, kSymC, v);
+    }
+    t.push(0, v);
+  }
+  T r[3];
+  t.result(r);
+  const int q = sym_row_owner(a, X);
+  const int64_t bq = (int64_t)a.blk_lo[q] * a.RB * kSymC;
+  const int64_t nlq = (int64_t)(a.blk_lo[q + 1] - a.blk_lo[q]) * a.RB * kSymC;
+  T* o = static_cast<T*>(a.Sbuf) + (int64_t)a.nn * 3 * bq + (int64_t)blockIdx.y * 3 * nlq +
+         (x - bq);
+  o[0] = r[0];
+  o[nlq] = r[1];
+  o[2 * nlq] = r[2];
+}
+
+// S(x) for an own body: every rank's nodes in global order from Rbuf[node][3][n_local],
+// merged into the full tree.
+template <typename T>
+__device__ __forceinline__ void sym_tree_all(const SymArgs& a, int64_t li, T* S) {
+  TreeAcc<T, 3> t;
+  t.occ = 0;
+  const T* R = static_cast<const T*>(a.Rbuf) + li;
+  int j = 0;
+  for (int q = 0; q < a.P; ++q) {
+    const int hi = a.blk_lo[q + 1];
+    for (int lo = a.blk_lo[q]; lo < hi; ++j) {
+      const int l = sym_dyadic_level(lo, hi);
+      const T* p = R + (int64_t)j * 3 * a.n_local;
+      T v[3] = {p[0], p[a.n_local], p[2 * a.n_local]};
+      t.push(l, v);
+      lo += 1 << l;
     }
   }
-  o[0] = sx;
-  o[a.n_local] = sy;
-  o[2 * a.n_local] = sz;
+  t.result(S);
 }
 
 // Ti = sum_q Pd[q] + sum_s Pi[s] (each ascending) for the bodies of the band's rows.
@@ -573,8 +672,9 @@ __global__ __launch_bounds__(256) void sym_row_reduce_kernel(SymArgs a) {
   static_cast<T*>(a.Ti)[(int64_t)k * a.n_local + (int64_t)(a.band0 + br) * kSymC + c] = acc;
 }
 
-// a = Ti + sum_g S_g, then kick-drift (cuda.cu:73-76, mpi.c:207-215) exactly as
-// the one-sided kernels' epilogue (nbody_kernels.hip integrate_store); ghost rows are zeroed.
+// a = Ti + S (the canonical tree over all ranks' nodes), then kick-drift (cuda.cu:73-76,
+// mpi.c:207-215) exactly as the one-sided kernels' epilogue (nbody_kernels.hip
+// integrate_store); ghost rows are zeroed.
 template <typename T>
 __global__ __launch_bounds__(256) void sym_finalize_kernel(SymArgs a) {
   using V4 = sym::Vec4<T>;
@@ -598,14 +698,9 @@ __global__ __launch_bounds__(256) void sym_finalize_kernel(SymArgs a) {
     return;
   }
   const T* ti = static_cast<const T*>(a.Ti) + li;
-  T ax = ti[0], ay = ti[a.n_local], az = ti[2 * a.n_local];
-  // Rbuf[source rank][its local group] in global group order g = 0..7.
-  for (int gg = 0; gg < kSymGroups; ++gg) {
-    const T* p = static_cast<const T*>(a.Rbuf) + (int64_t)gg * 3 * a.n_local + li;
-    ax += p[0];
-    ay += p[a.n_local];
-    az += p[2 * a.n_local];
-  }
+  T S[3];
+  sym_tree_all<T>(a, li, S);
+  const T ax = ti[0] + S[0], ay = ti[a.n_local] + S[1], az = ti[2 * a.n_local] + S[2];
   if (a.acc_out) {
     static_cast<V4*>(a.acc_out)[li] = V4{ax, ay, az, T(0)};
     return;
@@ -625,11 +720,11 @@ __global__ __launch_bounds__(256) void sym_finalize_kernel(SymArgs a) {
   static_cast<V4*>(a.X_next)[gi] = xn;
 }
 
-// One rank, one band: the group reduce, the row reduce and finalize in ONE kernel (no Sbuf /
+// One rank, one band: the node reduce, the row reduce and finalize in ONE kernel (no Sbuf /
 // Ti round trip, two launches fewer: at 65K bodies the three took ~28 us plus launch gaps of
 // a 0.73 ms step). The sums keep the exact order of the three-kernel path, so the bits are
-// the same: Ti = sum_q Pd (q ascending) + sum_s Pi (s ascending); S_g = sum of Pj over the
-// rows of group g (ascending, from 0); a = Ti + S_0 + ... + S_7. Block: 3 waves, wave k sums
+// the same: Ti = sum_q Pd (q ascending) + sum_s Pi (s ascending); S = the tree over the B
+// row blocks (leaves row-ascending from 0); a = Ti + S. Block: 3 waves, wave k sums
 // component k of 64 bodies (coalesced partial reads); wave 0 then integrates the 64 bodies.
 template <typename T>
 __global__ __launch_bounds__(192) void sym_tail_kernel(SymArgs a) {
@@ -666,30 +761,20 @@ __global__ __launch_bounds__(192) void sym_tail_kernel(SymArgs a) {
       for (int u = 0; u < U; ++u) ti += v[u];
     }
     for (; sg < segs; ++sg) ti += __builtin_nontemporal_load(pi + (int64_t)sg * 3 * kSymC);
-    // + S_g for g ascending (sym_group_reduce_kernel order, sums from 0; finalize order)
-    const int R = a.NC / kSymGroups;
-    const T* Pj = static_cast<const T*>(a.Pj) + k * kSymC + c;
-    // Rows outside X's shell add +0.0: an identity here, since a sum started at +0.0 never
-    // becomes -0.0, so the loads can be batched 8 at a time like the row reduce (validity is
-    // wave-uniform: the 64 bodies of a wave share their chunk X).
-    for (int g = 0; g < kSymGroups; ++g) {
-      const int hi = min((g + 1) * R, a.real_chunks);
-      T sgv = T(0);
-      for (int A0 = g * R; A0 < hi; A0 += U) {
-        T v[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const int A = A0 + u;
-          const int d = (X - A + a.NC) % a.NC;
-          const bool ok = A < hi && d != 0 && d <= shell_len(A, a.NC, a.parity);
-          v[u] = ok ? Pj[((int64_t)(A - a.a0) * a.H + (d - 1)) * 3 * kSymC] : T(0);
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) sgv += v[u];
-      }
-      ti += sgv;
+    // + S: the tree over the B row blocks (sym_node_reduce_kernel's single node [0, B))
+    TreeAcc<T, 1> t;
+    t.occ = 0;
+    const T* pjc = static_cast<const T*>(a.Pj) + k * kSymC + c;
+    for (int b = 0; b < a.B; ++b) {
+      const int A_lo = b * a.RB, A_hi = min((b + 1) * a.RB, a.real_chunks);
+      T v[1];
+      pj_row_sum<T, 1>(a, A_lo, max(A_lo, A_hi), X, pjc, kSymC, v);
+      t.push(0, v);
     }
-    acc_s[k][l] = ti;
+    T S[1];
+    t.result(S);
+    ti = ti + S[0];
+  acc_s[k][l] = ti;
   }
   __syncthreads();
   if (k != 0 || li >= a.n_local) return;
@@ -782,11 +867,22 @@ hipError_t launch_force_sym(const SymArgs& a, hipStream_t s) {
   return a.fp64 ? launch_force_sym_t<double>(a, s) : launch_force_sym_t<float>(a, s);
 }
 
-hipError_t launch_sym_group_reduce(const SymArgs& a, hipStream_t s) {
+hipError_t launch_sym_block_reduce(const SymArgs& a, hipStream_t s) {
+  if (!a.Bbuf || a.band_rows % a.RB || (a.a0 + a.band0) % a.RB) return hipErrorInvalidValue;
   const int64_t bodies = (int64_t)a.real_chunks * kSymC;
-  const dim3 grid((unsigned)((bodies + 255) / 256), kSymGroups / a.P);
-  if (a.fp64) hipLaunchKernelGGL(sym_group_reduce_kernel<double>, grid, dim3(256), 0, s, a);
-  else hipLaunchKernelGGL(sym_group_reduce_kernel<float>, grid, dim3(256), 0, s, a);
+  const dim3 grid((unsigned)((bodies + 255) / 256), (unsigned)(a.band_rows / a.RB));
+  if (a.fp64) hipLaunchKernelGGL(sym_block_reduce_kernel<double>, grid, dim3(256), 0, s, a);
+  else hipLaunchKernelGGL(sym_block_reduce_kernel<float>, grid, dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_sym_node_reduce(const SymArgs& a, hipStream_t s) {
+  // leaves from Pj need every own row in the slots (one band), else from Bbuf
+  if (!a.Bbuf && (a.band0 != 0 || a.band_rows != a.rows)) return hipErrorInvalidValue;
+  const int64_t bodies = (int64_t)a.real_chunks * kSymC;
+  const dim3 grid((unsigned)((bodies + 255) / 256), (unsigned)a.nn);
+  if (a.fp64) hipLaunchKernelGGL(sym_node_reduce_kernel<double>, grid, dim3(256), 0, s, a);
+  else hipLaunchKernelGGL(sym_node_reduce_kernel<float>, grid, dim3(256), 0, s, a);
   return hipGetLastError();
 }
 

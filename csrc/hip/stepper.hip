@@ -118,11 +118,20 @@ struct gs_stepper {
   char* sym_Pi = nullptr;  // element type: float or double (esz)
   char* sym_Pj = nullptr;
   char* sym_Pd = nullptr;
-  char* sym_S = nullptr;  // group sums by destination rank
-  char* sym_R = nullptr;  // group sums by source rank (== sym_S with one rank)
+  char* sym_S = nullptr;  // node sums by destination rank
+  char* sym_R = nullptr;  // node sums of every rank, global node order (== sym_S, one rank)
   char* sym_Ti = nullptr;  // per-body i-side totals [3][n_local]
+  char* sym_Bb = nullptr;  // multi-band runs: per-block leaf sums [own blocks][3][bodies]
   int32_t sym_NC = 0, sym_H = 0, sym_L = 0, sym_S_n = 0, sym_D = 1;
-  int32_t sym_band = 0;  // rows per band (Pi/Pj/Pd hold one band)
+  int32_t sym_band = 0;  // rows per band (Pi/Pj/Pd hold one band; a multiple of sym_RB)
+  // Row blocks and reduction-tree nodes (gs_sym_nodes): rank q owns blocks
+  // [blk_lo[q], blk_lo[q + 1]) = bodies [rbeg[q], rbeg[q] + rcnt[q]); it sends nn(q) nodes,
+  // the first of them global node nbase[q].
+  int32_t sym_B = 8, sym_RB = 1, sym_NN = 1;
+  int32_t blk_lo[9] = {0};
+  std::vector<int64_t> rbeg, rcnt;
+  std::vector<int32_t> nn, nbase;
+  bool uniform = true;  // every rank owns the same body count (P | B: ncclAllGather)
   hipEvent_t ev_sym = nullptr;
   // Per-rank emulation with modeled collectives (GRAVSIM_EMU_COMM_GBPS > 0): every all-gather
   // and group-sum exchange becomes a comm_model_kernel of the same byte count on s_comm.
@@ -301,11 +310,10 @@ bool multi(const gs_stepper* s) { return s->have_comm || s->emulate || s->virt; 
 // Bytes one rank receives per step: the all-gather's remote slices, and the group sums the
 // other ranks send it (sym schedule).
 size_t gather_bytes(const gs_stepper* s) {
-  return (size_t)(s->cfg.nranks - 1) * s->L.n_local * row_bytes(s);
+  return (size_t)(s->L.n_pad - s->L.n_local) * row_bytes(s);
 }
 size_t exchange_bytes(const gs_stepper* s) {
-  return (size_t)(s->cfg.nranks - 1) * (gs::kSymGroups / s->cfg.nranks) * 3 * s->L.n_local *
-         s->esz;
+  return (size_t)(s->sym_NN - s->nn[s->cfg.rank]) * 3 * s->L.n_local * s->esz;
 }
 
 // Emulated collective on s_comm (GRAVSIM_EMU_COMM_GBPS > 0): the byte count moved through HBM
@@ -385,8 +393,14 @@ gs::SymArgs sym_args(gs_stepper* s, int cur) {
   a.i_begin = s->L.local_begin;
   a.NC = s->sym_NC;
   a.P = s->cfg.nranks;
-  a.rows = s->sym_NC / s->cfg.nranks;
-  a.a0 = s->cfg.rank * a.rows;
+  a.rows = (int32_t)(s->L.n_local / gs::kSymC);
+  a.a0 = (int32_t)(s->L.local_begin / gs::kSymC);
+  a.B = s->sym_B;
+  a.RB = s->sym_RB;
+  a.rank = s->cfg.rank;
+  a.nn = s->nn[s->cfg.rank];
+  for (int q = 0; q <= s->cfg.nranks && q < 9; ++q) a.blk_lo[q] = s->blk_lo[q];
+  a.Bbuf = s->sym_Bb;
   a.S = s->sym_S_n;
   a.L = s->sym_L;
   a.D = s->sym_D;
@@ -425,13 +439,15 @@ gs::SymArgs sym_args(gs_stepper* s, int cur) {
 int sym_exchange_rccl(gs_stepper* s, bool join = true) {
   if (comp_record(s, s->ev_ready)) return -1;
   if (comm_do(s, [s]() -> int {
+        // To rank q: this rank's nn node sums of q's bodies (Sbuf block q); from rank q: its
+        // nn(q) node sums of this rank's bodies, at its global node offset in Rbuf.
         const int P = s->cfg.nranks, r = s->cfg.rank;
-        const size_t cnt = (size_t)(gs::kSymGroups / P) * 3 * s->L.n_local;  // elements
-        const size_t bytes = cnt * s->esz;
+        const size_t e = s->esz, nl = (size_t)s->L.n_local, my = (size_t)s->nn[r];
         const ncclDataType_t dt = s->esz == 8 ? ncclFloat64 : ncclFloat32;
         GS_HIP(hipStreamWaitEvent(s->s_comm, s->ev_ready, 0));
         GS_MARK(x0, x, s->s_comm);
-        GS_HIP(hipMemcpyAsync(s->sym_R + (size_t)r * bytes, s->sym_S + (size_t)r * bytes, bytes,
+        GS_HIP(hipMemcpyAsync(s->sym_R + (size_t)s->nbase[r] * 3 * nl * e,
+                              s->sym_S + my * 3 * (size_t)s->rbeg[r] * e, my * 3 * nl * e,
                               hipMemcpyDeviceToDevice, s->s_comm));
         if (s->emulate) {
           if (comm_model(s, s->sym_S, exchange_bytes(s))) return -1;
@@ -439,8 +455,10 @@ int sym_exchange_rccl(gs_stepper* s, bool join = true) {
           GS_NCCL(ncclGroupStart());
           for (int q = 0; q < P; ++q) {
             if (q == r) continue;
-            GS_NCCL(ncclSend(s->sym_S + (size_t)q * bytes, cnt, dt, q, s->comm, s->s_comm));
-            GS_NCCL(ncclRecv(s->sym_R + (size_t)q * bytes, cnt, dt, q, s->comm, s->s_comm));
+            GS_NCCL(ncclSend(s->sym_S + my * 3 * (size_t)s->rbeg[q] * e, my * 3 * s->rcnt[q], dt,
+                             q, s->comm, s->s_comm));
+            GS_NCCL(ncclRecv(s->sym_R + (size_t)s->nbase[q] * 3 * nl * e, (size_t)s->nn[q] * 3 * nl,
+                             dt, q, s->comm, s->s_comm));
           }
           GS_NCCL(ncclGroupEnd());
         }
@@ -461,7 +479,24 @@ int ensure_sym(gs_stepper* s) {
   if (s->L.mode != GS_MODE_SYM || s->sym_Pi) return 0;
   if (gs_sym_geometry(s->L.n_pad, &s->sym_NC, &s->sym_H, &s->sym_L, &s->sym_S_n, &s->sym_D))
     return -1;
-  const size_t nl = (size_t)s->L.n_local, rows = (size_t)s->sym_NC / s->cfg.nranks;
+  const int P = s->cfg.nranks;
+  s->rbeg.assign(P, 0);
+  s->rcnt.assign(P, 0);
+  s->nn.assign(P, 0);
+  s->nbase.assign(P, 0);
+  for (int q = 0; q < P; ++q) {
+    int32_t a0 = 0, rw = 0, nb = 0, nnq = 0;
+    if (gs_sym_rank_rows(s->L.n_pad, P, q, &a0, &rw) ||
+        gs_sym_nodes(s->L.n_pad, P, q, &s->sym_B, &s->sym_RB, &nnq, &nb, &s->sym_NN))
+      return -1;
+    s->rbeg[q] = (int64_t)a0 * gs::kSymC;
+    s->rcnt[q] = (int64_t)rw * gs::kSymC;
+    s->nn[q] = nnq;
+    s->nbase[q] = nb;
+    s->uniform = s->uniform && s->rcnt[q] == s->rcnt[0];
+  }
+  for (int q = 0; q <= P && q < 9; ++q) s->blk_lo[q] = gs::sym_blk_lo(s->sym_B, P, q);
+  const size_t nl = (size_t)s->L.n_local, rows = nl / gs::kSymC;
   const size_t e = s->esz;
   // Rows per band: the partial slots of one band stay within the budget: half of the free
   // HBM at creation (an MI355X has 288 GB; at least 32 GiB), GRAVSIM_SYM_BAND_MB overrides
@@ -472,19 +507,28 @@ int ensure_sym(gs_stepper* s) {
   size_t free_b = 0, total_b = 0;
   if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b / 2 > budget) budget = free_b / 2;
   if (const char* mb = getenv("GRAVSIM_SYM_BAND_MB")) budget = (size_t)atoll(mb) << 20;
-  size_t band = budget / per_row;
-  if (band < 1) band = 1;
+  // Bands hold whole row blocks, so each band's block leaves are complete (Bbuf).
+  const size_t rb = (size_t)s->sym_RB;
+  size_t band = budget / per_row / rb * rb;
+  if (band < rb) band = rb;
   if (band > rows) band = rows;
   s->sym_band = (int32_t)band;
   GS_HIP(hipMalloc(&s->sym_Pi, band * s->sym_S_n * 3 * gs::kSymC * e));
   GS_HIP(hipMalloc(&s->sym_Pj, band * s->sym_H * 3 * gs::kSymC * e));
   GS_HIP(hipMalloc(&s->sym_Pd, band * s->sym_D * 3 * gs::kSymC * e));
   GS_HIP(hipMalloc(&s->sym_Ti, 3 * nl * e));
-  GS_HIP(hipMalloc(&s->sym_S, (size_t)gs::kSymGroups * 3 * nl * e));
-  if (s->cfg.nranks > 1)
-    GS_HIP(hipMalloc(&s->sym_R, (size_t)gs::kSymGroups * 3 * nl * e));
-  else
-    s->sym_R = s->sym_S;
+  const size_t nb = (size_t)((s->L.n + gs::kSymC - 1) / gs::kSymC) * gs::kSymC;  // real chunks
+  if (band < rows) GS_HIP(hipMalloc(&s->sym_Bb, rows / rb * 3 * nb * e));
+  const int r = s->cfg.rank;
+  GS_HIP(hipMalloc(&s->sym_S, (size_t)s->nn[r] * 3 * (size_t)s->L.n_pad * e));
+  // (zeroed once: the per-rank emulation never receives the other ranks' nodes)
+  GS_HIP(hipMemsetAsync(s->sym_S, 0, (size_t)s->nn[r] * 3 * (size_t)s->L.n_pad * e, s->s_comp));
+  if (P > 1) {
+    GS_HIP(hipMalloc(&s->sym_R, (size_t)s->sym_NN * 3 * nl * e));
+    GS_HIP(hipMemsetAsync(s->sym_R, 0, (size_t)s->sym_NN * 3 * nl * e, s->s_comp));
+  } else {
+    s->sym_R = s->sym_S;  // [node 0][3][n_pad] either way
+  }
   return 0;
 }
 
@@ -552,6 +596,19 @@ int choose_groups(gs_stepper* s, int span, bool phi, bool concurrent = false) {
 }
 
 int ring_xfer_rccl(gs_stepper* s, int cur, int sub);
+int ring_src(const gs_stepper* s, int sub);
+
+// Bodies [*b0, *b0 + *cnt) of rank q's slice: the sym schedule's row blocks (uneven when P
+// does not divide the block count), else equal slices.
+void rank_slice(const gs_stepper* s, int q, int64_t* b0, int64_t* cnt) {
+  if (!s->rbeg.empty()) {
+    *b0 = s->rbeg[q];
+    *cnt = s->rcnt[q];
+  } else {
+    *b0 = (int64_t)q * s->L.n_local;
+    *cnt = s->L.n_local;
+  }
+}
 
 // In-place all-gather of X[cur] on s_comm (ev_gathered marks completion). With `gate` the
 // comm stream also publishes completion to a force launch already running (units 6). The sym
@@ -567,11 +624,11 @@ int gather(gs_stepper* s, int cur, bool gate = false) {
     const size_t count = (size_t)s->L.n_local * 4;
     GS_HIP(hipStreamWaitEvent(s->s_comm, s->ev_ready, 0));
     GS_MARK(g0, g, s->s_comm);
+    const ncclDataType_t dt = s->esz == 4 ? ncclFloat32 : ncclFloat64;
     if (s->sym_ring && use_sym(s)) {
-      const size_t slice = (size_t)s->L.n_local * row_bytes(s);
       for (int k = 1; k < s->cfg.nranks; ++k) {
         if (s->emulate) {
-          if (comm_model(s, buf, slice)) return -1;
+          if (comm_model(s, buf, (size_t)s->rcnt[ring_src(s, k)] * row_bytes(s))) return -1;
         } else if (ring_xfer_rccl(s, cur, k)) {
           return -1;
         }
@@ -579,9 +636,18 @@ int gather(gs_stepper* s, int cur, bool gate = false) {
       }
     } else if (s->emulate) {
       if (comm_model(s, buf, gather_bytes(s))) return -1;
+    } else if (!use_sym(s) || s->uniform) {
+      GS_NCCL(ncclAllGather(buf + (size_t)s->L.local_begin * row_bytes(s), buf, count, dt,
+                            s->comm, s->s_comm));
     } else {
-      GS_NCCL(ncclAllGather(buf + (size_t)s->cfg.rank * s->L.n_local * row_bytes(s), buf, count,
-                            s->esz == 4 ? ncclFloat32 : ncclFloat64, s->comm, s->s_comm));
+      // Uneven row blocks (P not dividing the block count): every rank broadcasts its own
+      // slice in place, all P in one group call (the Allgatherv of mpi.c:227-231).
+      GS_NCCL(ncclGroupStart());
+      for (int q = 0; q < s->cfg.nranks; ++q) {
+        char* sl = buf + (size_t)s->rbeg[q] * row_bytes(s);
+        GS_NCCL(ncclBroadcast(sl, sl, (size_t)s->rcnt[q] * 4, dt, q, s->comm, s->s_comm));
+      }
+      GS_NCCL(ncclGroupEnd());
     }
     GS_MARK(g1, g, s->s_comm);
     if (gate && !(s->sym_ring && use_sym(s)))
@@ -616,13 +682,15 @@ void rank_chunks(const gs_stepper* s, int src, int* c0, int* c1) {
 int ring_xfer_rccl(gs_stepper* s, int cur, int sub) {
   const int P = s->cfg.nranks, r = s->cfg.rank;
   char* buf = static_cast<char*>(s->X[cur]);
-  const size_t slice = (size_t)s->L.n_local * row_bytes(s);
-  const size_t count = (size_t)s->L.n_local * 4;
   const ncclDataType_t dt = s->esz == 4 ? ncclFloat32 : ncclFloat64;
-  const int send_src = ring_src(s, sub - 1), recv_src = ring_src(s, sub);
+  int64_t sb, sc, rb, rc;
+  rank_slice(s, ring_src(s, sub - 1), &sb, &sc);
+  rank_slice(s, ring_src(s, sub), &rb, &rc);
   GS_NCCL(ncclGroupStart());
-  GS_NCCL(ncclSend(buf + send_src * slice, count, dt, (r + 1) % P, s->comm, s->s_comm));
-  GS_NCCL(ncclRecv(buf + recv_src * slice, count, dt, (r - 1 + P) % P, s->comm, s->s_comm));
+  GS_NCCL(ncclSend(buf + (size_t)sb * row_bytes(s), (size_t)sc * 4, dt, (r + 1) % P, s->comm,
+                   s->s_comm));
+  GS_NCCL(ncclRecv(buf + (size_t)rb * row_bytes(s), (size_t)rc * 4, dt, (r - 1 + P) % P, s->comm,
+                   s->s_comm));
   GS_NCCL(ncclGroupEnd());
   return 0;
 }
@@ -746,8 +814,9 @@ int sym_force(gs_stepper* s, gs::SymArgs a, bool overlap_gather, bool exchange =
       GS_HIP(force_sym_launch(s, a, s->s_comp));
     }
     if (fused_tail(s)) continue;  // reductions + integrate in sym_tail_kernel (one band)
-    GS_HIP(gs::launch_sym_group_reduce(a, s->s_comp));
     const bool last = b0 + a.band_rows >= a.rows;
+    if (a.Bbuf) GS_HIP(gs::launch_sym_block_reduce(a, s->s_comp));  // the band's leaves
+    if (last) GS_HIP(gs::launch_sym_node_reduce(a, s->s_comp));
     if (exchange && last && sym_exchange_rccl(s, false)) return -1;
     GS_HIP(gs::launch_sym_row_reduce(a, s->s_comp));
     if (exchange && last) {
@@ -761,8 +830,7 @@ int sym_force(gs_stepper* s, gs::SymArgs a, bool overlap_gather, bool exchange =
 
 int enqueue_sym(gs_stepper* s, int cur, bool need_gather, bool gathered_externally, int part,
                 bool timed) {
-  gs::SymArgs a = sym_args(s, cur);
-  if (s->emulate) a.Rbuf = s->sym_S;  // timing emulation: modeled exchange, stale sums
+  gs::SymArgs a = sym_args(s, cur);  // (emulation: the other ranks' nodes in Rbuf stay 0)
   // Gate the remote units on the gather in-kernel (GRAVSIM_SYM_OVERLAP=3): a collective of
   // this stepper (RCCL or modeled) and one band (the gated launch covers every unit).
   const bool gated = part == 3 && need_gather && !gathered_externally && xcomm(s) &&
@@ -1274,7 +1342,7 @@ int gs_stepper_create(const gs_config* cfg, gs_stepper** out) {
   }
   if (s->L.mode == GS_MODE_SYM) {
     // Deferred-unit list of the gated launch (one band's units) and the local-first order.
-    const int rows = s->sym_NC / cfg->nranks;
+    const int rows = (int)(s->L.n_local / gs::kSymC);
     const size_t units = (size_t)rows * (s->sym_S_n + s->sym_D) + 1;
     FAIL_CLEAN(hipMalloc(&s->defer, units * sizeof(unsigned)));
     FAIL_CLEAN(hipMemsetAsync(s->defer, 0, units * sizeof(unsigned), s->s_comp));
@@ -1332,7 +1400,7 @@ int gs_stepper_destroy(gs_stepper* s) {
                   (void*)s->nonfinite, (void*)s->sym_Pi, (void*)s->sym_Pj, (void*)s->sym_Pd,
                   (void*)s->sym_S, (void*)s->sym_R, (void*)s->sym_Ti, (void*)s->gate_buf,
                   (void*)s->defer, (void*)s->sym_lf, s->emu_buf, (void*)s->utrace,
-                  (void*)s->ring_gate, (void*)s->audit})
+                  (void*)s->ring_gate, (void*)s->audit, (void*)s->sym_Bb})
     if (p) (void)hipFree(p);
   for (hipEvent_t e : {s->ev_ready, s->ev_gathered, s->ev_t0, s->ev_local, s->ev_end,
                        s->ev_remote, s->ev_fork, s->ev_rem2, s->ev_sym})
@@ -1497,7 +1565,7 @@ int gs_stepper_audit(gs_stepper* s, uint64_t* units_done, uint64_t* units_per_st
   if (units_per_step) *units_per_step = 0;
   if (!s->audit) return 0;  // one-sided schedules: no unit audit
   GS_HIP(hipSetDevice(s->cfg.device));
-  const uint64_t rows = (uint64_t)(s->sym_NC / s->cfg.nranks);
+  const uint64_t rows = (uint64_t)(s->L.n_local / gs::kSymC);
   if (units_per_step) *units_per_step = rows * (uint64_t)(s->sym_S_n + s->sym_D);
   if (units_done) {
     GS_HIP(hipStreamSynchronize(s->s_comp));
@@ -1668,7 +1736,7 @@ int gs_group_step(gs_stepper** sh, int32_t P, int32_t nsteps) {
   GS_HIP(hipSetDevice(sh[0]->cfg.device));
   for (int r = 0; r < P; ++r) sh[r]->virt = P > 1;
   hipStream_t gsm = sh[0]->s_comm;
-  const size_t slice = (size_t)sh[0]->L.n_local * row_bytes(sh[0]);
+  const int64_t rbytes = (int64_t)row_bytes(sh[0]);
   for (int32_t it = 0; it < nsteps; ++it) {
     const int cur = (int)(sh[0]->k & 1);
     const bool need = P > 1 && !sh[0]->full[cur];
@@ -1690,8 +1758,10 @@ int gs_group_step(gs_stepper** sh, int32_t P, int32_t nsteps) {
       for (int sub = 1; sub < P; ++sub) {
         for (int r = 0; r < P; ++r) {
           const int left = (r - 1 + P) % P, src = ring_src(sh[r], sub);
-          GS_HIP(hipMemcpyAsync(static_cast<char*>(sh[r]->X[cur]) + src * slice,
-                                static_cast<char*>(sh[left]->X[cur]) + src * slice, slice,
+          int64_t b0, cnt;
+          rank_slice(sh[0], src, &b0, &cnt);
+          GS_HIP(hipMemcpyAsync(static_cast<char*>(sh[r]->X[cur]) + b0 * rbytes,
+                                static_cast<char*>(sh[left]->X[cur]) + b0 * rbytes, cnt * rbytes,
                                 hipMemcpyDeviceToDevice, gsm));
         }
         for (int r = 0; r < P; ++r) GS_HIP(hipEventRecord(sh[r]->ev_recv[sub], gsm));
@@ -1720,24 +1790,30 @@ int gs_group_step(gs_stepper** sh, int32_t P, int32_t nsteps) {
       for (int dst = 0; dst < P; ++dst)
         for (int src = 0; src < P; ++src) {
           if (src == dst) continue;
-          GS_HIP(hipMemcpyAsync(static_cast<char*>(sh[dst]->X[cur]) + src * slice,
-                                static_cast<char*>(sh[src]->X[cur]) + src * slice, slice,
+          int64_t b0, cnt;
+          rank_slice(sh[0], src, &b0, &cnt);
+          GS_HIP(hipMemcpyAsync(static_cast<char*>(sh[dst]->X[cur]) + b0 * rbytes,
+                                static_cast<char*>(sh[src]->X[cur]) + b0 * rbytes, cnt * rbytes,
                                 hipMemcpyDeviceToDevice, gsm));
         }
       for (int r = 0; r < P; ++r) GS_HIP(hipEventRecord(sh[r]->ev_gathered, gsm));
     }
     if (use_sym(sh[0]) && P > 1) {
-      // Symmetric schedule: force + group reduce on every shard, then the group-sum
-      // exchange as device copies (shard r's block for q -> shard q's slot r), then finalize.
-      const size_t cnt = (size_t)(gs::kSymGroups / P) * 3 * sh[0]->L.n_local * sh[0]->esz;
+      // Symmetric schedule: force + node reduce on every shard, then the node-sum exchange
+      // as device copies (shard r's block for q -> shard q's slots of r's nodes), then
+      // finalize.
+      const size_t e = sh[0]->esz;
       for (int r = 0; r < P; ++r)
         if (enqueue_sym(sh[r], cur, need, true, 1, false)) return -1;
       for (int r = 0; r < P; ++r) GS_HIP(hipEventRecord(sh[r]->ev_ready, sh[r]->s_comp));
       for (int r = 0; r < P; ++r) GS_HIP(hipStreamWaitEvent(gsm, sh[r]->ev_ready, 0));
       for (int q = 0; q < P; ++q)
-        for (int r = 0; r < P; ++r)
-          GS_HIP(hipMemcpyAsync(sh[q]->sym_R + (size_t)r * cnt, sh[r]->sym_S + (size_t)q * cnt,
-                                cnt, hipMemcpyDeviceToDevice, gsm));
+        for (int r = 0; r < P; ++r) {
+          const size_t nr = (size_t)sh[0]->nn[r], nlq = (size_t)sh[0]->rcnt[q];
+          GS_HIP(hipMemcpyAsync(sh[q]->sym_R + (size_t)sh[0]->nbase[r] * 3 * nlq * e,
+                                sh[r]->sym_S + nr * 3 * (size_t)sh[0]->rbeg[q] * e,
+                                nr * 3 * nlq * e, hipMemcpyDeviceToDevice, gsm));
+        }
       GS_HIP(hipEventRecord(sh[0]->ev_sym, gsm));
       for (int r = 0; r < P; ++r) {
         GS_HIP(hipStreamWaitEvent(sh[r]->s_comp, sh[0]->ev_sym, 0));

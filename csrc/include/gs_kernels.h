@@ -37,20 +37,22 @@ inline int split_span(const KArgs<T>& a) {
 
 // ---- Newton-3 symmetric schedule (fp32/fp64, fast cutoff; nbody_sym.hip) -------------
 // Canonical decomposition, a function of the padded body count only (so every rank count
-// P | 8 produces the same bits): chunks of kSymC = 2048 bodies, NC = n_pad / 2048 of them,
-// G = 8 row groups of NC / 8 chunks. Chunk A pairs with the next h(A) chunks cyclically
-// (h = NC/2 - 1, plus the antipodal chunk A + NC/2 for half of the rows, alternating by
-// parity: every unordered chunk pair exactly once, equal work per block of rows) and with
-// itself (one-sided). Row A's shell is cut into segments of L quanta (128 bodies; see
-// gs_sym_geometry), its diagonal chunk into D parts; one workgroup per unit writes an i-side
-// partial (Pi[row][segment] or Pd[row][part]) and, for every shell tile it visits, the
-// j-side partial of its 2048 i-bodies into Pj[row][d-1]. Rows are processed in bands (all of
-// a rank's rows unless the partial buffers would exceed the band budget); per band the group
-// reduce continues S_g(x) (rows A of group g ascending, S zeroed at step start) and the row
-// reduce forms Ti = sum_q Pd[q] + sum_s Pi[s]. Final: a = Ti + sum_g S_g (g ascending), then
-// the KD integrate. Every sum runs in the same order for any band size and any P | 8.
+// P from 1 to 8 produces the same bits): chunks of kSymC = 2048 bodies, NC = n_pad / 2048 of
+// them, B row blocks of RB = NC / B rows (gs_common.h sym_blocks: B <= 64). Chunk A pairs
+// with the next h(A) chunks cyclically (h = NC/2 - 1, plus the antipodal chunk A + NC/2 for
+// half of the rows, alternating by parity: every unordered chunk pair exactly once, equal
+// work per block of rows) and with itself (one-sided). Row A's shell is cut into segments of
+// L quanta (128 bodies; see gs_sym_geometry), its diagonal chunk into D parts; one workgroup
+// per unit writes an i-side partial (Pi[row][segment] or Pd[row][part]) and, for every shell
+// tile it visits, the j-side partial of its 2048 i-bodies into Pj[row][d-1]. Rows are
+// processed in bands of whole blocks (all of a rank's rows unless the partial buffers would
+// exceed the band budget); the row reduce forms Ti = sum_q Pd[q] + sum_s Pi[s] per band. The
+// j-side sums reach a body as S = a binary tree over the B blocks (leaves row-ascending); a
+// rank owns whole blocks (mpi.c's remainder rule) and reduces the dyadic nodes covering its
+// range (from Pj with one band, from per-block leaves in Bbuf with several). Final:
+// a = Ti + S, then the KD integrate. Every sum runs in the same order for any band size and
+// any P from 1 to 8.
 constexpr int kSymC = 2048;
-constexpr int kSymGroups = 8;
 
 struct SymArgs {
   // Arrays are float (fp32 run) or double (fp64 run); the launchers pick the instantiation.
@@ -59,14 +61,18 @@ struct SymArgs {
   void* Pj;            // [rows][H][3][kSymC] j-side partials, H = NC / 2
   void* Pd;            // [rows][D][3][kSymC] diagonal-chunk partials
   void* Ti;            // [3][n_local] per-body i-side total: sum_q Pd[q] + sum_s Pi[s]
-  void* Sbuf;          // [P][G/P][3][n_local] group sums by destination rank
-  const void* Rbuf;    // [P][G/P][3][n_local] group sums received, by source rank
+  void* Sbuf;          // [dest rank q][own node k < nn][3][n_local(q)] node sums by destination
+  const void* Rbuf;    // [node j, all ranks' nodes in global order][3][n_local] received
+  void* Bbuf;          // multi-band only: [own block][3][real bodies] per-block leaf sums
   void* X_next;        // [n_pad * 4]
   void* vel;           // [n_local * 4]
   void* acc_out;       // optional [n_local * 4]: emit accelerations instead of integrating
   int64_t n_real, n_local, i_begin;
   int32_t NC, a0, rows, S, L, H, P, real_chunks;
   int32_t D;           // parts of the diagonal chunk (L < 16 quanta: 16 / L)
+  int32_t B, RB;       // row blocks and rows per block
+  int32_t rank, nn;    // this rank and the dyadic nodes it reduces and sends
+  int32_t blk_lo[9];   // rank q owns blocks [blk_lo[q], blk_lo[q + 1]), q < P
   int32_t band0, band_rows;  // rows [band0, band0 + band_rows) of this rank (rank-relative)
                              // are in the Pi/Pj/Pd buffers (row index - band0)
   int32_t fp64;        // element type of every array above
@@ -116,7 +122,8 @@ hipError_t launch_force_sym(const SymArgs& a, hipStream_t s);
 hipError_t launch_comm_model(const void* src, void* dst, size_t bytes, uint64_t ticks, int wgs,
                              hipStream_t s);
 hipError_t launch_gate_set(unsigned* gate, hipStream_t s);
-hipError_t launch_sym_group_reduce(const SymArgs& a, hipStream_t s);  // accumulates into Sbuf
+hipError_t launch_sym_block_reduce(const SymArgs& a, hipStream_t s);  // band leaves -> Bbuf
+hipError_t launch_sym_node_reduce(const SymArgs& a, hipStream_t s);   // own nodes -> Sbuf
 hipError_t launch_sym_row_reduce(const SymArgs& a, hipStream_t s);    // the band's rows -> Ti
 hipError_t launch_sym_finalize(const SymArgs& a, hipStream_t s);
 // One rank, one band: group reduce + row reduce + finalize in one kernel, same bits.

@@ -24,8 +24,8 @@ int main() {
   // layout: every (n, P) partitions the padded range exactly, chunk independent of P
   for (int64_t n : {1, 3, 1000, 2048, 2049, 100003}) {
     int32_t chunk0 = -1;
-    for (int P : {1, 2, 3, 8}) {
-      int64_t covered = 0;
+    for (int P : {1, 2, 3, 7, 8}) {
+      int64_t covered = 0, n_pad = 0;
       for (int r = 0; r < P; ++r) {
         gs_config c{};
         c.n = n; c.rank = r; c.nranks = P;
@@ -33,10 +33,16 @@ int main() {
         EXPECT(gs_layout_compute(&c, &L) == 0, "layout n=%lld P=%d", (long long)n, P);
         EXPECT(L.local_begin == covered, "slice order");
         covered += L.n_local;
+        n_pad = L.n_pad;
         if (chunk0 < 0) chunk0 = L.chunk;
         EXPECT(L.chunk == chunk0, "chunk depends on P");
-        EXPECT(L.n_pad % ((int64_t)P * L.chunk) == 0, "padding");
+        // one-sided schedules: equal slices; sym: whole 2048-row blocks, possibly uneven
+        if (L.mode == GS_MODE_SYM)
+          EXPECT(L.n_pad % 16384 == 0 && L.n_local % 2048 == 0, "sym padding");
+        else
+          EXPECT(L.n_pad % ((int64_t)P * L.chunk) == 0, "padding");
       }
+      EXPECT(covered == n_pad, "slices tile the padded range");
     }
   }
   gs_config bad{};

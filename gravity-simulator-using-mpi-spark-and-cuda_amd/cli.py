@@ -41,7 +41,7 @@ def build_parser() -> argparse.ArgumentParser:
                    help="GPU force kernel: lds (LDS-DMA j tiles), smem (SGPR j stream), mfma "
                         "(experimental fp32: r^2 on the matrix cores, re-centred; slower)")
     p.add_argument("--mode", choices=["auto", "fused", "split", "sym"], default=d.mode,
-                   help="GPU schedule; sym = Newton-3 pairs (fp32, fast cutoff, P | 8)")
+                   help="GPU schedule; sym = Newton-3 pairs (any P <= 8; the default from 16K bodies)")
     p.add_argument("--ipl", type=int, default=d.ipl, choices=[0, 1, 2, 4, 8])
     p.add_argument("--chunk", type=int, default=d.chunk)
     p.add_argument("--no-graph", dest="graph", action="store_false")

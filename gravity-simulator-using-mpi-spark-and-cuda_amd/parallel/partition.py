@@ -10,6 +10,11 @@ order fixed, so instead:
 * rank r owns rows [r*n_pad/P, (r+1)*n_pad/P);
 * every body's acceleration is sum over chunks c (in order) of a chunk sum that starts at 0,
   so partials computed on any rank, in any launch shape, add up to the same bits.
+
+The Newton-3 (sym) schedule pads as an 8-rank run would and cuts its NC chunk rows into B
+row blocks (B <= 64, a power of two dividing NC); rank r owns whole blocks by mpi.c's own
+remainder rule (the first B mod P ranks hold one more), so every P from 1 to 8 is balanced to
+within one block and the reduction tree over the blocks keeps the bits P-independent.
 """
 from __future__ import annotations
 
@@ -86,11 +91,60 @@ def sym_geometry(n_pad: int) -> dict:
     return {"NC": nc, "H": h, "L": seg, "S": -(-16 * h // seg), "D": 16 // seg if seg < 16 else 1}
 
 
+def sym_blocks(nc: int) -> int:
+    """Row blocks of the sym schedule: the largest power of two <= 64 dividing NC."""
+    b = 64
+    while b > 1 and nc % b:
+        b >>= 1
+    return b
+
+
+def sym_blk_lo(B: int, P: int, r: int) -> int:
+    """First block of rank r (mpi.c:184-187's remainder rule over the B blocks)."""
+    base, rem = divmod(B, P)
+    return r * base + min(r, rem)
+
+
+def dyadic_nodes(lo: int, hi: int) -> list[tuple[int, int]]:
+    """(first block, level) of the aligned power-of-two pieces covering [lo, hi)."""
+    out = []
+    while lo < hi:
+        l = 0
+        while (lo >> l) & 1 == 0 and lo + (2 << l) <= hi:
+            l += 1
+        out.append((lo, l))
+        lo += 1 << l
+    return out
+
+
+def sym_rank_rows(n_pad: int, nranks: int, rank: int) -> tuple[int, int]:
+    """(first row, rows) of one rank in the sym schedule (layout.cpp gs_sym_rank_rows)."""
+    nc = n_pad // SYM_CHUNK
+    B = sym_blocks(nc)
+    if not 1 <= nranks <= B or not 0 <= rank < nranks:
+        raise ValueError("sym: nranks must be 1 .. the row-block count")
+    rb = nc // B
+    lo, hi = sym_blk_lo(B, nranks, rank), sym_blk_lo(B, nranks, rank + 1)
+    return lo * rb, (hi - lo) * rb
+
+
+def sym_nodes(n_pad: int, nranks: int) -> list[list[tuple[int, int]]]:
+    """Per rank, the reduction-tree nodes it sends (layout.cpp gs_sym_nodes)."""
+    B = sym_blocks(n_pad // SYM_CHUNK)
+    return [dyadic_nodes(sym_blk_lo(B, nranks, q), sym_blk_lo(B, nranks, q + 1))
+            for q in range(nranks)]
+
+
 def sym_bytes(n_pad: int, nranks: int, esz: int = 4) -> int:
-    """Partial-slot bytes per rank if all of the rank's rows were held at once (one band)."""
+    """Partial-slot bytes of rank 0 (the largest share) if all its rows were held at once
+    (one band), plus the node sums it sends and receives (layout.cpp gs_sym_bytes)."""
     g = sym_geometry(n_pad)
-    n_local = n_pad // nranks
-    return n_local * 3 * esz * (g["S"] + g["H"] + g["D"]) + 2 * n_local * SYM_GROUPS * 3 * esz
+    _, rows = sym_rank_rows(n_pad, nranks, 0)
+    n_local = rows * SYM_CHUNK
+    nodes = sym_nodes(n_pad, nranks)
+    NN = sum(len(x) for x in nodes)
+    return n_local * 3 * esz * (g["S"] + g["H"] + g["D"]) + \
+        (len(nodes[0]) * n_pad + NN * n_local) * 3 * esz
 
 
 def sym_auto(n: int, nranks: int, chunk: int = 0, dtype: str = "fp32") -> bool:
@@ -98,8 +152,8 @@ def sym_auto(n: int, nranks: int, chunk: int = 0, dtype: str = "fp32") -> bool:
     del chunk  # (the choice depends on n, the rank count and the dtype only)
     # from 16K (fp32) / 32K (fp64) bodies sym wins, padding included
     # (profiles/r2_sizes_auto_vs_sym.txt); the partial slots are processed in bounded bands,
-    # so memory does not limit the choice
-    return 8 % nranks == 0 and n >= (16384 if dtype == "fp32" else 32768)
+    # so memory does not limit the choice; any P up to 8 owns whole row blocks
+    return nranks <= 8 and n >= (16384 if dtype == "fp32" else 32768)
 
 
 def layout(n: int, rank: int = 0, nranks: int = 1, chunk: int = 0, sym: bool = False) -> Layout:
@@ -110,11 +164,17 @@ def layout(n: int, rank: int = 0, nranks: int = 1, chunk: int = 0, sym: bool = F
     c = chunk or auto_chunk(n)
     if c % 1024:
         raise ValueError("chunk must be a multiple of 1024")
-    if sym and 8 % nranks:
-        raise ValueError("the sym schedule needs nranks dividing 8")
-    n_pad = sym_pad(n, c) if sym else round_up(n, nranks * c)
-    n_local = n_pad // nranks
-    return Layout(n=n, n_pad=n_pad, n_local=n_local, local_begin=rank * n_local, chunk=c,
+    if sym and nranks > 8:
+        raise ValueError("the sym schedule needs nranks <= 8")
+    if sym:
+        n_pad = sym_pad(n, c)
+        a0, rows = sym_rank_rows(n_pad, nranks, rank)
+        begin, n_local = a0 * SYM_CHUNK, rows * SYM_CHUNK
+    else:
+        n_pad = round_up(n, nranks * c)
+        n_local = n_pad // nranks
+        begin = rank * n_local
+    return Layout(n=n, n_pad=n_pad, n_local=n_local, local_begin=begin, chunk=c,
                   n_chunks=(n + c - 1) // c, rank=rank, nranks=nranks)
 
 

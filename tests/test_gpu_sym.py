@@ -4,7 +4,7 @@ Reference: cuda.cu:53-60 evaluates each pair once (j > i) and scatters +F/-F int
 bodies (cuda.cu:43-49) with a data race; pyspark.py:80-84 does the same
 pair reduction on the driver. The sym schedule keeps the pair-once saving race-free; these
 tests pin its accuracy against the fp64 oracle, its determinism, graph replay, and bitwise
-independence of the rank count (virtual ranks, P | 8).
+independence of the rank count (virtual ranks, every P up to 8).
 """
 import numpy as np
 import pytest
@@ -118,9 +118,12 @@ def test_sym_determinism_and_graph(hip):
 
 
 @pytest.mark.parametrize("P,dtype", [(2, "fp32"), (4, "fp32"), (8, "fp32"), (2, "fp64"),
-                                     (8, "fp64")])
+                                     (8, "fp64"), (3, "fp32"), (6, "fp32"), (7, "fp32"),
+                                     (5, "fp64")])
 def test_sym_virtual_ranks_bitwise(hip, P, dtype):
-    """P shards (all-gather + group-sum exchange by device copies) == 1 rank, bitwise."""
+    """P shards (all-gather + node-sum exchange by device copies) == 1 rank, bitwise, for
+    every P up to 8: P not dividing the 8 row blocks of 40,000 bodies gives uneven slices
+    (P = 3: 3/3/2 blocks, 7: 2/1/1/1/1/1/1), mpi.c's remainder rule."""
     from gravsim.runtime.engines import VirtualGroup
 
     cfg = SimConfig(n=40000, dtype=dtype, device="gpu", mode="sym")
@@ -182,7 +185,7 @@ def test_sym_fp64_close_to_split(hip):
     assert rel < 1e-13
 
 
-@pytest.mark.parametrize("P,dtype", [(1, "fp32"), (2, "fp32"), (1, "fp64")])
+@pytest.mark.parametrize("P,dtype", [(1, "fp32"), (2, "fp32"), (1, "fp64"), (3, "fp32")])
 def test_sym_bands_bitwise(hip, monkeypatch, P, dtype):
     """Processing the rows in many small bands (bounded partial memory) gives the same bits
     as one band: every sum continues in the same order."""

@@ -16,7 +16,7 @@ from gravsim.parallel import partition
 
 @pytest.mark.parametrize("n", [1, 2, 3, 8, 1000, 2048, 2049, 16383, 16384, 20000, 32768, 65536,
                                100_003, 1 << 20, 16_777_216])
-@pytest.mark.parametrize("P", [1, 2, 3, 4, 8])
+@pytest.mark.parametrize("P", [1, 2, 3, 4, 5, 6, 7, 8])
 @pytest.mark.parametrize("dtype", ["fp32", "fp64"])
 def test_python_layout_matches_native(n, P, dtype):
     lib = _native.cpu_lib()
@@ -30,7 +30,9 @@ def test_python_layout_matches_native(n, P, dtype):
         p = partition.layout(n, r, P, sym=sym)
         assert (L.n_pad, L.n_local, L.local_begin, L.chunk, L.n_chunks) == \
             (p.n_pad, p.n_local, p.local_begin, p.chunk, p.n_chunks)
-        assert p.n_pad % (P * p.chunk) == 0 and p.n_pad >= n
+        assert p.n_pad >= n
+        if not sym:
+            assert p.n_pad % (P * p.chunk) == 0
         assert p.chunk == partition.auto_chunk(n)  # chunk depends on n only
 
 
@@ -115,10 +117,10 @@ def test_mfma_kernel_config_validation():
 
 
 @pytest.mark.parametrize("n", [1000, 20000, 100_003, 1 << 20])
-@pytest.mark.parametrize("P", [1, 2, 4, 8])
+@pytest.mark.parametrize("P", [1, 2, 3, 4, 5, 6, 7, 8])
 def test_sym_layout_independent_of_world_size(n, P):
-    """mode=sym pads as an 8-rank run would: n_pad (hence the chunk/row/group structure and
-    the summation order) is the same for every P dividing 8, and matches the native layout."""
+    """mode=sym pads as an 8-rank run would: n_pad (hence the chunk/row/block structure and
+    the summation order) is the same for every P up to 8, and matches the native layout."""
     lib = _native.cpu_lib()
     c = _native.GsConfig(n=n, dtype=0, rank=P - 1, nranks=P, device=0,
                          mode=_native.MODE_IDS["sym"])
@@ -145,7 +147,7 @@ def test_sym_layout_independent_of_world_size(n, P):
 
 def test_sym_layout_rejects_unsupported():
     lib = _native.cpu_lib()
-    for kw in (dict(nranks=3, rank=0), dict(kernel=3)):
+    for kw in (dict(nranks=9, rank=0), dict(kernel=3)):
         base = dict(n=50000, dtype=0, rank=0, nranks=1, device=0, mode=_native.MODE_IDS["sym"])
         base.update(kw)
         L = _native.GsLayout()
@@ -153,7 +155,13 @@ def test_sym_layout_rejects_unsupported():
 
 
 def test_sym_auto_at_headline_size():
-    """N = 1M fp32 picks the Newton-3 schedule for P = 1, 2, 4, 8 with unchanged padding."""
-    for P in (1, 2, 4, 8):
+    """N = 1M fp32 picks the Newton-3 schedule for every P from 1 to 8 with unchanged
+    padding; ranks own whole row blocks of 8 rows (64 blocks), mpi.c's remainder rule."""
+    for P in range(1, 9):
         assert partition.sym_auto(1 << 20, P)
-        assert partition.layout(1 << 20, 0, P, sym=True).n_pad == 1 << 20
+        lays = [partition.layout(1 << 20, r, P, sym=True) for r in range(P)]
+        assert all(L.n_pad == 1 << 20 for L in lays)
+        counts = [L.n_local // (8 * 2048) for L in lays]  # blocks per rank
+        assert sum(counts) == 64 and max(counts) - min(counts) <= 1
+        assert counts == sorted(counts, reverse=True)  # the first 64 mod P ranks hold one more
+        assert [L.local_begin for L in lays] == [sum(counts[:r]) * 8 * 2048 for r in range(P)]

@@ -112,6 +112,12 @@ _GRAPH_COMM_XFAIL = pytest.mark.xfail(
     (2, "ring", "sym", "fp32", 20000, OV3),
     (4, "ring", "sym", "fp32", 40000, OV3),
     (8, "ring", "sym", "fp32", 40000, OV3),
+    # P not dividing the row blocks (40,000 bodies: 8 blocks): uneven slices, the all-gather
+    # as one group of in-place broadcasts, mpi.c's remainder rule
+    (3, "allgather", "sym", "fp32", 40000, None),
+    (6, "allgather", "sym", "fp32", 40000, None),
+    (3, "ring", "sym", "fp32", 40000, None),
+    (5, "allgather", "sym-eager", "fp64", 40000, OV0),
     # the round-2 default (ungated, eager) and ungated under the segmented plan
     (4, "allgather", "sym-eager", "fp32", 40000, OV0),
     (8, "allgather", "sym", "fp32", 40000, OV0),

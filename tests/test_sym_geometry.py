@@ -12,6 +12,7 @@ import numpy as np
 import pytest
 
 from gravsim.ops import _native
+from gravsim.parallel import partition
 
 
 def _geo(n_pad):
@@ -50,13 +51,14 @@ def test_parity_balances_ranks(P):
     assert max(old) - min(old) == rows  # round 1: the first half of the ranks held long rows
 
 
-@pytest.mark.parametrize("n_pad,P", [(65536, 8), (262144, 4), (1 << 20, 8), (1 << 20, 2)])
+@pytest.mark.parametrize("n_pad,P", [(65536, 8), (262144, 4), (1 << 20, 8), (1 << 20, 2),
+                                     (1 << 20, 3), (1 << 20, 7), (262144, 6), (65536, 5)])
 @pytest.mark.parametrize("fill", [-1, 1024, 0])
 def test_unit_map_permutation_and_locality(n_pad, P, fill):
     lib, g = _geo(n_pad)
     NC, L, S, D = g["NC"], g["L"], g["S"], g["D"]
-    rows = NC // P
     for rank in (0, P - 1):
+        a0, rows = partition.sym_rank_rows(n_pad, P, rank)
         out = (ctypes.c_int32 * (rows * (S + D)))()
         n = lib.gs_sym_unit_map(n_pad, rank, P, 1, fill, out, len(out))
         assert n == rows * (S + D)
@@ -66,7 +68,6 @@ def test_unit_map_permutation_and_locality(n_pad, P, fill):
         unit = m & 0xFFFF
         key = row.astype(np.int64) * (S + D) + unit
         assert np.array_equal(np.sort(key), np.arange(rows * (S + D)))  # a permutation
-        a0 = rank * rows
         A = a0 + row.astype(np.int64)
         u = unit.astype(np.int64)
         h = np.array([lib.gs_sym_shell_len(int(x), NC, 1) for x in range(NC)])[A]
@@ -83,7 +84,7 @@ def test_unit_map_permutation_and_locality(n_pad, P, fill):
 
 
 @pytest.mark.parametrize("n_pad,P", [(65536, 8), (262144, 4), (1 << 20, 8), (1 << 20, 2),
-                                     (1 << 24, 8)])
+                                     (1 << 24, 8), (1 << 20, 3), (262144, 6), (1 << 20, 7)])
 @pytest.mark.parametrize("fill", [-1, 1024, 0])
 def test_ring_unit_map_stages(n_pad, P, fill):
     """Ring strategy of the sym schedule: the slice of rank (r - k) mod P lands at stage k.
@@ -91,8 +92,9 @@ def test_ring_unit_map_stages(n_pad, P, fill):
     permutation, the local prefix comes first and the rest is ordered by stage."""
     lib, g = _geo(n_pad)
     NC, L, S, D = g["NC"], g["L"], g["S"], g["D"]
-    rows = NC // P
+    starts = [partition.sym_rank_rows(n_pad, P, q)[0] for q in range(P)]
     for rank in (0, P - 1):
+        a0, rows = partition.sym_rank_rows(n_pad, P, rank)
         out = (ctypes.c_int32 * (rows * (S + D)))()
         n = lib.gs_sym_unit_map_ring(n_pad, rank, P, 1, fill, out, len(out))
         assert n == rows * (S + D)
@@ -104,14 +106,17 @@ def test_ring_unit_map_stages(n_pad, P, fill):
         key = row * (S + D) + unit
         assert np.array_equal(np.sort(key), np.arange(rows * (S + D)))
         assert np.array_equal(remote, stage > 0)
-        A = rank * rows + row
+        A = a0 + row
         h = np.array([lib.gs_sym_shell_len(int(x), NC, 1) for x in range(NC)])[A]
         want = np.zeros(len(m), dtype=np.int64)
-        for i in np.nonzero((unit < S) & (unit * L < 16 * h))[0]:
-            q0, q1 = unit[i] * L, (unit[i] + 1) * L - 1
-            for d in range(1 + q0 // 16, 2 + q1 // 16):
-                owner = ((A[i] + d) % NC) // rows
-                want[i] = max(want[i], (rank - owner) % P)
+        owner_of_row = np.searchsorted(starts, np.arange(NC), side="right") - 1
+        seg = np.nonzero((unit < S) & (unit * L < 16 * h))[0]
+        d_lo = 1 + unit[seg] * L // 16
+        d_hi = 1 + ((unit[seg] + 1) * L - 1) // 16
+        for k in range(int((d_hi - d_lo).max()) + 1):  # the chunks each segment touches
+            d = d_lo + k
+            st = (rank - owner_of_row[(A[seg] + d) % NC]) % P
+            want[seg] = np.where(d <= d_hi, np.maximum(want[seg], st), want[seg])
         assert np.array_equal(stage, want)
         local_prefix = int(np.argmax(stage > 0)) if (stage > 0).any() else len(stage)
         assert (np.diff(stage[local_prefix:]) >= 0).all()  # stage order after the prefix
@@ -120,3 +125,75 @@ def test_ring_unit_map_stages(n_pad, P, fill):
     # too many rows for the 12-bit row field: no gated ring map (the launch stays ungated)
     big = 1 << 25
     assert lib.gs_sym_unit_map_ring(big, 0, 1, 1, -1, None, 0) == 0
+
+
+@pytest.mark.parametrize("n_pad", [16384, 49152, 65536, 1 << 20, 1 << 24])
+@pytest.mark.parametrize("P", range(1, 9))
+def test_rank_blocks_and_nodes_match_native(n_pad, P):
+    """Rows per rank (whole row blocks, mpi.c's remainder rule) and the dyadic reduction
+    nodes each rank sends: native gs_sym_rank_rows / gs_sym_nodes equal the Python mirror;
+    the ranks tile the rows in order and the nodes tile the blocks."""
+    lib = _native.cpu_lib()
+    NC = n_pad // 2048
+    B = partition.sym_blocks(NC)
+    if P > B:
+        return
+    nodes = partition.sym_nodes(n_pad, P)
+    row = 0
+    for r in range(P):
+        a0, rows = ctypes.c_int32(), ctypes.c_int32()
+        assert lib.gs_sym_rank_rows(n_pad, P, r, ctypes.byref(a0), ctypes.byref(rows)) == 0
+        assert (a0.value, rows.value) == partition.sym_rank_rows(n_pad, P, r)
+        assert a0.value == row and rows.value % (NC // B) == 0
+        row += rows.value
+        v = [ctypes.c_int32() for _ in range(5)]
+        assert lib.gs_sym_nodes(n_pad, P, r, *[ctypes.byref(x) for x in v]) == 0
+        Bn, RB, nn, nb, NN = (x.value for x in v)
+        assert (Bn, RB) == (B, NC // B)
+        assert nn == len(nodes[r]) and nb == sum(len(x) for x in nodes[:r])
+        assert NN == sum(len(x) for x in nodes)
+    assert row == NC
+    cover = [b for rn in nodes for lo, l in rn for b in range(lo, lo + (1 << l))]
+    assert cover == list(range(B))
+    for rn in nodes:
+        for lo, l in rn:
+            assert lo % (1 << l) == 0  # aligned: a node of the canonical tree
+
+
+def _tree(leaves):
+    while len(leaves) > 1:
+        leaves = [leaves[i] + leaves[i + 1] for i in range(0, len(leaves), 2)]
+    return leaves[0]
+
+
+def _counter_merge(nodes_vals):
+    """The receiver's merge (nbody_sym.hip TreeAcc): nodes in global order, left + right."""
+    acc, occ = {}, 0
+    for level, v in nodes_vals:
+        k = level
+        while occ >> k & 1:
+            v = acc[k] + v
+            occ &= ~(1 << k)
+            k += 1
+        acc[k] = v
+        occ |= 1 << k
+    (k,) = [k for k in acc if occ >> k & 1]
+    return acc[k]
+
+
+@pytest.mark.parametrize("B", [8, 16, 32, 64])
+def test_node_merge_equals_full_tree_bitwise_for_every_P(B):
+    """fp32 leaves: every rank reduces its dyadic nodes (a sub-tree each) and the receiver
+    merges them in global order. The result is the full tree's, bit for bit, for every P:
+    the j-side sums do not depend on the rank count."""
+    rng = np.random.default_rng(B)
+    leaves = (rng.standard_normal((B, 1000)) * np.exp(rng.uniform(-20, 20, (B, 1)))).astype(
+        np.float32)
+    full = _tree(list(leaves))
+    n_pad = B * (3 if B < 64 else 1) * 2048  # NC with sym_blocks(NC) == B
+    assert partition.sym_blocks(n_pad // 2048) == B
+    for P in range(1, min(8, B) + 1):
+        vals = [(l, _tree(list(leaves[lo:lo + (1 << l)])))
+                for rn in partition.sym_nodes(n_pad, P) for lo, l in rn]
+        got = _counter_merge(vals)
+        assert np.array_equal(got.view(np.uint32), full.view(np.uint32)), P
