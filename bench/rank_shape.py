@@ -10,6 +10,9 @@ and shows how much of it the schedule hides. Predicted strong-scaling efficiency
 ms(P=1) / (P * ms(P)). Not physics: remote slices hold stale positions.
 
     python bench/rank_shape.py --n 1048576 --ranks 1,2,4,8 --comm-gbps 0,64 --overlap 0,3
+
+Since round 3 the sym schedule runs every P up to 8 (uneven row blocks for P not dividing
+the 64 blocks): --rank all measures every rank of such a run (rank 0 holds the most blocks).
 """
 from __future__ import annotations
 
@@ -27,7 +30,7 @@ def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=1 << 20)
     ap.add_argument("--ranks", default="1,2,4,8")
-    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=4)
     ap.add_argument("--dtype", default="fp32")
     ap.add_argument("--ipl", default="0", help="comma list")
     ap.add_argument("--kernel", default="auto", help="comma list")
@@ -38,8 +41,12 @@ def main() -> int:
     ap.add_argument("--comm-us", type=float, default=15.0, help="modeled latency per collective")
     ap.add_argument("--comm-wgs", type=int, default=16, help="workgroups of a modeled collective")
     ap.add_argument("--overlap", default="0", help="comma list of sym overlap modes 0..3")
-    ap.add_argument("--graph", action="store_true", help="replay multi-rank steps from a graph")
-    ap.add_argument("--rank", type=int, default=-1, help="emulated rank (default: the last)")
+    ap.add_argument("--graph", default="segmented",
+                    help="comma list of multi-rank step modes: eager | segmented (the default: "
+                         "compute segments as graphs, collectives eager between them) | full "
+                         "(collectives captured too)")
+    ap.add_argument("--rank", default="-1",
+                    help="emulated rank: an index, -1 the last, 'all' every rank")
     ap.add_argument("--repeat", type=int, default=1, help="run the whole grid this many times "
                     "(alternating configurations, for A/B on a noisy clock)")
     ap.add_argument("--lf-fill", default="",
@@ -71,8 +78,13 @@ def main() -> int:
                                   [int(x) for x in a.overlap.split(",")],
                                   [int(x) for x in a.gate_probe.split(",")],
                                   a.lf_fill.split(","), a.diag_last.split(","),
-                                  a.parity.split(",")))
-    for P, ipl, kernel, strategy, mode, gbps, ov, gp, fill, dl, par in grid * a.repeat:
+                                  a.parity.split(","), a.graph.split(",")))
+    runs = []
+    for P, *rest in grid:
+        ranks = range(P) if a.rank == "all" else \
+            [((int(a.rank) if int(a.rank) >= 0 else P - 1) if P > 1 else 0)]
+        runs += [(P, r, *rest) for r in ranks]
+    for P, r, ipl, kernel, strategy, mode, gbps, ov, gp, fill, dl, par, gmode in runs * a.repeat:
         os.environ["GRAVSIM_SYM_DIAG_LAST"] = dl
         os.environ["GRAVSIM_SYM_PARITY"] = par
         os.environ["GRAVSIM_EMU_COMM_GBPS"] = str(gbps)
@@ -82,8 +94,8 @@ def main() -> int:
         else:
             os.environ.pop("GRAVSIM_SYM_LF_FILL", None)
         cfg = SimConfig(n=a.n, dtype=a.dtype, device="gpu", ipl=ipl, kernel=kernel,
-                        strategy=strategy, mode=mode, graph_comm=a.graph)
-        r = (a.rank if a.rank >= 0 else P - 1) if P > 1 else 0
+                        strategy=strategy, mode=mode, graph=gmode != "eager",
+                        graph_comm=gmode == "full")
         e = HipEngine(cfg, r, P)
         e.set_overlap(ov)
         e.init_ics("solar+random", cfg.seed)
@@ -107,7 +119,7 @@ def main() -> int:
                               strategy=strategy, mode=e.native_layout["mode"], comm_gbps=gbps,
                               comm_us=a.comm_us, overlap=ov, gate_probe=gp, lf_fill=fill,
                               diag_last=int(dl), parity=int(par),
-                              graph=a.graph,
+                              graph=gmode, graph_info=e.graph_info(),
                               ms_per_step=ms,
                               predicted_efficiency=(b / (P * ms)) if b else None,
                               predicted_body_updates_per_s=a.n / (ms * 1e-3), phase=phase,

@@ -461,6 +461,17 @@ __device__ __forceinline__ void force_sym_entry(SymArgs a) {
       force_sym_body<T, EXACT>(a, (int)u);
       __syncthreads();  // next_s and the LDS tiles are rewritten by the next unit
     }
+    if (a.rearm_lastwg && threadIdx.x == 0) {
+      // Round 2's first re-arm (opt-in for its targeted test, docs/DESIGN.md §8): the last
+      // workgroup out (work[1] counts exits; every workgroup's fetches precede its exit add)
+      // zeroes both counters, so the next launch needs no memset.
+      const unsigned e =
+          __hip_atomic_fetch_add(a.work + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+      if (e == gridDim.x - 1) {
+        __hip_atomic_store(a.work, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(a.work + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
   } else {
     const unsigned n = a.defer[0];
     if (blockIdx.x == 0 && threadIdx.x == 0 && n > 0)

@@ -182,6 +182,7 @@ struct gs_stepper {
   // force launch starts its unit counter at k instead of 0, so units 0 .. k-1 never run,
   // exactly the failure class of a stale re-armed counter (a memset node when captured).
   unsigned fault_skip = 0;
+  bool rearm_lastwg = false;  // GRAVSIM_SYM_REARM=lastwg: round 2's in-kernel counter re-arm
   // Segmented step graph of multi-rank runs (use_graph 1): the compute stream's work between
   // two cross-stream points is captured as one graph segment; the collectives (RCCL, or the
   // emulation's modeled ones) and the event record/wait that order them against the compute
@@ -753,7 +754,8 @@ int ring_finish(gs_stepper* s, const gs::KArgs<T>& a) {
 // counter is known to be 0 (re-armed by the fused tail kernel enqueued after the previous
 // launch on this stream), then marks it dirty until the next fused tail.
 hipError_t force_sym_launch(gs_stepper* s, gs::SymArgs a, hipStream_t st) {
-  a.work_zero = s->work_zero ? 1 : 0;
+  a.work_zero = s->work_zero || s->rearm_lastwg ? 1 : 0;
+  a.rearm_lastwg = s->rearm_lastwg ? 1 : 0;
   s->work_zero = false;
   if (s->fault_skip && a.work && (a.units == 0 || a.units == 6)) {
     const hipError_t e = hipMemsetD32Async(a.work, (int)s->fault_skip, 1, st);
@@ -1261,6 +1263,7 @@ int gs_stepper_create(const gs_config* cfg, gs_stepper** out) {
   if (const char* v = getenv("GRAVSIM_SYM_FUSED_TAIL")) s->fuse_tail = atoi(v) != 0 ? 1 : 0;
   if (const char* v = getenv("GRAVSIM_SYM_PARITY")) s->parity = atoi(v) != 0 ? 1 : 0;
   if (const char* v = getenv("GRAVSIM_FAULT_SKIP_UNITS")) s->fault_skip = (unsigned)atoi(v);
+  if (const char* v = getenv("GRAVSIM_SYM_REARM")) s->rearm_lastwg = strcmp(v, "lastwg") == 0;
   const int64_t own_first = s->L.local_begin / s->L.chunk;
   const int64_t own_last = (s->L.local_begin + s->L.n_local) / s->L.chunk;
   s->own_c0 = (int)(own_first < s->L.n_chunks ? own_first : s->L.n_chunks);

@@ -112,6 +112,9 @@ struct SymArgs {
   // work[0] is already 0 on this stream (the fused tail kernel that ran after the previous
   // dynamic launch re-armed it): the launcher skips its memset.
   int32_t work_zero;
+  // GRAVSIM_SYM_REARM=lastwg (targeted test only): the last workgroup of a dynamic launch
+  // re-arms work[0] and its exit count work[1] in-kernel instead of the launcher's memset.
+  int32_t rearm_lastwg;
   // Work audit (nullptr: off): +1 per force unit that ran to completion (or was empty), so a
   // step's count must be rows x (S + D) whatever the launch split, deferral or fetch order.
   unsigned long long* audit;

@@ -137,3 +137,39 @@ def test_cutoff_paths_below_the_cutoff_pinned(hip, dtype):
     far = np.setdiff1d(np.arange(n), [100, 101])
     rel = np.abs(a_fa[far] - a_ex[far]).max() / np.abs(a_ex[far]).max()
     assert rel < (1e-5 if dtype == "fp32" else 1e-12), rel
+
+
+@pytest.mark.parametrize("n,band_mb,steps", [(65536, "1", 20), (1 << 20, "1540", 2)])
+def test_lastwg_rearm_targeted(hip, monkeypatch, n, band_mb, steps):
+    """Round 2's first re-arm of the dynamic unit counter (the last workgroup out zeroes it
+    in-kernel; opt-in GRAVSIM_SYM_REARM=lastwg), targeted at the failure it was retired for
+    (docs/DESIGN.md §8): many dynamic launches back to back on one stream, band after band
+    (65,536 bodies: one row per band, 32 launches per step, a 16-workgroup first wave so every
+    band launch fetches dynamically; 1M: the original 4-band test), replayed from a hipGraph.
+    Every unit must run exactly once per step (device count) and the bits must equal the
+    stream-ordered memset's. Run once per suite, not in a loop."""
+    from gravsim.runtime.engines import HipEngine
+
+    monkeypatch.setenv("GRAVSIM_SYM_FIRST_WAVE", "16")
+    monkeypatch.setenv("GRAVSIM_SYM_BAND_MB", band_mb)
+    out = {}
+    for rearm in ("lastwg", "memset"):
+        if rearm == "lastwg":
+            monkeypatch.setenv("GRAVSIM_SYM_REARM", "lastwg")
+        else:
+            monkeypatch.delenv("GRAVSIM_SYM_REARM", raising=False)
+        e = HipEngine(SimConfig(n=n, dtype="fp32", device="gpu", mode="sym"))
+        try:
+            e.init_ics("solar+random", 13)
+            e.audit_reset()
+            e.step(steps)
+            e.sync()
+            done, per = e.audit()
+            assert done == per * steps, (rearm, done, per)
+            assert e.graph_info()["mode"] == "graph"
+            b = e.state()
+            out[rearm] = (b.pos, b.vel)
+        finally:
+            e.close()
+    assert np.array_equal(out["lastwg"][0], out["memset"][0])
+    assert np.array_equal(out["lastwg"][1], out["memset"][1])
