@@ -1557,6 +1557,8 @@ int gs_stepper_set_cutoff_mode(gs_stepper* s, int32_t mode) {
   return 0;
 }
 
+int32_t gs_stepper_get_overlap(gs_stepper* s) { return s->sym_overlap; }
+
 int gs_stepper_graph_info(gs_stepper* s, int32_t* mode, int32_t* segments) {
   if (mode) *mode = !s->plan.empty() ? 2 : (s->graph ? 1 : 0);
   if (segments) *segments = s->plan_graphs;

@@ -158,6 +158,11 @@ class HipEngine:
         default for P > 1)."""
         _native.check(self.lib, self.lib.gs_stepper_set_overlap(self._s, int(mode)), "overlap")
 
+    @property
+    def overlap(self) -> int:
+        """The sym schedule's overlap mode in force (3 by default for P > 1)."""
+        return int(self.lib.gs_stepper_get_overlap(self._s))
+
     def set_schedule(self, graph: int, dyn_cap: int = -1) -> None:
         """graph: 0 eager, 1 single-rank hipGraph replay, 2 multi-rank capture too;
         dyn_cap: <= 1 static force units (one per workgroup), > 1 dynamic unit fetch,

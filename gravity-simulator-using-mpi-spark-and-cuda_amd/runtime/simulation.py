@@ -156,9 +156,12 @@ class Simulation:
         periods = [p for p in (cfg.progress_every if log else 0, cfg.checkpoint_every,
                                cfg.record_every, cfg.nan_check_every, cfg.dump_every)
                    if p and p > 0]
-        timing = cfg.phase_timing and isinstance(self.engine, HipEngine)
+        gpu = isinstance(self.engine, HipEngine)
+        timing = cfg.phase_timing and gpu
         if timing:
             self.engine.set_timing(True)
+        if gpu:
+            self.engine.audit_reset()
         comm.barrier(self.dist)
         t0 = time.perf_counter()
         s = 0
@@ -188,6 +191,17 @@ class Simulation:
             extra = {"phase": ph, "comm_ms": ph["comm_ms"],
                      "exposed_comm_ms": ph["exposed_comm_ms"]}
         self.check_finite()
+        if gpu:
+            # Work audit (as bench.py's): every sym force unit ran once per step on every rank.
+            done, per = self.engine.audit()
+            short = comm.allreduce_sum(self.dist, 0.0 if done == per * steps else 1.0)
+            if short:
+                raise RuntimeError(f"work audit: {int(short)} rank(s) ran the wrong number of "
+                                   f"force units (rank {self.dist.rank}: {done} of {per * steps})")
+            gi = self.engine.graph_info()
+            extra.update(work_audit="ok" if per else "n/a (one-sided schedule)",
+                         overlap=self.engine.overlap, graph=gi["mode"],
+                         graph_segments=gi["segments"] or None)
         lay = getattr(self.engine, "native_layout", {})
         from ..ops._native import KERNEL_NAMES, MODE_NAMES
 

@@ -30,13 +30,32 @@ timeout -k 10 600 python bench.py --gpus 8 --steps 2 --warmup 1 --n 1048576 > $o
   || { tail -30 $out/bench8_1m.log; exit 1; }
 grep '^{' $out/bench8_1m.log
 # CLI: 2 ranks (sym, checkpoint every 3) vs 1 rank, then a 1-rank resume of the 2-rank
-# checkpoint; the three final dumps must be identical text.
+# checkpoint, plus 3 and 8 ranks (3: uneven row blocks, 3/3/2 of 8); the final dumps must be
+# identical text, and every multi-rank run must report the gated overlap (3), the
+# segmented step graph and a clean work audit in its metrics line.
 common="--n 40000 --device gpu --mode sym --log-format none --quiet"
+rm -f $out/m*.json
 timeout -k 10 240 python -m gravsim $common --steps 6 --nproc 2 --dump $out/p2.txt \
-  --checkpoint-dir $out/ck --checkpoint-every 3 > $out/cli2.log 2>&1 || { tail -30 $out/cli2.log; exit 1; }
+  --checkpoint-dir $out/ck --checkpoint-every 3 --metrics-json $out/m2.json > $out/cli2.log 2>&1 \
+  || { tail -30 $out/cli2.log; exit 1; }
 timeout -k 10 240 python -m gravsim $common --steps 6 --dump $out/p1.txt \
   > $out/cli1.log 2>&1 || { tail -30 $out/cli1.log; exit 1; }
+timeout -k 10 240 python -m gravsim $common --steps 6 --nproc 3 --dump $out/p3.txt \
+  --metrics-json $out/m3.json > $out/cli3.log 2>&1 || { tail -30 $out/cli3.log; exit 1; }
+timeout -k 10 300 python -m gravsim $common --steps 6 --nproc 8 --dump $out/p8.txt \
+  --metrics-json $out/m8.json > $out/cli8.log 2>&1 || { tail -30 $out/cli8.log; exit 1; }
 ck3=$(ls $out/ck/*00000003* | head -1)
 timeout -k 10 240 python -m gravsim $common --steps 3 --resume "$ck3" --dump $out/pr.txt \
   > $out/clir.log 2>&1 || { tail -30 $out/clir.log; exit 1; }
-cmp $out/p1.txt $out/p2.txt && cmp $out/p1.txt $out/pr.txt && echo "CLI dumps identical (P=2, P=1, P=2 ckpt -> P=1 resume)"
+cmp $out/p1.txt $out/p2.txt && cmp $out/p1.txt $out/p3.txt && cmp $out/p1.txt $out/p8.txt \
+  && cmp $out/p1.txt $out/pr.txt \
+  && echo "CLI dumps identical (P=1, 2, 3, 8; P=2 ckpt -> P=1 resume)" || exit 1
+python - $out/m2.json $out/m3.json $out/m8.json <<'PY' || exit 1
+import json, sys
+for f in sys.argv[1:]:
+    m = json.loads(open(f).read().splitlines()[-1])
+    e = m["extra"]
+    print(f, "nranks", m["nranks"], "overlap", e["overlap"], "graph", e["graph"],
+          "segments", e["graph_segments"], "work_audit", e["work_audit"])
+    assert e["overlap"] == 3 and e["graph"] == "segmented" and e["work_audit"] == "ok", e
+PY
