@@ -42,7 +42,7 @@ for task in "$@"; do
     tests)
       if [ -n "${task#tests}" ]; then k="${task#tests:}"; else k=""; fi
       step 1500 $out/pytest_gpu${k:+_sel}.log python -u -m pytest tests -x -v -m gpu \
-        --timeout 300 --timeout-method thread ${k:+-k "$k"} ;;
+        --timeout 300 --timeout-method thread --durations=30 ${k:+-k "$k"} ;;
     smoke) step 300 $out/smoke.log python __graft_entry__.py smoke ;;
     bench) step 600 $out/bench_$(date +%s).log python bench.py $a ;;
     prof)
