@@ -318,11 +318,14 @@ size_t exchange_bytes(const gs_stepper* s) {
 }
 
 // Emulated collective on s_comm (GRAVSIM_EMU_COMM_GBPS > 0): the byte count moved through HBM
-// by emu_wgs workgroups that stay resident for latency + bytes / rate (comm_model.hip).
-int comm_model(gs_stepper* s, const void* src, size_t bytes) {
+// by emu_wgs workgroups that stay resident for latency + bytes / rate (comm_model.hip). The
+// kernel copies min(bytes, src_cap, emu_cap) bytes (src_cap: what the source buffer holds);
+// the modeled time always uses the full byte count.
+int comm_model(gs_stepper* s, const void* src, size_t bytes, size_t src_cap) {
   if (s->emu_gbps <= 0.0 || bytes == 0) return 0;
-  if (bytes > s->emu_cap) bytes = s->emu_cap;  // (sized at create for the larger collective)
   const double us = s->emu_lat_us + (double)bytes / (s->emu_gbps * 1e3);
+  if (bytes > s->emu_cap) bytes = s->emu_cap;  // (sized at create for the larger collective)
+  if (bytes > src_cap) bytes = src_cap;
   const uint64_t ticks = (uint64_t)(us * s->clk_khz / 1e3);
   GS_HIP(gs::launch_comm_model(src, s->emu_buf, bytes, ticks, s->emu_wgs, s->s_comm));
   return 0;
@@ -451,7 +454,10 @@ int sym_exchange_rccl(gs_stepper* s, bool join = true) {
                               s->sym_S + my * 3 * (size_t)s->rbeg[r] * e, my * 3 * nl * e,
                               hipMemcpyDeviceToDevice, s->s_comm));
         if (s->emulate) {
-          if (comm_model(s, s->sym_S, exchange_bytes(s))) return -1;
+          // (the bytes this rank receives, read from its receive buffer: NN x 3 per own body)
+          if (comm_model(s, s->sym_R, exchange_bytes(s),
+                         (size_t)s->sym_NN * 3 * (size_t)s->L.n_local * s->esz))
+            return -1;
         } else if (P > 1) {
           GS_NCCL(ncclGroupStart());
           for (int q = 0; q < P; ++q) {
@@ -629,14 +635,15 @@ int gather(gs_stepper* s, int cur, bool gate = false) {
     if (s->sym_ring && use_sym(s)) {
       for (int k = 1; k < s->cfg.nranks; ++k) {
         if (s->emulate) {
-          if (comm_model(s, buf, (size_t)s->rcnt[ring_src(s, k)] * row_bytes(s))) return -1;
+          const size_t sl = (size_t)s->rcnt[ring_src(s, k)] * row_bytes(s);
+          if (comm_model(s, buf, sl, (size_t)s->L.n_pad * row_bytes(s))) return -1;
         } else if (ring_xfer_rccl(s, cur, k)) {
           return -1;
         }
         if (gate) GS_HIP(gs::launch_gate_set(s->ring_gate + 8 * cur + k, s->s_comm));
       }
     } else if (s->emulate) {
-      if (comm_model(s, buf, gather_bytes(s))) return -1;
+      if (comm_model(s, buf, gather_bytes(s), (size_t)s->L.n_pad * row_bytes(s))) return -1;
     } else if (!use_sym(s) || s->uniform) {
       GS_NCCL(ncclAllGather(buf + (size_t)s->L.local_begin * row_bytes(s), buf, count, dt,
                             s->comm, s->s_comm));

@@ -56,6 +56,24 @@ def test_segmented_plan_matches_eager(hip, monkeypatch, strategy, overlap):
     assert np.array_equal(res[True][1], res[False][1])
 
 
+@pytest.mark.parametrize("P,rank", [(3, 0), (3, 2), (5, 4), (6, 5), (7, 0), (7, 6)])
+def test_uneven_rank_emulation_runs(hip, monkeypatch, P, rank):
+    """Per-rank emulation of P not dividing the 64 row blocks (1M bodies): rank 0 holds the
+    most blocks, the last ranks the fewest and receive the most tree nodes; the modeled
+    collectives (gather, node exchange) stay inside their buffers and every unit runs."""
+    e = _emu(monkeypatch, 1 << 20, P, rank, 64, 3)
+    try:
+        e.init_ics("solar+random", 2)
+        e.audit_reset()
+        e.step(2)
+        e.sync()
+        done, per = e.audit()
+        assert done == 2 * per and per > 0
+        assert e.nonfinite() == 0
+    finally:
+        e.close()
+
+
 def test_overlap_modes_same_bits(hip, monkeypatch):
     """Every overlap mode computes every unit exactly once into the same slots: the emulated
     rank's state after 4 steps is bitwise identical for modes 0..3 (a unit missed by the
