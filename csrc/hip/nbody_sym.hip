@@ -534,14 +534,13 @@ struct TreeAcc {
   }
 };
 
-// Row-ascending sum of Pj over rows [A_lo, A_hi) for body (X, c), one component per C:
-// the loads of U rows are issued ahead of their ordered adds; rows outside X's shell add 0.
+// Adds, in ascending row order, Pj of the rows in [A_lo, A_hi) whose shell holds chunk X
+// (body (X, c), one component per C); the loads of U rows are issued ahead of their ordered
+// adds.
 template <typename T, int C>
-__device__ __forceinline__ void pj_row_sum(const SymArgs& a, int A_lo, int A_hi, int X,
-                                           const T* pjc, int64_t comp_stride, T* out) {
-#pragma unroll
-  for (int k = 0; k < C; ++k) out[k] = T(0);
-  constexpr int U = 4;
+__device__ __forceinline__ void pj_range_add(const SymArgs& a, int A_lo, int A_hi, int X,
+                                             const T* pjc, int64_t comp_stride, T* out) {
+  constexpr int U = 8;
   for (int A0 = A_lo; A0 < A_hi; A0 += U) {
     T v[U][C];
 #pragma unroll
@@ -557,6 +556,25 @@ __device__ __forceinline__ void pj_row_sum(const SymArgs& a, int A_lo, int A_hi,
     for (int u = 0; u < U; ++u)
 #pragma unroll
       for (int k = 0; k < C; ++k) out[k] += v[u][k];
+  }
+}
+
+// Row-ascending sum of Pj over the rows [A_lo, A_hi) of one block for body (X, c), from +0.0.
+// Only rows A with X - A in [1, NC/2] (mod NC) can hold X in their shell: a cyclic range of
+// NC/2 rows, at most two linear pieces, visited in ascending order. Skipping the other rows
+// keeps the bits of adding +0.0 for them (a sum started at +0.0 never becomes -0.0) and
+// halves the loop.
+template <typename T, int C>
+__device__ __forceinline__ void pj_row_sum(const SymArgs& a, int A_lo, int A_hi, int X,
+                                           const T* pjc, int64_t comp_stride, T* out) {
+#pragma unroll
+  for (int k = 0; k < C; ++k) out[k] = T(0);
+  const int s0 = X - a.NC / 2;  // the shell rows of X: [s0, X - 1] cyclically
+  if (s0 >= 0) {
+    pj_range_add<T, C>(a, max(A_lo, s0), min(A_hi, X), X, pjc, comp_stride, out);
+  } else {
+    pj_range_add<T, C>(a, A_lo, min(A_hi, X), X, pjc, comp_stride, out);
+    pj_range_add<T, C>(a, max(A_lo, s0 + a.NC), A_hi, X, pjc, comp_stride, out);
   }
 }
 
@@ -586,47 +604,45 @@ __global__ __launch_bounds__(256) void sym_block_reduce_kernel(SymArgs a) {
   o[2 * nb] = v[2];
 }
 
-// Node k (blockIdx.y) of this rank's dyadic decomposition, for every body x of a real chunk:
-// the tree over the node's blocks, leaves from Pj directly (one band holds all the rank's
-// rows) or from Bbuf (multi-band runs). Output Sbuf[dest rank q][node k][3][n_local(q)].
+// Node k of this rank's dyadic decomposition, component comp (blockIdx.y = 3 k + comp), for
+// every body x of a real chunk: the tree over the node's blocks, leaves from Pj directly (one
+// band holds all the rank's rows) or from Bbuf (multi-band runs). One component per thread
+// triples the loads in flight (the kernel is latency-bound: 0.81 ms at 1M with 3 per thread).
+// Output Sbuf[dest rank q][node k][3][n_local(q)].
 template <typename T>
 __global__ __launch_bounds__(256) void sym_node_reduce_kernel(SymArgs a) {
   const int64_t nb = (int64_t)a.real_chunks * kSymC;
   const int64_t x = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (x >= nb) return;
   const int X = (int)(x / kSymC), c = (int)(x % kSymC);
+  const int node = (int)blockIdx.y / 3, comp = (int)blockIdx.y % 3;
   const int own_lo = a.blk_lo[a.rank], own_hi = a.blk_lo[a.rank + 1];
   int lo = own_lo, l = sym_dyadic_level(lo, own_hi);
-  for (int k = 0; k < (int)blockIdx.y; ++k) {
+  for (int k = 0; k < node; ++k) {
     lo += 1 << l;
     l = sym_dyadic_level(lo, own_hi);
   }
-  TreeAcc<T, 3> t;
+  TreeAcc<T, 1> t;
   t.occ = 0;
   const T* Bb = static_cast<const T*>(a.Bbuf);
+  const T* pjc = static_cast<const T*>(a.Pj) + (int64_t)comp * kSymC + c;
   for (int b = lo; b < lo + (1 << l); ++b) {
-    T v[3];
+    T v[1];
     if (Bb) {
-      const T* p = Bb + (int64_t)(b - own_lo) * 3 * nb + x;
-      v[0] = p[0];
-      v[1] = p[nb];
-      v[2] = p[2 * nb];
+      v[0] = Bb[((int64_t)(b - own_lo) * 3 + comp) * nb + x];
     } else {
       const int A_lo = b * a.RB, A_hi = min((b + 1) * a.RB, a.real_chunks);
-      pj_row_sum<T, 3>(a, A_lo, max(A_lo, A_hi), X, static_cast<const T*>(a.Pj) + c, kSymC, v);
+      pj_row_sum<T, 1>(a, A_lo, max(A_lo, A_hi), X, pjc, kSymC, v);
     }
     t.push(0, v);
   }
-  T r[3];
+  T r[1];
   t.result(r);
   const int q = sym_row_owner(a, X);
   const int64_t bq = (int64_t)a.blk_lo[q] * a.RB * kSymC;
   const int64_t nlq = (int64_t)(a.blk_lo[q + 1] - a.blk_lo[q]) * a.RB * kSymC;
-  T* o = static_cast<T*>(a.Sbuf) + (int64_t)a.nn * 3 * bq + (int64_t)blockIdx.y * 3 * nlq +
-         (x - bq);
-  o[0] = r[0];
-  o[nlq] = r[1];
-  o[2 * nlq] = r[2];
+  static_cast<T*>(a.Sbuf)[(int64_t)a.nn * 3 * bq + ((int64_t)node * 3 + comp) * nlq + (x - bq)] =
+      r[0];
 }
 
 // S(x) for an own body: every rank's nodes in global order from Rbuf[node][3][n_local],
@@ -891,7 +907,7 @@ hipError_t launch_sym_node_reduce(const SymArgs& a, hipStream_t s) {
   // leaves from Pj need every own row in the slots (one band), else from Bbuf
   if (!a.Bbuf && (a.band0 != 0 || a.band_rows != a.rows)) return hipErrorInvalidValue;
   const int64_t bodies = (int64_t)a.real_chunks * kSymC;
-  const dim3 grid((unsigned)((bodies + 255) / 256), (unsigned)a.nn);
+  const dim3 grid((unsigned)((bodies + 255) / 256), (unsigned)(3 * a.nn));
   if (a.fp64) hipLaunchKernelGGL(sym_node_reduce_kernel<double>, grid, dim3(256), 0, s, a);
   else hipLaunchKernelGGL(sym_node_reduce_kernel<float>, grid, dim3(256), 0, s, a);
   return hipGetLastError();
