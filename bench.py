@@ -428,8 +428,10 @@ def main(argv=None) -> int:
                 "mode": mode,
                 **kernel_info,
                 "cutoff_path": "exact-select" if fmode["exact"] else
-                f"fast (core^2={fmode['eps2']:.3g} m^2; bit-identical to the 1e-10 m hard cutoff "
-                "for separations above ~1 cm)",
+                f"fast (r^2 + c^2 with c^2={fmode['eps2']:.3g} m^2 instead of the hard-cutoff "
+                "select: bit-identical to the 1e-10 m select for separations above ~1 cm; a "
+                "pair closer than the cutoff gets a finite softened force mu r / (r^2 + c^2)^1.5 "
+                "instead of 0; exact_cutoff_ms_per_step times the select)",
                 # eager | graph (one hipGraph per two steps) | segmented (multi-rank: compute
                 # segments as graphs, RCCL collectives eager between them)
                 "graph": ginfo["mode"],

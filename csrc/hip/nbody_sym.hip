@@ -535,20 +535,25 @@ struct TreeAcc {
 };
 
 // Adds, in ascending row order, Pj of the rows in [A_lo, A_hi) whose shell holds chunk X
-// (body (X, c), one component per C); the loads of U rows are issued ahead of their ordered
-// adds.
+// (body (X, c), one component per C). The caller passes a range where the distance
+// d = X - A + wrap lies in [1, NC/2], so only the antipodal row (d = NC/2) needs the shell
+// test; row A's partial sits (H - 1) x 3 x kSymC elements after row A - 1's. The loads of U
+// rows are issued ahead of their ordered adds.
 template <typename T, int C>
 __device__ __forceinline__ void pj_range_add(const SymArgs& a, int A_lo, int A_hi, int X,
-                                             const T* pjc, int64_t comp_stride, T* out) {
+                                             int wrap, const T* pjc, int64_t comp_stride,
+                                             T* out) {
   constexpr int U = 8;
-  for (int A0 = A_lo; A0 < A_hi; A0 += U) {
+  const int64_t step = (int64_t)(a.H - 1) * 3 * kSymC;
+  const T* p0 = pjc + ((int64_t)(A_lo - a.a0 - a.band0) * a.H + (X - A_lo + wrap - 1)) * 3 * kSymC;
+  for (int A0 = A_lo; A0 < A_hi; A0 += U, p0 += U * step) {
     T v[U][C];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int A = A0 + u;
-      const int d = (X - A + a.NC) % a.NC;
-      const bool ok = A < A_hi && d != 0 && d <= shell_len(A, a.NC, a.parity);
-      const T* p = pjc + ((int64_t)(A - a.a0 - a.band0) * a.H + (d - 1)) * 3 * kSymC;
+      const int d = X - A + wrap;
+      const bool ok = A < A_hi && (d != a.NC / 2 || shell_len(A, a.NC, a.parity) == a.NC / 2);
+      const T* p = p0 + u * step;
 #pragma unroll
       for (int k = 0; k < C; ++k) v[u][k] = ok ? p[k * comp_stride] : T(0);
     }
@@ -571,10 +576,10 @@ __device__ __forceinline__ void pj_row_sum(const SymArgs& a, int A_lo, int A_hi,
   for (int k = 0; k < C; ++k) out[k] = T(0);
   const int s0 = X - a.NC / 2;  // the shell rows of X: [s0, X - 1] cyclically
   if (s0 >= 0) {
-    pj_range_add<T, C>(a, max(A_lo, s0), min(A_hi, X), X, pjc, comp_stride, out);
+    pj_range_add<T, C>(a, max(A_lo, s0), min(A_hi, X), X, 0, pjc, comp_stride, out);
   } else {
-    pj_range_add<T, C>(a, A_lo, min(A_hi, X), X, pjc, comp_stride, out);
-    pj_range_add<T, C>(a, max(A_lo, s0 + a.NC), A_hi, X, pjc, comp_stride, out);
+    pj_range_add<T, C>(a, A_lo, min(A_hi, X), X, 0, pjc, comp_stride, out);
+    pj_range_add<T, C>(a, max(A_lo, s0 + a.NC), A_hi, X, a.NC, pjc, comp_stride, out);
   }
 }
 
@@ -604,45 +609,50 @@ __global__ __launch_bounds__(256) void sym_block_reduce_kernel(SymArgs a) {
   o[2 * nb] = v[2];
 }
 
-// Node k of this rank's dyadic decomposition, component comp (blockIdx.y = 3 k + comp), for
-// every body x of a real chunk: the tree over the node's blocks, leaves from Pj directly (one
-// band holds all the rank's rows) or from Bbuf (multi-band runs). One component per thread
-// triples the loads in flight (the kernel is latency-bound: 0.81 ms at 1M with 3 per thread).
-// Output Sbuf[dest rank q][node k][3][n_local(q)].
+// Node k (blockIdx.y) of this rank's dyadic decomposition, for every body x of a real chunk:
+// the tree over the node's blocks, leaves from Pj directly (one band holds all the rank's
+// rows) or from Bbuf (multi-band runs). Output Sbuf[dest rank q][node k][3][n_local(q)].
+// Latency-bound (a chain of row loads per body): 3 components per thread amortise the row
+// bookkeeping, U = 8 rows of loads are in flight, and only the NC/2 rows that can hold the
+// body in their shell are visited (pj_row_sum).
 template <typename T>
 __global__ __launch_bounds__(256) void sym_node_reduce_kernel(SymArgs a) {
   const int64_t nb = (int64_t)a.real_chunks * kSymC;
   const int64_t x = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (x >= nb) return;
   const int X = (int)(x / kSymC), c = (int)(x % kSymC);
-  const int node = (int)blockIdx.y / 3, comp = (int)blockIdx.y % 3;
   const int own_lo = a.blk_lo[a.rank], own_hi = a.blk_lo[a.rank + 1];
   int lo = own_lo, l = sym_dyadic_level(lo, own_hi);
-  for (int k = 0; k < node; ++k) {
+  for (int k = 0; k < (int)blockIdx.y; ++k) {
     lo += 1 << l;
     l = sym_dyadic_level(lo, own_hi);
   }
-  TreeAcc<T, 1> t;
+  TreeAcc<T, 3> t;
   t.occ = 0;
   const T* Bb = static_cast<const T*>(a.Bbuf);
-  const T* pjc = static_cast<const T*>(a.Pj) + (int64_t)comp * kSymC + c;
   for (int b = lo; b < lo + (1 << l); ++b) {
-    T v[1];
+    T v[3];
     if (Bb) {
-      v[0] = Bb[((int64_t)(b - own_lo) * 3 + comp) * nb + x];
+      const T* p = Bb + (int64_t)(b - own_lo) * 3 * nb + x;
+      v[0] = p[0];
+      v[1] = p[nb];
+      v[2] = p[2 * nb];
     } else {
       const int A_lo = b * a.RB, A_hi = min((b + 1) * a.RB, a.real_chunks);
-      pj_row_sum<T, 1>(a, A_lo, max(A_lo, A_hi), X, pjc, kSymC, v);
+      pj_row_sum<T, 3>(a, A_lo, max(A_lo, A_hi), X, static_cast<const T*>(a.Pj) + c, kSymC, v);
     }
     t.push(0, v);
   }
-  T r[1];
+  T r[3];
   t.result(r);
   const int q = sym_row_owner(a, X);
   const int64_t bq = (int64_t)a.blk_lo[q] * a.RB * kSymC;
   const int64_t nlq = (int64_t)(a.blk_lo[q + 1] - a.blk_lo[q]) * a.RB * kSymC;
-  static_cast<T*>(a.Sbuf)[(int64_t)a.nn * 3 * bq + ((int64_t)node * 3 + comp) * nlq + (x - bq)] =
-      r[0];
+  T* o = static_cast<T*>(a.Sbuf) + (int64_t)a.nn * 3 * bq + (int64_t)blockIdx.y * 3 * nlq +
+         (x - bq);
+  o[0] = r[0];
+  o[nlq] = r[1];
+  o[2 * nlq] = r[2];
 }
 
 // S(x) for an own body: every rank's nodes in global order from Rbuf[node][3][n_local],
@@ -907,7 +917,7 @@ hipError_t launch_sym_node_reduce(const SymArgs& a, hipStream_t s) {
   // leaves from Pj need every own row in the slots (one band), else from Bbuf
   if (!a.Bbuf && (a.band0 != 0 || a.band_rows != a.rows)) return hipErrorInvalidValue;
   const int64_t bodies = (int64_t)a.real_chunks * kSymC;
-  const dim3 grid((unsigned)((bodies + 255) / 256), (unsigned)(3 * a.nn));
+  const dim3 grid((unsigned)((bodies + 255) / 256), (unsigned)a.nn);
   if (a.fp64) hipLaunchKernelGGL(sym_node_reduce_kernel<double>, grid, dim3(256), 0, s, a);
   else hipLaunchKernelGGL(sym_node_reduce_kernel<float>, grid, dim3(256), 0, s, a);
   return hipGetLastError();

@@ -104,14 +104,11 @@ _GRAPH_COMM_XFAIL = pytest.mark.xfail(
     (8, "allgather", "sym", "fp32", 20000, None),  # the 8-GPU shape: one group per destination
     (2, "allgather", "sym", "fp64", 20000, None),
     (4, "ring", "split", "fp32", 9000, None),
-    (4, "allgather", "sym", "fp32", 40000, OV3),
     (8, "allgather", "sym", "fp32", 40000, OV3),
-    (2, "allgather", "sym", "fp64", 20000, OV3),
-    # ring strategy of the sym schedule: P-1 neighbour stages, ungated and gated per stage
-    (4, "ring", "sym", "fp32", 20000, None),
-    (2, "ring", "sym", "fp32", 20000, OV3),
-    (4, "ring", "sym", "fp32", 40000, OV3),
-    (8, "ring", "sym", "fp32", 40000, OV3),
+    # ring strategy of the sym schedule: P-1 neighbour stages, each gating its own units
+    (2, "ring", "sym", "fp32", 20000, None),
+    (4, "ring", "sym", "fp32", 40000, None),
+    (8, "ring", "sym", "fp32", 40000, None),
     # P not dividing the row blocks (40,000 bodies: 8 blocks): uneven slices, the all-gather
     # as one group of in-place broadcasts, mpi.c's remainder rule
     (3, "allgather", "sym", "fp32", 40000, None),
@@ -119,7 +116,7 @@ _GRAPH_COMM_XFAIL = pytest.mark.xfail(
     (3, "ring", "sym", "fp32", 40000, None),
     (5, "allgather", "sym-eager", "fp64", 40000, OV0),
     # the round-2 default (ungated, eager) and ungated under the segmented plan
-    (4, "allgather", "sym-eager", "fp32", 40000, OV0),
+    (2, "allgather", "sym-eager", "fp32", 40000, OV0),
     (8, "allgather", "sym", "fp32", 40000, OV0),
     (2, "allgather", "sym-eager", "fp64", 20000, None),
     # "sym-graph": capturing the multi-rank step, collectives included, over RCCL's socket
