@@ -181,7 +181,9 @@ extern "C" int gs_sym_nodes(int64_t n_pad, int32_t nranks, int32_t rank, int32_t
   const int32_t NC = (int32_t)(n_pad / 2048), b = gs::sym_blocks(NC);
   int32_t before = 0, total = 0, mine = 0;
   for (int32_t q = 0; q < nranks; ++q) {
-    const int32_t k = gs::sym_node_count(gs::sym_blk_lo(b, nranks, q), gs::sym_blk_lo(b, nranks, q + 1));
+    const int32_t k = gs::sym_node_count(gs::sym_blk_lo(b, nranks, q),
+                                         gs::sym_blk_lo(b, nranks, q + 1),
+                                         gs::sym_node_maxl(b, nranks));
     if (q < rank) before += k;
     if (q == rank) mine = k;
     total += k;

@@ -824,10 +824,24 @@ int sym_force(gs_stepper* s, gs::SymArgs a, bool overlap_gather, bool exchange =
     }
     if (fused_tail(s)) continue;  // reductions + integrate in sym_tail_kernel (one band)
     const bool last = b0 + a.band_rows >= a.rows;
+    // Without an exchange the row reduce (Pi, Pd -> Ti) and the block / node reduce (Pj) are
+    // independent streaming sums: fork the row reduce onto s_rem so both share the GPU (a
+    // fork / join inside a captured step graph).
+    const bool fork = !xcomm(s);
+    if (fork) {
+      GS_HIP(hipEventRecord(s->ev_fork, s->s_comp));
+      GS_HIP(hipStreamWaitEvent(s->s_rem, s->ev_fork, 0));
+      GS_HIP(gs::launch_sym_row_reduce(a, s->s_rem));
+    }
     if (a.Bbuf) GS_HIP(gs::launch_sym_block_reduce(a, s->s_comp));  // the band's leaves
     if (last) GS_HIP(gs::launch_sym_node_reduce(a, s->s_comp));
     if (exchange && last && sym_exchange_rccl(s, false)) return -1;
-    GS_HIP(gs::launch_sym_row_reduce(a, s->s_comp));
+    if (fork) {
+      GS_HIP(hipEventRecord(s->ev_remote, s->s_rem));
+      GS_HIP(hipStreamWaitEvent(s->s_comp, s->ev_remote, 0));
+    } else {
+      GS_HIP(gs::launch_sym_row_reduce(a, s->s_comp));
+    }
     if (exchange && last) {
       GS_MARK(j0, j, s->s_comp);
       if (comp_wait(s, s->ev_sym)) return -1;

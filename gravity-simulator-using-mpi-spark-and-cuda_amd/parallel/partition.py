@@ -105,16 +105,26 @@ def sym_blk_lo(B: int, P: int, r: int) -> int:
     return r * base + min(r, rem)
 
 
-def dyadic_nodes(lo: int, hi: int) -> list[tuple[int, int]]:
-    """(first block, level) of the aligned power-of-two pieces covering [lo, hi)."""
+def dyadic_nodes(lo: int, hi: int, maxl: int = 30) -> list[tuple[int, int]]:
+    """(first block, level) of the aligned power-of-two pieces covering [lo, hi), none above
+    level maxl."""
     out = []
     while lo < hi:
         l = 0
-        while (lo >> l) & 1 == 0 and lo + (2 << l) <= hi:
+        while l < maxl and (lo >> l) & 1 == 0 and lo + (2 << l) <= hi:
             l += 1
         out.append((lo, l))
         lo += 1 << l
     return out
+
+
+def sym_node_maxl(B: int, P: int) -> int:
+    """One rank splits its range into 8 nodes (more threads in the node reduce, same bits);
+    with several ranks every node is sent to every other rank, so nodes stay maximal."""
+    if P > 1:
+        return 30
+    lb = B.bit_length() - 1
+    return lb - 3 if lb > 3 else 0
 
 
 def sym_rank_rows(n_pad: int, nranks: int, rank: int) -> tuple[int, int]:
@@ -131,7 +141,8 @@ def sym_rank_rows(n_pad: int, nranks: int, rank: int) -> tuple[int, int]:
 def sym_nodes(n_pad: int, nranks: int) -> list[list[tuple[int, int]]]:
     """Per rank, the reduction-tree nodes it sends (layout.cpp gs_sym_nodes)."""
     B = sym_blocks(n_pad // SYM_CHUNK)
-    return [dyadic_nodes(sym_blk_lo(B, nranks, q), sym_blk_lo(B, nranks, q + 1))
+    return [dyadic_nodes(sym_blk_lo(B, nranks, q), sym_blk_lo(B, nranks, q + 1),
+                         sym_node_maxl(B, nranks))
             for q in range(nranks)]
 
 
