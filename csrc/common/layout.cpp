@@ -172,6 +172,14 @@ extern "C" int gs_sym_rank_rows(int64_t n_pad, int32_t nranks, int32_t rank, int
   return 0;
 }
 
+// Largest reduction-tree node level in use (gs_common.h sym_node_maxl; the A/B knob
+// GRAVSIM_SYM_NODE_SPLIT=0 keeps one rank's range as a single node).
+extern "C" int32_t gs_sym_node_maxl(int32_t B, int32_t nranks) {
+  const char* v = getenv("GRAVSIM_SYM_NODE_SPLIT");
+  if (v && atoi(v) == 0) return 30;
+  return gs::sym_node_maxl(B, nranks);
+}
+
 // Row blocks and reduction-tree nodes: B blocks of RB rows; rank `rank` sends nn dyadic
 // nodes (sub-trees of its block range); nodes of lower ranks come first (nb of them); NN
 // nodes in all.
@@ -183,7 +191,7 @@ extern "C" int gs_sym_nodes(int64_t n_pad, int32_t nranks, int32_t rank, int32_t
   for (int32_t q = 0; q < nranks; ++q) {
     const int32_t k = gs::sym_node_count(gs::sym_blk_lo(b, nranks, q),
                                          gs::sym_blk_lo(b, nranks, q + 1),
-                                         gs::sym_node_maxl(b, nranks));
+                                         gs_sym_node_maxl(b, nranks));
     if (q < rank) before += k;
     if (q == rank) mine = k;
     total += k;

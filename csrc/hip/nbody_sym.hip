@@ -622,7 +622,7 @@ __global__ __launch_bounds__(256) void sym_node_reduce_kernel(SymArgs a) {
   if (x >= nb) return;
   const int X = (int)(x / kSymC), c = (int)(x % kSymC);
   const int own_lo = a.blk_lo[a.rank], own_hi = a.blk_lo[a.rank + 1];
-  const int maxl = sym_node_maxl(a.B, a.P);
+  const int maxl = a.node_maxl;
   int lo = own_lo, l = sym_dyadic_level(lo, own_hi, maxl);
   for (int k = 0; k < (int)blockIdx.y; ++k) {
     lo += 1 << l;
@@ -663,7 +663,7 @@ __device__ __forceinline__ void sym_tree_all(const SymArgs& a, int64_t li, T* S)
   TreeAcc<T, 3> t;
   t.occ = 0;
   const T* R = static_cast<const T*>(a.Rbuf) + li;
-  const int maxl = sym_node_maxl(a.B, a.P);
+  const int maxl = a.node_maxl;
   int j = 0;
   for (int q = 0; q < a.P; ++q) {
     const int hi = a.blk_lo[q + 1];

@@ -183,6 +183,7 @@ struct gs_stepper {
   // exactly the failure class of a stale re-armed counter (a memset node when captured).
   unsigned fault_skip = 0;
   bool rearm_lastwg = false;  // GRAVSIM_SYM_REARM=lastwg: round 2's in-kernel counter re-arm
+  bool fork_row = true;       // GRAVSIM_SYM_FORK_ROW=0: row reduce after the node reduce (A/B)
   // Segmented step graph of multi-rank runs (use_graph 1): the compute stream's work between
   // two cross-stream points is captured as one graph segment; the collectives (RCCL, or the
   // emulation's modeled ones) and the event record/wait that order them against the compute
@@ -403,6 +404,7 @@ gs::SymArgs sym_args(gs_stepper* s, int cur) {
   a.RB = s->sym_RB;
   a.rank = s->cfg.rank;
   a.nn = s->nn[s->cfg.rank];
+  a.node_maxl = gs_sym_node_maxl(s->sym_B, s->cfg.nranks);
   for (int q = 0; q <= s->cfg.nranks && q < 9; ++q) a.blk_lo[q] = s->blk_lo[q];
   a.Bbuf = s->sym_Bb;
   a.S = s->sym_S_n;
@@ -827,7 +829,7 @@ int sym_force(gs_stepper* s, gs::SymArgs a, bool overlap_gather, bool exchange =
     // Without an exchange the row reduce (Pi, Pd -> Ti) and the block / node reduce (Pj) are
     // independent streaming sums: fork the row reduce onto s_rem so both share the GPU (a
     // fork / join inside a captured step graph).
-    const bool fork = !xcomm(s);
+    const bool fork = !xcomm(s) && s->fork_row;
     if (fork) {
       GS_HIP(hipEventRecord(s->ev_fork, s->s_comp));
       GS_HIP(hipStreamWaitEvent(s->s_rem, s->ev_fork, 0));
@@ -1285,6 +1287,7 @@ int gs_stepper_create(const gs_config* cfg, gs_stepper** out) {
   if (const char* v = getenv("GRAVSIM_SYM_PARITY")) s->parity = atoi(v) != 0 ? 1 : 0;
   if (const char* v = getenv("GRAVSIM_FAULT_SKIP_UNITS")) s->fault_skip = (unsigned)atoi(v);
   if (const char* v = getenv("GRAVSIM_SYM_REARM")) s->rearm_lastwg = strcmp(v, "lastwg") == 0;
+  if (const char* v = getenv("GRAVSIM_SYM_FORK_ROW")) s->fork_row = atoi(v) != 0;
   const int64_t own_first = s->L.local_begin / s->L.chunk;
   const int64_t own_last = (s->L.local_begin + s->L.n_local) / s->L.chunk;
   s->own_c0 = (int)(own_first < s->L.n_chunks ? own_first : s->L.n_chunks);

@@ -99,6 +99,7 @@ int64_t gs_sym_bytes(int64_t n_pad, int32_t nranks, int32_t esz);
 int gs_sym_rank_rows(int64_t n_pad, int32_t nranks, int32_t rank, int32_t* a0, int32_t* rows);
 int gs_sym_nodes(int64_t n_pad, int32_t nranks, int32_t rank, int32_t* B, int32_t* RB,
                  int32_t* nn, int32_t* nb, int32_t* NN);
+int32_t gs_sym_node_maxl(int32_t B, int32_t nranks);
 // Shell length of chunk row A (antipodal pairs split by parity; parity 0: rows A < NC/2).
 int32_t gs_sym_shell_len(int32_t A, int32_t NC, int32_t parity);
 // Unit order of the gated sym launch for one rank (see layout.cpp); returns the entry count.

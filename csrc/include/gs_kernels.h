@@ -72,6 +72,7 @@ struct SymArgs {
   int32_t D;           // parts of the diagonal chunk (L < 16 quanta: 16 / L)
   int32_t B, RB;       // row blocks and rows per block
   int32_t rank, nn;    // this rank and the dyadic nodes it reduces and sends
+  int32_t node_maxl;   // largest node level (gs_sym_node_maxl)
   int32_t blk_lo[9];   // rank q owns blocks [blk_lo[q], blk_lo[q + 1]), q < P
   int32_t band0, band_rows;  // rows [band0, band0 + band_rows) of this rank (rank-relative)
                              // are in the Pi/Pj/Pd buffers (row index - band0)

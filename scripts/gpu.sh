@@ -17,6 +17,7 @@
 #   counters                  rocprofv3 -L (the PMC counters this box offers)
 #   ipc                       two-process HIP IPC with / without HSA_ENABLE_IPC_MODE_LEGACY=0
 #   abaudit[:<bench args>]    interleaved bench.py A/B of the work-audit counter (GRAVSIM_AUDIT)
+#   abfork[:<bench args>]     reduce-phase span per step: row reduce forked / node split A/B
 # Outputs land in gpurun_out/<task>*.log.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
@@ -77,6 +78,19 @@ for task in "$@"; do
         --output-format csv -- python bench/rank_shape.py $a
       head -8 $out/rankprof/rp_kernel_stats.csv ;;
     counters) step 120 $out/counters.txt rocprofv3 -L ;;
+    abfork)
+      # reduce-phase span per step with the row reduce forked beside the node reduce (1) or
+      # after it (0), from kernel traces of the 1M bench (scripts/reduce_span.py)
+      # arms: fork,split (GRAVSIM_SYM_FORK_ROW, GRAVSIM_SYM_NODE_SPLIT)
+      for arm in 1,1 0,1 0,0 1,0 1,1 0,1 0,0 1,0; do
+        f=${arm%,*}; sp=${arm#*,}; d=$out/abfork_${f}_${sp}
+        rm -rf $d
+        step 600 $d.log env GRAVSIM_SYM_FORK_ROW=$f GRAVSIM_SYM_NODE_SPLIT=$sp rocprofv3 \
+          --kernel-trace -d $d -o tr --output-format csv -- python bench.py --steps 6 \
+          --warmup 2 --exact-steps 0 --phase-steps 0 --check-samples 0 --no-replay-audit $a
+        t=$(find $d -name "*kernel_trace.csv" | head -1)
+        echo "fork=$f split=$sp $(python scripts/reduce_span.py $t)" | tee -a $out/abfork.txt
+      done ;;
     ipc)
       # two-process HIP IPC (memory + event) with the launcher's dmabuf setting and without it
       step 300 $out/ipc_dmabuf.log env HSA_ENABLE_IPC_MODE_LEGACY=0 python tests/ipc_peer.py pair
