@@ -172,12 +172,14 @@ extern "C" int gs_sym_rank_rows(int64_t n_pad, int32_t nranks, int32_t rank, int
   return 0;
 }
 
-// Largest reduction-tree node level in use (gs_common.h sym_node_maxl; the A/B knob
-// GRAVSIM_SYM_NODE_SPLIT=0 keeps one rank's range as a single node).
+// Largest reduction-tree node level in use: maximal nodes (one per rank for P dividing 64).
+// GRAVSIM_SYM_NODE_SPLIT=1 (A/B only) splits one rank's range into 8 nodes, 8x the threads
+// of the node reduce with the same bits; it measured slower: reduce phase at 1M 1373-1381 us
+// per step against 1342-1343 (kernel traces, profiles/r3_reduce_fork_split_ab.txt).
 extern "C" int32_t gs_sym_node_maxl(int32_t B, int32_t nranks) {
   const char* v = getenv("GRAVSIM_SYM_NODE_SPLIT");
-  if (v && atoi(v) == 0) return 30;
-  return gs::sym_node_maxl(B, nranks);
+  if (v && atoi(v) != 0) return gs::sym_node_maxl(B, nranks);
+  return 30;
 }
 
 // Row blocks and reduction-tree nodes: B blocks of RB rows; rank `rank` sends nn dyadic

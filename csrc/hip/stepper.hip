@@ -183,7 +183,10 @@ struct gs_stepper {
   // exactly the failure class of a stale re-armed counter (a memset node when captured).
   unsigned fault_skip = 0;
   bool rearm_lastwg = false;  // GRAVSIM_SYM_REARM=lastwg: round 2's in-kernel counter re-arm
-  bool fork_row = true;       // GRAVSIM_SYM_FORK_ROW=0: row reduce after the node reduce (A/B)
+  // GRAVSIM_SYM_FORK_ROW=1 (A/B only): the row reduce on a second stream beside the node
+  // reduce. Measured slower: the two streaming sums contend (reduce phase at 1M 1533-1592 us
+  // per step against 1342-1381 in sequence; profiles/r3_reduce_fork_split_ab.txt).
+  bool fork_row = false;
   // Segmented step graph of multi-rank runs (use_graph 1): the compute stream's work between
   // two cross-stream points is captured as one graph segment; the collectives (RCCL, or the
   // emulation's modeled ones) and the event record/wait that order them against the compute
@@ -827,8 +830,8 @@ int sym_force(gs_stepper* s, gs::SymArgs a, bool overlap_gather, bool exchange =
     if (fused_tail(s)) continue;  // reductions + integrate in sym_tail_kernel (one band)
     const bool last = b0 + a.band_rows >= a.rows;
     // Without an exchange the row reduce (Pi, Pd -> Ti) and the block / node reduce (Pj) are
-    // independent streaming sums: fork the row reduce onto s_rem so both share the GPU (a
-    // fork / join inside a captured step graph).
+    // independent: fork_row (A/B knob) runs the row reduce on s_rem beside them (a fork /
+    // join inside a captured step graph). In sequence is faster (see fork_row).
     const bool fork = !xcomm(s) && s->fork_row;
     if (fork) {
       GS_HIP(hipEventRecord(s->ev_fork, s->s_comp));
@@ -1287,7 +1290,7 @@ int gs_stepper_create(const gs_config* cfg, gs_stepper** out) {
   if (const char* v = getenv("GRAVSIM_SYM_PARITY")) s->parity = atoi(v) != 0 ? 1 : 0;
   if (const char* v = getenv("GRAVSIM_FAULT_SKIP_UNITS")) s->fault_skip = (unsigned)atoi(v);
   if (const char* v = getenv("GRAVSIM_SYM_REARM")) s->rearm_lastwg = strcmp(v, "lastwg") == 0;
-  if (const char* v = getenv("GRAVSIM_SYM_FORK_ROW")) s->fork_row = atoi(v) != 0;
+  if (const char* v = getenv("GRAVSIM_SYM_FORK_ROW")) s->fork_row = atoi(v) != 0;  // (A/B)
   const int64_t own_first = s->L.local_begin / s->L.chunk;
   const int64_t own_last = (s->L.local_begin + s->L.n_local) / s->L.chunk;
   s->own_c0 = (int)(own_first < s->L.n_chunks ? own_first : s->L.n_chunks);

@@ -108,9 +108,10 @@ GS_HD int32_t sym_node_count(int32_t lo, int32_t hi, int32_t maxl = 30) {
   }
   return n;
 }
-// Largest node level: one rank (nothing crosses ranks) splits its range into 8 nodes, so
-// the node reduce has 8x the threads (the receiver's merge gives the same bits); with
-// several ranks nodes stay maximal, since every node is sent to every other rank.
+// Node level cap of the GRAVSIM_SYM_NODE_SPLIT=1 A/B variant (layout.cpp gs_sym_node_maxl):
+// one rank splits its range into 8 nodes (8x the node-reduce threads; the receiver's merge
+// gives the same bits); with several ranks nodes stay maximal, since every node is sent to
+// every other rank.
 GS_HD int32_t sym_node_maxl(int32_t B, int32_t P) {
   if (P > 1) return 30;
   int32_t lb = 0;

@@ -119,9 +119,9 @@ def dyadic_nodes(lo: int, hi: int, maxl: int = 30) -> list[tuple[int, int]]:
 
 
 def sym_node_maxl(B: int, P: int) -> int:
-    """One rank splits its range into 8 nodes (more threads in the node reduce, same bits);
-    with several ranks every node is sent to every other rank, so nodes stay maximal."""
-    if P > 1:
+    """Node level cap (layout.cpp gs_sym_node_maxl): nodes are maximal unless the A/B knob
+    GRAVSIM_SYM_NODE_SPLIT=1 splits one rank's range into 8 (measured slower)."""
+    if P > 1 or os.environ.get("GRAVSIM_SYM_NODE_SPLIT", "0") in ("", "0"):
         return 30
     lb = B.bit_length() - 1
     return lb - 3 if lb > 3 else 0

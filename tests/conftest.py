@@ -32,7 +32,8 @@ def hip():
 # module imported at collection) would silently alter every later test.
 _PROCESS_KNOBS = ("GRAVSIM_EMULATE_RANK", "GRAVSIM_UNIT_TRACE", "GRAVSIM_EMU_COMM_GBPS",
                   "GRAVSIM_SYM_DYN_CAP", "GRAVSIM_SYM_FIRST_WAVE", "GRAVSIM_SYM_BAND_MB",
-                  "GRAVSIM_FAULT_SKIP_UNITS", "GRAVSIM_SYM_REARM")
+                  "GRAVSIM_FAULT_SKIP_UNITS", "GRAVSIM_SYM_REARM",
+                  "GRAVSIM_SYM_FORK_ROW", "GRAVSIM_SYM_NODE_SPLIT")
 
 
 @pytest.fixture(autouse=True)
