@@ -502,35 +502,43 @@ __global__ __launch_bounds__(Geo<double>::kThreads) GS_SYM_WPE64 void force_sym_
 // receiver completes the tree with a binary-counter merge (left + right), so S(x) has the
 // same bits for every rank count.
 
-// Pending sub-trees of a binary-counter merge: acc[k] holds a finished node of 2^k blocks
-// while bit k of occ is set. Fully unrolled with constant indices (registers, no scratch).
+// Binary-counter merge of dyadic sub-trees pushed in global order: pos counts the blocks
+// merged so far and its set bits are the pending levels, kept as a stack with the lowest
+// (most recent) on top. A node of level l starts at a multiple of 2^l, so nothing below l is
+// pending: pushing it merges (left + right) with the top while bit l, l + 1, ... of pos is
+// set (the carries of pos + 2^l), then becomes the top. Every index is a compile-time
+// constant, so the stack lives in registers (an earlier form indexed acc[level] and went to
+// scratch); callers push in a wave-uniform order, so the carry branches do not diverge.
 template <typename T, int C>
 struct TreeAcc {
-  T acc[7][C];
-  unsigned occ;
+  static constexpr int kDepth = 7;  // B <= 64 blocks
+  T st[kDepth][C];
+  unsigned pos;
   __device__ __forceinline__ void push(int level, T* v) {
+    unsigned p = pos >> level;
 #pragma unroll
-    for (int k = 0; k < 7; ++k) {
-      if (k < level) continue;
-      if (occ & (1u << k)) {
+    for (int k = 0; k < kDepth; ++k) {
+      if (!(p & 1u)) break;
 #pragma unroll
-        for (int c = 0; c < C; ++c) v[c] = acc[k][c] + v[c];  // left + right
-        occ &= ~(1u << k);
-      } else {
+      for (int c = 0; c < C; ++c) v[c] = st[0][c] + v[c];  // left + right
 #pragma unroll
-        for (int c = 0; c < C; ++c) acc[k][c] = v[c];
-        occ |= 1u << k;
-        return;
-      }
+      for (int s = 0; s + 1 < kDepth; ++s)
+#pragma unroll
+        for (int c = 0; c < C; ++c) st[s][c] = st[s + 1][c];
+      p >>= 1;
     }
+#pragma unroll
+    for (int s = kDepth - 1; s > 0; --s)
+#pragma unroll
+      for (int c = 0; c < C; ++c) st[s][c] = st[s - 1][c];
+#pragma unroll
+    for (int c = 0; c < C; ++c) st[0][c] = v[c];
+    pos += 1u << level;
   }
-  __device__ __forceinline__ void result(T* v) const {  // occ holds exactly one bit
+  // Once pos is a power of two (a whole node or the whole tree) one sub-tree is pending.
+  __device__ __forceinline__ void result(T* v) const {
 #pragma unroll
-    for (int k = 0; k < 7; ++k)
-      if (occ == (1u << k)) {
-#pragma unroll
-        for (int c = 0; c < C; ++c) v[c] = acc[k][c];
-      }
+    for (int c = 0; c < C; ++c) v[c] = st[0][c];
   }
 };
 
@@ -629,7 +637,7 @@ __global__ __launch_bounds__(256) void sym_node_reduce_kernel(SymArgs a) {
     l = sym_dyadic_level(lo, own_hi, maxl);
   }
   TreeAcc<T, 3> t;
-  t.occ = 0;
+  t.pos = 0;
   const T* Bb = static_cast<const T*>(a.Bbuf);
   for (int b = lo; b < lo + (1 << l); ++b) {
     T v[3];
@@ -661,7 +669,7 @@ __global__ __launch_bounds__(256) void sym_node_reduce_kernel(SymArgs a) {
 template <typename T>
 __device__ __forceinline__ void sym_tree_all(const SymArgs& a, int64_t li, T* S) {
   TreeAcc<T, 3> t;
-  t.occ = 0;
+  t.pos = 0;
   const T* R = static_cast<const T*>(a.Rbuf) + li;
   const int maxl = a.node_maxl;
   int j = 0;
@@ -802,7 +810,7 @@ __global__ __launch_bounds__(192) void sym_tail_kernel(SymArgs a) {
     for (; sg < segs; ++sg) ti += __builtin_nontemporal_load(pi + (int64_t)sg * 3 * kSymC);
     // + S: the tree over the B row blocks (sym_node_reduce_kernel's single node [0, B))
     TreeAcc<T, 1> t;
-    t.occ = 0;
+    t.pos = 0;
     const T* pjc = static_cast<const T*>(a.Pj) + k * kSymC + c;
     for (int b = 0; b < a.B; ++b) {
       const int A_lo = b * a.RB, A_hi = min((b + 1) * a.RB, a.real_chunks);

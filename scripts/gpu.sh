@@ -18,6 +18,7 @@
 #   ipc                       two-process HIP IPC with / without HSA_ENABLE_IPC_MODE_LEGACY=0
 #   abaudit[:<bench args>]    interleaved bench.py A/B of the work-audit counter (GRAVSIM_AUDIT)
 #   abfork[:<bench args>]     reduce-phase span per step: row reduce forked / node split A/B
+#   span[:<bench args>]       reduce-phase span per step of the default schedule
 # Outputs land in gpurun_out/<task>*.log.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
@@ -90,6 +91,16 @@ for task in "$@"; do
           --warmup 2 --exact-steps 0 --phase-steps 0 --check-samples 0 --no-replay-audit $a
         t=$(find $d -name "*kernel_trace.csv" | head -1)
         echo "fork=$f split=$sp $(python scripts/reduce_span.py $t)" | tee -a $out/abfork.txt
+      done ;;
+    span)
+      # reduce-phase span per step of the default schedule (two runs), same recipe as abfork
+      for i in 1 2; do
+        d=$out/span_$i; rm -rf $d
+        step 600 $d.log rocprofv3 --kernel-trace -d $d -o tr --output-format csv -- python \
+          bench.py --steps 6 --warmup 2 --exact-steps 0 --phase-steps 0 --check-samples 0 \
+          --no-replay-audit $a
+        t=$(find $d -name "*kernel_trace.csv" | head -1)
+        echo "default $(python scripts/reduce_span.py $t)" | tee -a $out/span.txt
       done ;;
     ipc)
       # two-process HIP IPC (memory + event) with the launcher's dmabuf setting and without it
