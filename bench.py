@@ -319,6 +319,9 @@ def main(argv=None) -> int:
     t1 = time.perf_counter()
     wall = comm.allreduce_max(dist, t1 - t0)
     ginfo = eng.graph_info()
+    # HBM the stepper holds (its allocation ledger; RCCL's own buffers excluded), max over ranks
+    mem = eng.mem_info() if hasattr(eng, "mem_info") else {}
+    hbm_max = comm.allreduce_max(dist, float(sum(mem.values())))
 
     # ---- audits of the timed work (untimed) --------------------------------------------
     failures = []
@@ -447,6 +450,8 @@ def main(argv=None) -> int:
                 "momentum_rel_drift": drift,
                 "exact_cutoff_ms_per_step": exact_ms,
                 "nonfinite": int(bad),
+                "hbm": {"gb_per_rank_max": round(hbm_max / 1e9, 3),
+                        "by_buffer_gb_rank0": {k: round(v / 1e9, 4) for k, v in mem.items()}},
             },
             "work_audit": "ok" if not failures else "; ".join(failures),
             "audit": {"units": units, "replay": replay},

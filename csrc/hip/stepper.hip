@@ -10,28 +10,32 @@
 //                    -> in-place ncclAllGather of (x, y, z, mu) rows on a high-priority comm
 //                    stream, overlapped with the rank-local j-chunks on the compute stream;
 //                    ordering by events, no barrier.
-// Step k (P ranks, ping-pong buffers X[0], X[1]):
+// One-sided split schedule, step k (P ranks, ping-pong buffers X[0], X[1]):
 //   s_comm : wait(own slice of X[k&1] written) -> ncclAllGather in place -> record gathered
 //   s_comp : split kernel over own chunks (reads only the own slice)     -> partials
 //   s_rem  : wait(gathered) -> ONE split launch over every remote chunk  -> partials
 //   s_comp : wait(remote) -> reduce in canonical chunk order + KD integrate
 //            -> own slice of X[(k+1)&1]
-// The two split launches run concurrently (one chunk per workgroup). With one rank the step
-// is a single fused launch (KD integrate in its epilogue) or split + reduce; the loop is
-// captured once into a hipGraph (two steps = one ping-pong period) and replayed. With
-// use_graph >= 2 the multi-rank step, collective included, is captured too.
+// With one rank the step is a single fused launch (KD integrate in its epilogue) or split +
+// reduce.
 //
-// Newton-3 sym schedule (GS_MODE_SYM, the default from 16K bodies fp32 / 32K fp64; nbody_sym.hip):
-//   s_comm : ncclAllGather in place (as above)
-//   s_comp : wait(gathered) -> every unit in one launch (diagonal chunks one-sided, shell
-//            chunks both sides of every pair) -> group reduce
-//   s_comm : group-sum exchange: ncclSend/ncclRecv to every peer (one group call), beside
-//            the row reduce on s_comp
-//   s_comp : wait(exchange) -> finalize (fixed-order sum + KD integrate) -> own slice of
-//            X[(k+1)&1]
-// (work beside the gather: see sym_force; a launch boundary costs more than the gather.)
-// The partial slots and summation order depend on N only, so every P dividing 8 gives the
-// same bits.
+// Newton-3 sym schedule (GS_MODE_SYM, the default from 16K bodies fp32 / 32K fp64, any P up
+// to 8; nbody_sym.hip):
+//   s_comm : all-gather in place (ncclAllGather, or grouped ncclBroadcast for uneven slices),
+//            then gate_set_kernel opens the gather gate
+//   s_comp : ONE force launch, rank-local units first; a remote unit that finds the gate
+//            closed defers itself; the deferred units run in a small launch behind the gather
+//            event (sym_overlap 3, the multi-rank default) -> node reduce (this rank's dyadic
+//            sub-trees of the row-block tree, per destination rank)
+//   s_comm : node exchange: ncclSend/ncclRecv of every destination's node sums (one group)
+//   s_comp : row reduce (i-side totals), then wait(exchange) -> finalize (the tree merge in
+//            global node order + KD integrate) -> own slice of X[(k+1)&1]
+// The partial slots and every summation order depend on n_pad only, so any P from 1 to 8
+// gives the same bits.
+//
+// Replay: one rank captures two steps (one ping-pong period) as one hipGraph; multi-rank
+// steps replay a segmented plan (compute segments as graphs, collectives eager between them,
+// build_plan); use_graph >= 2 captures the collectives too (opt-in, --graph-comm).
 #include <dlfcn.h>
 #include <execinfo.h>
 #include <hip/hip_runtime.h>
@@ -201,6 +205,15 @@ struct gs_stepper {
   std::vector<PlanOp> plan;  // one ping-pong period (two steps)
   bool rec = false;          // recording a plan: s_comp is capturing a segment
   int plan_graphs = 0;       // graph segments per period (diagnostics)
+  // Device memory ledger: every HBM buffer the stepper owns, by name (gs_stepper_mem_entry);
+  // destroy frees exactly these. All of them are allocated before the first step, sized from
+  // the layout (the sym bands from the free HBM), so nothing is allocated inside the loop.
+  struct MemEntry {
+    void* p;
+    size_t bytes;
+    const char* tag;
+  };
+  std::vector<MemEntry> mem;
 };
 
 namespace {
@@ -239,6 +252,27 @@ struct Range {
 };
 
 size_t row_bytes(const gs_stepper* s) { return 4 * s->esz; }
+
+// hipMalloc through the ledger; on failure the error names the buffer, its size and the
+// free HBM (a 16M-body rank needs ~110 GB of partial slots).
+template <typename T>
+int dev_alloc(gs_stepper* s, T** p, size_t bytes, const char* tag) {
+  void* v = nullptr;
+  const hipError_t e = hipMalloc(&v, bytes ? bytes : 16);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    size_t free_b = 0, total_b = 0;
+    (void)hipMemGetInfo(&free_b, &total_b);
+    char b[320];
+    snprintf(b, sizeof(b), "device allocation of %s (%.3f GB) failed: %s (free %.3f of %.3f GB)",
+             tag, bytes / 1e9, hipGetErrorString(e), free_b / 1e9, total_b / 1e9);
+    gs_set_error(b);
+    return -1;
+  }
+  *p = static_cast<T*>(v);
+  s->mem.push_back({v, bytes, tag});
+  return 0;
+}
 
 // ---- compute-stream ordering points (eager, or cut points of a recorded plan) ----------
 // End the open capture segment and keep it as a graph if it holds any node.
@@ -525,18 +559,18 @@ int ensure_sym(gs_stepper* s) {
   if (band < rb) band = rb;
   if (band > rows) band = rows;
   s->sym_band = (int32_t)band;
-  GS_HIP(hipMalloc(&s->sym_Pi, band * s->sym_S_n * 3 * gs::kSymC * e));
-  GS_HIP(hipMalloc(&s->sym_Pj, band * s->sym_H * 3 * gs::kSymC * e));
-  GS_HIP(hipMalloc(&s->sym_Pd, band * s->sym_D * 3 * gs::kSymC * e));
-  GS_HIP(hipMalloc(&s->sym_Ti, 3 * nl * e));
+  if (dev_alloc(s, &s->sym_Pi, band * s->sym_S_n * 3 * gs::kSymC * e, "sym_Pi")) return -1;
+  if (dev_alloc(s, &s->sym_Pj, band * s->sym_H * 3 * gs::kSymC * e, "sym_Pj")) return -1;
+  if (dev_alloc(s, &s->sym_Pd, band * s->sym_D * 3 * gs::kSymC * e, "sym_Pd")) return -1;
+  if (dev_alloc(s, &s->sym_Ti, 3 * nl * e, "sym_Ti")) return -1;
   const size_t nb = (size_t)((s->L.n + gs::kSymC - 1) / gs::kSymC) * gs::kSymC;  // real chunks
-  if (band < rows) GS_HIP(hipMalloc(&s->sym_Bb, rows / rb * 3 * nb * e));
+  if (band < rows && dev_alloc(s, &s->sym_Bb, rows / rb * 3 * nb * e, "sym_Bbuf")) return -1;
   const int r = s->cfg.rank;
-  GS_HIP(hipMalloc(&s->sym_S, (size_t)s->nn[r] * 3 * (size_t)s->L.n_pad * e));
+  if (dev_alloc(s, &s->sym_S, (size_t)s->nn[r] * 3 * (size_t)s->L.n_pad * e, "sym_S")) return -1;
   // (zeroed once: the per-rank emulation never receives the other ranks' nodes)
   GS_HIP(hipMemsetAsync(s->sym_S, 0, (size_t)s->nn[r] * 3 * (size_t)s->L.n_pad * e, s->s_comp));
   if (P > 1) {
-    GS_HIP(hipMalloc(&s->sym_R, (size_t)s->sym_NN * 3 * nl * e));
+    if (dev_alloc(s, &s->sym_R, (size_t)s->sym_NN * 3 * nl * e, "sym_R")) return -1;
     GS_HIP(hipMemsetAsync(s->sym_R, 0, (size_t)s->sym_NN * 3 * nl * e, s->s_comp));
   } else {
     s->sym_R = s->sym_S;  // [node 0][3][n_pad] either way
@@ -550,8 +584,7 @@ int ensure_sym(gs_stepper* s) {
 // when the requested cutoff lies inside that core (the default 1e-10 m does).
 int ensure_partial(gs_stepper* s) {
   if (s->partial) return 0;
-  GS_HIP(hipMalloc(&s->partial, (size_t)s->L.n_chunks * s->L.n_local * row_bytes(s)));
-  return 0;
+  return dev_alloc(s, &s->partial, (size_t)s->L.n_chunks * s->L.n_local * row_bytes(s), "partial");
 }
 
 void resolve_force_mode(gs_stepper* s) {
@@ -1305,6 +1338,13 @@ int gs_stepper_create(const gs_config* cfg, gs_stepper** out) {
       return -1;                  \
     }                             \
   } while (0)
+#define ALLOC_CLEAN(ptr, bytes, tag)     \
+  do {                                   \
+    if (dev_alloc(s, ptr, bytes, tag)) { \
+      gs_stepper_destroy(s);             \
+      return -1;                         \
+    }                                    \
+  } while (0)
   FAIL_CLEAN(hipSetDevice(cfg->device));
   FAIL_CLEAN(hipDeviceGetAttribute(&s->cus, hipDeviceAttributeMultiprocessorCount, cfg->device));
   {
@@ -1343,10 +1383,10 @@ int gs_stepper_create(const gs_config* cfg, gs_stepper** out) {
   s->prog.assign(64, nullptr);
   for (auto& e : s->prog) FAIL_CLEAN(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   const size_t rb = row_bytes(s);
-  FAIL_CLEAN(hipMalloc(&s->X[0], (size_t)s->L.n_pad * rb));
-  FAIL_CLEAN(hipMalloc(&s->X[1], (size_t)s->L.n_pad * rb));
-  FAIL_CLEAN(hipMalloc(&s->vel, (size_t)s->L.n_local * rb));
-  FAIL_CLEAN(hipMalloc(&s->acc, (size_t)s->L.n_local * rb));
+  ALLOC_CLEAN(&s->X[0], (size_t)s->L.n_pad * rb, "X0");
+  ALLOC_CLEAN(&s->X[1], (size_t)s->L.n_pad * rb, "X1");
+  ALLOC_CLEAN(&s->vel, (size_t)s->L.n_local * rb, "vel");
+  ALLOC_CLEAN(&s->acc, (size_t)s->L.n_local * rb, "acc");
   // Per-chunk partials (n_chunks x n_local rows) only for the split schedule; a single-rank
   // fused run never touches them (16M bodies: 64 GB saved), and allocates on demand.
   if ((s->L.mode == GS_MODE_SPLIT || (cfg->nranks > 1 && s->L.mode != GS_MODE_SYM)) &&
@@ -1358,23 +1398,23 @@ int gs_stepper_create(const gs_config* cfg, gs_stepper** out) {
     gs_stepper_destroy(s);
     return -1;
   }
-  FAIL_CLEAN(hipMalloc(&s->mass_dev, (size_t)s->L.n_pad * sizeof(double)));
-  FAIL_CLEAN(hipMalloc(&s->nonfinite, sizeof(unsigned long long)));
-  FAIL_CLEAN(hipMalloc(&s->ring_gate, 16 * sizeof(unsigned)));
+  ALLOC_CLEAN(&s->mass_dev, (size_t)s->L.n_pad * sizeof(double), "mass");
+  ALLOC_CLEAN(&s->nonfinite, sizeof(unsigned long long), "nonfinite");
+  ALLOC_CLEAN(&s->ring_gate, 16 * sizeof(unsigned), "ring_gate");
   FAIL_CLEAN(hipMemsetAsync(s->ring_gate, 0, 16 * sizeof(unsigned), s->s_comp));
   // [0..1] gather gates, [2..3] deferral stats, [4] dynamic unit-fetch counter
-  FAIL_CLEAN(hipMalloc(&s->gate_buf, 8 * sizeof(unsigned)));
+  ALLOC_CLEAN(&s->gate_buf, 8 * sizeof(unsigned), "gate");
   FAIL_CLEAN(hipMemsetAsync(s->gate_buf, 0, 8 * sizeof(unsigned), s->s_comp));
   if (s->L.mode == GS_MODE_SYM && !(getenv("GRAVSIM_AUDIT") && atoi(getenv("GRAVSIM_AUDIT")) == 0)) {
     // (GRAVSIM_AUDIT=0: no unit counter, for A/B timing of its cost only)
-    FAIL_CLEAN(hipMalloc(&s->audit, sizeof(unsigned long long)));
+    ALLOC_CLEAN(&s->audit, sizeof(unsigned long long), "audit");
     FAIL_CLEAN(hipMemsetAsync(s->audit, 0, sizeof(unsigned long long), s->s_comp));
   }
   if (s->L.mode == GS_MODE_SYM) {
     // Deferred-unit list of the gated launch (one band's units) and the local-first order.
     const int rows = (int)(s->L.n_local / gs::kSymC);
     const size_t units = (size_t)rows * (s->sym_S_n + s->sym_D) + 1;
-    FAIL_CLEAN(hipMalloc(&s->defer, units * sizeof(unsigned)));
+    ALLOC_CLEAN(&s->defer, units * sizeof(unsigned), "defer");
     FAIL_CLEAN(hipMemsetAsync(s->defer, 0, units * sizeof(unsigned), s->s_comp));
     // unit -> row << 16 | segment (bit 31: remote), local units first (layout.cpp).
     long fill = 4L * s->cus;  // two dispatch waves of 2 workgroups per CU
@@ -1388,7 +1428,7 @@ int gs_stepper_create(const gs_config* cfg, gs_stepper** out) {
                                       lf.data(), (int64_t)lf.size());
     lf.resize(got > 0 ? (size_t)got : 0);  // 0: geometry too large for the 16-bit fields
     if (!lf.empty()) {
-      FAIL_CLEAN(hipMalloc(&s->sym_lf, lf.size() * sizeof(int32_t)));
+      ALLOC_CLEAN(&s->sym_lf, lf.size() * sizeof(int32_t), "unit_map");
       FAIL_CLEAN(hipMemcpy(s->sym_lf, lf.data(), lf.size() * sizeof(int32_t),
                            hipMemcpyHostToDevice));
     }
@@ -1396,7 +1436,7 @@ int gs_stepper_create(const gs_config* cfg, gs_stepper** out) {
   if (s->L.mode == GS_MODE_SYM && getenv("GRAVSIM_UNIT_TRACE")) {
     // One entry per unit of a band-wide launch plus as many deferred ones (units 7).
     s->utrace_main = (int64_t)s->sym_band * (s->sym_S_n + s->sym_D);
-    FAIL_CLEAN(hipMalloc(&s->utrace, (size_t)(2 * s->utrace_main) * 4 * sizeof(unsigned long long)));
+    ALLOC_CLEAN(&s->utrace, (size_t)(2 * s->utrace_main) * 4 * sizeof(unsigned long long), "unit_trace");
     FAIL_CLEAN(hipMemsetAsync(s->utrace, 0, (size_t)(2 * s->utrace_main) * 4 * 8, s->s_comp));
   }
   if (s->emulate && s->emu_gbps > 0.0) {
@@ -1404,7 +1444,7 @@ int gs_stepper_create(const gs_config* cfg, gs_stepper** out) {
     s->emu_cap = gather_bytes(s);
     if (s->L.mode == GS_MODE_SYM && exchange_bytes(s) > s->emu_cap) s->emu_cap = exchange_bytes(s);
     s->emu_cap &= ~(size_t)15;
-    FAIL_CLEAN(hipMalloc(&s->emu_buf, s->emu_cap ? s->emu_cap : 16));
+    ALLOC_CLEAN(&s->emu_buf, s->emu_cap, "emu_comm");
   }
   // Zero on the compute stream itself: it is non-blocking, so a legacy-stream hipMemset
   // would NOT be ordered before later work on it (it could land after the IC kernel).
@@ -1413,6 +1453,7 @@ int gs_stepper_create(const gs_config* cfg, gs_stepper** out) {
   FAIL_CLEAN(hipMemsetAsync(s->vel, 0, (size_t)s->L.n_local * rb, s->s_comp));
   FAIL_CLEAN(hipStreamSynchronize(s->s_comp));
 #undef FAIL_CLEAN
+#undef ALLOC_CLEAN
   *out = s;
   return 0;
 }
@@ -1425,13 +1466,8 @@ int gs_stepper_destroy(gs_stepper* s) {
   if (s->s_rem2) (void)hipStreamSynchronize(s->s_rem2);
   drop_graphs(s);
   if (s->have_comm) (void)ncclCommDestroy(s->comm);
-  if (s->sym_R == s->sym_S) s->sym_R = nullptr;
-  for (void* p : {s->X[0], s->X[1], s->vel, s->partial, s->acc, (void*)s->mass_dev,
-                  (void*)s->nonfinite, (void*)s->sym_Pi, (void*)s->sym_Pj, (void*)s->sym_Pd,
-                  (void*)s->sym_S, (void*)s->sym_R, (void*)s->sym_Ti, (void*)s->gate_buf,
-                  (void*)s->defer, (void*)s->sym_lf, s->emu_buf, (void*)s->utrace,
-                  (void*)s->ring_gate, (void*)s->audit, (void*)s->sym_Bb})
-    if (p) (void)hipFree(p);
+  for (const auto& m : s->mem) (void)hipFree(m.p);
+  s->mem.clear();
   for (hipEvent_t e : {s->ev_ready, s->ev_gathered, s->ev_t0, s->ev_local, s->ev_end,
                        s->ev_remote, s->ev_fork, s->ev_rem2, s->ev_sym})
     if (e) (void)hipEventDestroy(e);
@@ -1585,6 +1621,15 @@ int gs_stepper_set_cutoff_mode(gs_stepper* s, int32_t mode) {
 }
 
 int32_t gs_stepper_get_overlap(gs_stepper* s) { return s->sym_overlap; }
+
+int32_t gs_stepper_mem_entry(gs_stepper* s, int32_t i, const char** tag, uint64_t* bytes) {
+  if (!s) return -1;
+  if (i >= 0 && i < (int32_t)s->mem.size()) {
+    if (tag) *tag = s->mem[i].tag;
+    if (bytes) *bytes = s->mem[i].bytes;
+  }
+  return (int32_t)s->mem.size();
+}
 
 int gs_stepper_graph_info(gs_stepper* s, int32_t* mode, int32_t* segments) {
   if (mode) *mode = !s->plan.empty() ? 2 : (s->graph ? 1 : 0);

@@ -188,6 +188,9 @@ int gs_stepper_audit_reset(gs_stepper* s);
 // segmented plan (multi-rank: compute segments as graphs, collectives eager between them);
 // *segments = graph segments per two steps (mode 2).
 int gs_stepper_graph_info(gs_stepper* s, int32_t* mode, int32_t* segments);
+// Device memory ledger: entry i (name, bytes) of the HBM buffers this stepper owns; returns
+// the entry count (i out of range: only the count).
+int32_t gs_stepper_mem_entry(gs_stepper* s, int32_t i, const char** tag, uint64_t* bytes);
 // Unit timeline of the last sym force launch (stepper created with GRAVSIM_UNIT_TRACE set):
 // copies up to `cap` entries of 4 words {start, end (100 MHz ticks), HW_ID | XCC_ID << 32,
 // row << 32 | segment} (all zero: the slot ran no unit) and clears them. Returns the count;

@@ -161,6 +161,8 @@ def hip_lib():
         _sig(lib, "gs_stepper_audit", c_int32, [S, POINTER(c_uint64), POINTER(c_uint64)])
         _sig(lib, "gs_stepper_audit_reset", c_int32, [S])
         _sig(lib, "gs_stepper_graph_info", c_int32, [S, POINTER(c_int32), POINTER(c_int32)])
+        _sig(lib, "gs_stepper_mem_entry", c_int32,
+             [S, c_int32, POINTER(ctypes.c_char_p), POINTER(c_uint64)])
         _sig(lib, "gs_stepper_set_timeout", c_int32, [S, c_double])
         _sig(lib, "gs_stepper_unit_trace", c_int64, [S, c_void_p, c_int64])
         _sig(lib, "gs_stepper_compute_stream", c_void_p, [S])

@@ -190,6 +190,17 @@ class HipEngine:
         self.lib.gs_stepper_graph_info(self._s, ctypes.byref(m), ctypes.byref(n))
         return {"mode": ("eager", "graph", "segmented")[m.value], "segments": n.value}
 
+    def mem_info(self) -> dict:
+        """HBM this rank's stepper holds, by buffer (bytes), from its allocation ledger (RCCL's
+        own buffers are not included)."""
+        tag, nb = ctypes.c_char_p(), ctypes.c_uint64()
+        n = self.lib.gs_stepper_mem_entry(self._s, -1, None, None)
+        out: dict = {}
+        for i in range(max(n, 0)):
+            self.lib.gs_stepper_mem_entry(self._s, i, ctypes.byref(tag), ctypes.byref(nb))
+            out[tag.value.decode()] = out.get(tag.value.decode(), 0) + int(nb.value)
+        return out
+
     def audit_reset(self) -> None:
         _native.check(self.lib, self.lib.gs_stepper_audit_reset(self._s), "audit reset")
 

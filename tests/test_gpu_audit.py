@@ -87,6 +87,7 @@ def test_bench_audit_ok_and_reports_physics(hip):
     assert c["sampled_rel_err"] < 1e-4 and c["sampled_rel_err_final"] < 1e-4
     assert c["momentum_rel_drift"] < 1e-5
     assert c["exact_cutoff_ms_per_step"] > 0
+    assert c["hbm"]["gb_per_rank_max"] > 0 and "sym_Pj" in c["hbm"]["by_buffer_gb_rank0"]
 
 
 def test_bench_audit_catches_skipped_units(hip):
@@ -173,3 +174,27 @@ def test_lastwg_rearm_targeted(hip, monkeypatch, n, band_mb, steps):
             e.close()
     assert np.array_equal(out["lastwg"][0], out["memset"][0])
     assert np.array_equal(out["lastwg"][1], out["memset"][1])
+
+
+def test_device_memory_ledger(hip):
+    """The stepper's HBM ledger (gs_stepper_mem_entry) lists every buffer with the size the
+    layout implies: ping-pong rows, the one band of partial slots, the node sums."""
+    from gravsim.parallel import partition
+    from gravsim.runtime.engines import HipEngine
+
+    n = 65536
+    e = HipEngine(SimConfig(n=n, dtype="fp32", device="gpu", mode="sym"))
+    try:
+        m = e.mem_info()
+        n_pad = e.layout.n_pad
+        g = partition.sym_geometry(n_pad)
+        assert m["X0"] == m["X1"] == n_pad * 16
+        assert m["vel"] == n_pad * 16
+        slots = n_pad * 3 * 4
+        assert m["sym_Pi"] == slots * g["S"] and m["sym_Pj"] == slots * g["H"]
+        assert m["sym_Pd"] == slots * g["D"]
+        assert m["sym_S"] == len(partition.sym_nodes(n_pad, 1)[0]) * 3 * n_pad * 4
+        assert "sym_R" not in m and "partial" not in m  # one rank: R is S; no split slots
+        assert all(v > 0 for v in m.values())
+    finally:
+        e.close()
