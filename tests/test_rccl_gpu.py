@@ -7,8 +7,10 @@ then treats the ranks as separate hosts and moves data through its socket transp
 loopback instead of xGMI. The collectives, peer calls, stream/event ordering and buffer
 offsets of the multi-rank schedule are the production ones; only the transport differs.
 """
+import json
 import os
 import socket
+import time
 
 import numpy as np
 import pytest
@@ -36,7 +38,9 @@ def _worker(rank, world, port, out_dir, n, steps, strategy="allgather", mode="au
     from gravsim.parallel import comm
     from gravsim.runtime.engines import HipEngine
 
+    t_mark = [("start", time.perf_counter())]
     dist = comm.init(timeout_s=120)
+    t_mark.append(("gloo_init", time.perf_counter()))
     status = "ok"
     try:
         # "<mode>-graph": the multi-rank step, collectives included, captured in a hipGraph;
@@ -50,16 +54,19 @@ def _worker(rank, world, port, out_dir, n, steps, strategy="allgather", mode="au
         eng = HipEngine(cfg, rank, world, device=0, dist=dist)
         uid = HipEngine.unique_id() if rank == 0 else None
         uid = comm.broadcast_bytes(dist, uid)
+        t_mark.append(("engine", time.perf_counter()))
         try:
             eng.comm_init(uid)
         except RuntimeError as e:
             status = "comm_init failed: " + str(e)
+        t_mark.append(("rccl_init", time.perf_counter()))
         ok = comm.allreduce_sum(dist, 0.0 if status == "ok" else 1.0)
         if ok == 0:
             eng.init_ics("solar+random", 5)
             eng.audit_reset()
             eng.step(steps)
             eng.sync(timeout_s=120)
+            t_mark.append(("steps", time.perf_counter()))
             done, per = eng.audit()
             gi = eng.graph_info()
             with open(os.path.join(out_dir, f"audit{rank}.txt"), "w") as f:
@@ -80,8 +87,17 @@ def _worker(rank, world, port, out_dir, n, steps, strategy="allgather", mode="au
             if rank == 0:
                 with open(os.path.join(out_dir, "comm_ms.txt"), "w") as f:
                     f.write(repr(ps["comm_ms"]))
+            t_mark.append(("state_phase", time.perf_counter()))
         eng.close()
+        t_mark.append(("close", time.perf_counter()))
     finally:
+        # GRAVSIM_TEST_TIMES=<file>: per-rank phase seconds, appended as one JSON line
+        if os.environ.get("GRAVSIM_TEST_TIMES"):
+            with open(os.environ["GRAVSIM_TEST_TIMES"], "a") as f:
+                f.write(json.dumps({"world": world, "rank": rank, "n": n, "mode": mode,
+                                    "strategy": strategy, **{
+                                        t_mark[i][0]: round(t_mark[i][1] - t_mark[i - 1][1], 3)
+                                        for i in range(1, len(t_mark))}}) + "\n")
         if rank == 0:
             with open(os.path.join(out_dir, "status.txt"), "w") as f:
                 f.write(status)
