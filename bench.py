@@ -6,7 +6,7 @@ N is fixed as the GPU count grows (strong scaling). The default (mode auto) at t
 the Newton-3 schedule: every unordered pair is evaluated once and applied to both bodies
 (csrc/hip/nbody_sym.hip). Each rank owns N/P bodies (a block of 2048-body chunk rows), joins
 an in-place RCCL all-gather of positions, evaluates its rows' cyclic half-shell of chunk
-pairs, exchanges the group sums of the far sides with ncclSend/ncclRecv, and integrates its
+pairs, exchanges its reduction-tree node sums of the far sides with ncclSend/ncclRecv, and integrates its
 own bodies (kick-drift). Single-rank steps replay a hipGraph; multi-rank steps replay a
 segmented plan: the compute work between two collectives as graph segments, the RCCL calls
 issued eagerly between them (--graph-comm captures the collectives too, opt-in).
@@ -399,7 +399,7 @@ def main(argv=None) -> int:
                                      "cyclic half-shell of 2048-body chunks",
                            "n_pad": lay["n_pad"]}
             exch = ("ring of P-1 neighbour stages" if a.strategy == "ring" else "all-gather") + \
-                " + group-sum send/recv"
+                " + node-sum send/recv"
             pairs = cfg.n * (cfg.n - 1) / 2  # unordered pairs, each evaluated once
         else:
             kernel_info = {"kernel": _native.KERNEL_NAMES.get(lay["kernel"]), "ipl": lay["ipl"],

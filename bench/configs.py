@@ -8,7 +8,7 @@
 
 Per-rank emulation (GRAVSIM_EMULATE_RANK=1) runs one rank's exact launch shapes. Its
 collectives are modeled (csrc/hip/comm_model.hip): the all-gather (1M fp32, P = 8: 14.7 MB
-received per GPU) and the group-sum exchange (10.5 MB) become kernels of those byte counts
+received per GPU) and the node-sum exchange (10.5 MB) become kernels of those byte counts
 on the comm stream that stay resident for latency + bytes / rate, at a conservative
 --comm-gbps (default 64 GB/s per rank, 15 us per collective; xGMI is 7 links x ~153 GB/s).
 Whole-node body-updates/s is predicted as N / ms(rank) with that comm cost included. Writes

@@ -1,6 +1,6 @@
 """Per-GPU step time of ONE rank of a P-rank run, measured on one GPU.
 
-Runs rank r's exact launch shapes (sym: gather -> force units -> group reduce -> group-sum
+Runs rank r's exact launch shapes (sym: gather -> force units -> node reduce -> node-sum
 exchange beside the row reduce -> finalize; split: local + remote chunks on two compute
 streams -> reduce/integrate) under GRAVSIM_EMULATE_RANK=1. The collectives are either free
 (--comm-gbps 0, round 1's emulation) or modeled: a comm_model kernel of the collective's

@@ -118,7 +118,7 @@ struct gs_stepper {
   double eps2 = 0.0;           // r^2 offset used by the kernels
   int cus = 256;               // compute units
   int occ[3] = {0, 0, 0};      // split-kernel workgroups per CU by force mode
-  // Newton-3 symmetric schedule (GS_MODE_SYM): partial slots, group sums, geometry.
+  // Newton-3 symmetric schedule (GS_MODE_SYM): partial slots, node sums, geometry.
   char* sym_Pi = nullptr;  // element type: float or double (esz)
   char* sym_Pj = nullptr;
   char* sym_Pd = nullptr;
@@ -138,7 +138,7 @@ struct gs_stepper {
   bool uniform = true;  // every rank owns the same body count (P | B: ncclAllGather)
   hipEvent_t ev_sym = nullptr;
   // Per-rank emulation with modeled collectives (GRAVSIM_EMU_COMM_GBPS > 0): every all-gather
-  // and group-sum exchange becomes a comm_model_kernel of the same byte count on s_comm.
+  // and node-sum exchange becomes a comm_model_kernel of the same byte count on s_comm.
   double emu_gbps = 0.0, emu_lat_us = 15.0;
   int emu_wgs = 16;
   void* emu_buf = nullptr;
@@ -346,7 +346,7 @@ bool xcomm(const gs_stepper* s) { return s->have_comm || s->emulate; }
 // Remote slices must be brought in before they are read (RCCL, emulation, virtual ranks).
 bool multi(const gs_stepper* s) { return s->have_comm || s->emulate || s->virt; }
 
-// Bytes one rank receives per step: the all-gather's remote slices, and the group sums the
+// Bytes one rank receives per step: the all-gather's remote slices, and the node sums the
 // other ranks send it (sym schedule).
 size_t gather_bytes(const gs_stepper* s) {
   return (size_t)(s->L.n_pad - s->L.n_local) * row_bytes(s);
@@ -765,11 +765,12 @@ int ring_finish(gs_stepper* s, const gs::KArgs<T>& a) {
   return 0;
 }
 
-// Symmetric schedule, parts: 1 = force + group reduce (+ RCCL group-sum exchange),
+// Symmetric schedule, parts: 1 = force + node reduce (+ RCCL node-sum exchange),
 // 2 = finalize (sum + integrate), 3 = both. Virtual-rank groups run part 1 on every shard,
 // exchange by device copies, then part 2 (gs_group_step).
-// Force + reductions over the rank's rows, band by band: the force units, the group reduce
-// (the first band starts S_g, later ones continue it) and the row reduce (Ti). With one band
+// Force + reductions over the rank's rows, band by band: the force units, the block / node
+// reduce (multi-band runs: block leaves into Bbuf, the node reduce after the last band) and
+// the row reduce (Ti). With one band
 // and a pending all-gather (sym_overlap: the multi-rank default is 3, GRAVSIM_SYM_OVERLAP or
 // gs_stepper_set_overlap choose another):
 //   3: ONE launch whose grid lists the rank-local units first; a remote unit runs if the
@@ -787,13 +788,13 @@ int ring_finish(gs_stepper* s, const gs::KArgs<T>& a) {
 // Modes 1 and 2 pay a launch boundary (a unit is ~0.6 ms of work at 1M) to hide a ~0.1 ms
 // gather and lost to 0 in round 1's emulation with free collectives (0: 21.0-21.2 ms,
 // 1: 21.4-21.6, 2: 22.4-22.6; profiles/r1_sym_overlap_ab.txt); they are kept for A/B runs.
-// With `exchange` the RCCL group-sum exchange starts right
-// after the last group reduce and runs beside the last row reduce; the compute stream joins
+// With `exchange` the RCCL node-sum exchange starts right
+// after the node reduce and runs beside the last row reduce; the compute stream joins
 // it afterwards.
-// One rank (no exchange, no virtual shards), one band, up to 256K bodies: the group reduce,
-// row reduce and finalize run as one sym_tail_kernel (same bits). Interleaved A/B
+// One rank (no exchange, no virtual shards), one band, up to 256K bodies: the tree over the
+// row blocks, the row reduce and finalize run as one sym_tail_kernel (same bits). Interleaved A/B
 // (profiles/r2_fused_tail_ab.jsonl): 65K 0.707 vs 0.708 ms, 256K 10.51 vs 10.57 ms, but 1M
-// 166.8 vs 166.1 ms, where the fused kernel's 8x fewer threads for the group sums lose.
+// 166.8 vs 166.1 ms, where the fused kernel's fewer threads for the j-side sums lose.
 // GRAVSIM_SYM_FUSED_TAIL=0 / 1 forces the three-kernel / fused tail at any size.
 // Every sym force launch goes through here: it tells the launcher whether the dynamic unit
 // counter is known to be 0 (re-armed by the fused tail kernel enqueued after the previous
@@ -1699,7 +1700,7 @@ int gs_stepper_wait(gs_stepper* s, double timeout_s) {
 
 // Phase timing of the eager steps enqueued since gs_stepper_set_timing(s, 1) / the previous
 // call (at most 256), averaged per step. out[0] steps, [1] total ms, [2] all-gather ms and
-// [3] group-sum exchange ms (spans on the comm stream), [4] exposed gather ms and [5]
+// [3] node-sum exchange ms (spans on the comm stream), [4] exposed gather ms and [5]
 // exposed exchange ms (compute-stream stalls on them: exposed comm = [4] + [5]), [6] the
 // most force units one step deferred past the gather (overlap 3), [7] reserved (0).
 int gs_stepper_phase_stats(gs_stepper* s, double* out8) {
@@ -2008,7 +2009,7 @@ int gs_stepper_comm_init(gs_stepper* s, const void* id128, int32_t rank, int32_t
       GS_NCCL(ncclGroupEnd());
     }
     if (nranks > 1 && s->L.mode == GS_MODE_SYM) {
-      // The sym schedule's group-sum exchange talks to every peer: connect them all now.
+      // The sym schedule's node-sum exchange talks to every peer: connect them all now.
       GS_NCCL(ncclGroupStart());
       for (int q = 0; q < nranks; ++q) {
         if (q == rank) continue;

@@ -159,7 +159,7 @@ int gs_stepper_accel_step_path(gs_stepper* s, double* acc4);
 int64_t gs_stepper_count_nonfinite(gs_stepper* s);
 int64_t gs_stepper_steps_done(gs_stepper* s);
 // Per-step phase timing of the last step (ms): up to the local/force phase, the step's
-// collectives (all-gather + group-sum exchange spans on the comm stream), and the whole step.
+// collectives (all-gather + node-sum exchange spans on the comm stream), and the whole step.
 int gs_stepper_phase_ms(gs_stepper* s, float* local_ms, float* comm_ms, float* total_ms);
 // Eager steps record per-step phase events while on (hipGraph replay is off meanwhile).
 int gs_stepper_set_timing(gs_stepper* s, int32_t on);

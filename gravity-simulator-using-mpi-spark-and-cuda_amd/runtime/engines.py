@@ -129,7 +129,7 @@ class HipEngine:
 
     def phase_stats(self) -> dict:
         """Per-step averages over the timed steps since set_timing(True) / the last call.
-        comm_ms: the step's collectives on the comm stream (all-gather + group-sum exchange);
+        comm_ms: the step's collectives on the comm stream (all-gather + node-sum exchange);
         exposed_comm_ms: how long the compute stream stalled on them; deferred_units: the
         most force units a step had to run after the gather (overlap 3)."""
         out = (ctypes.c_double * 8)()

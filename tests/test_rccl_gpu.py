@@ -1,5 +1,5 @@
 """Real RCCL path (in-place all-gather + overlapped local chunks, ring pass, the sym
-schedule's group-sum send/recv) with 2 and 4 processes.
+schedule's node-sum send/recv) with 2 to 8 processes (P = 3, 5, 6: uneven slices).
 
 The GPU box exposes one MI355X, so every rank shares device 0. RCCL refuses two ranks of one
 host on one device ("Duplicate GPU detected"), so each rank gets its own NCCL_HOSTID: RCCL
@@ -33,6 +33,12 @@ def _worker(rank, world, port, out_dir, n, steps, strategy="allgather", mode="au
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK="0", GRAVSIM_RCCL_RANK_HOSTS="1")
     os.environ.update(env or {})
+    if os.environ.get("GRAVSIM_TEST_NCCL_DEBUG"):  # diagnostics: RCCL INFO log per rank
+        os.makedirs(os.environ["GRAVSIM_TEST_NCCL_DEBUG"], exist_ok=True)
+        os.environ.update(NCCL_DEBUG="INFO", NCCL_DEBUG_SUBSYS="INIT,BOOTSTRAP,NET,GRAPH,ENV",
+                          NCCL_DEBUG_TIMESTAMP_FORMAT="%H:%M:%S.%f ",
+                          NCCL_DEBUG_FILE=os.path.join(os.environ["GRAVSIM_TEST_NCCL_DEBUG"],
+                                                       f"w{world}_n{n}_r{rank}.log"))
     import gravsim  # noqa: F401
     from gravsim.config import SimConfig
     from gravsim.parallel import comm
@@ -196,7 +202,7 @@ def test_rccl_one_rank_full_schedule_bitwise(hip, monkeypatch, graph, strategy):
     from gravsim.runtime.engines import HipEngine
 
     monkeypatch.setenv("GRAVSIM_FORCE_COMM", "1")
-    # "sym": the Newton-3 schedule (all-gather, then the group-sum exchange through RCCL);
+    # "sym": the Newton-3 schedule (all-gather, then the node-sum exchange through RCCL);
     # "sym3": the same with the gated local-first launch (graph 2 captures the gate kernels).
     sym = strategy.startswith("sym")
     if strategy == "sym3":
