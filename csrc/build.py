@@ -30,7 +30,8 @@ CPU_SRC = [CSRC / "common" / "layout.cpp", CSRC / "cpu" / "cpu_engine.cpp"]
 HIP_SRC = [CSRC / "common" / "layout.cpp", CSRC / "hip" / "nbody_kernels.hip",
            CSRC / "hip" / "nbody_sym.hip",
            CSRC / "hip" / "nbody_mfma.hip", CSRC / "hip" / "comm_model.hip",
-           CSRC / "hip" / "ipc.hip", CSRC / "hip" / "stepper.hip"]
+           CSRC / "hip" / "ipc.hip", CSRC / "hip" / "stepper.hip",
+           CSRC / "hip" / "stepper_comm.hip", CSRC / "hip" / "stepper_plan.hip"]
 TOOL_SRC = [CSRC / "tools" / "gravsim_main.cpp"]
 
 CPU_LIB = OUT / "libgravsim_cpu.so"

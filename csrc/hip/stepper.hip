@@ -36,187 +36,10 @@
 // Replay: one rank captures two steps (one ping-pong period) as one hipGraph; multi-rank
 // steps replay a segmented plan (compute segments as graphs, collectives eager between them,
 // build_plan); use_graph >= 2 captures the collectives too (opt-in, --graph-comm).
-#include <dlfcn.h>
-#include <execinfo.h>
-#include <hip/hip_runtime.h>
-#include <signal.h>
-#include <unistd.h>
-#include <math.h>
-#include <rccl/rccl.h>
-#include <stdio.h>
-#include <stdlib.h>
-#include <string.h>
+#include "gs_stepper.h"
 
-#include <chrono>
-#include <functional>
-#include <string>
-#include <thread>
-#include <vector>
 
-#include "gravsim.h"
-#include "gs_common.h"
-#include "gs_kernels.h"
-
-void gs_set_error(const char* msg);
-
-#define GS_HIP(call)                                                                \
-  do {                                                                              \
-    hipError_t e_ = (call);                                                         \
-    if (e_ != hipSuccess) {                                                         \
-      char b_[384];                                                                 \
-      snprintf(b_, sizeof(b_), "%s:%d %s: %s", __FILE__, __LINE__, #call,           \
-               hipGetErrorString(e_));                                              \
-      gs_set_error(b_);                                                             \
-      return -1;                                                                    \
-    }                                                                               \
-  } while (0)
-
-#define GS_NCCL(call)                                                               \
-  do {                                                                              \
-    ncclResult_t r_ = (call);                                                       \
-    if (r_ != ncclSuccess) {                                                        \
-      char b_[384];                                                                 \
-      snprintf(b_, sizeof(b_), "%s:%d %s: %s", __FILE__, __LINE__, #call,           \
-               ncclGetErrorString(r_));                                             \
-      gs_set_error(b_);                                                             \
-      return -1;                                                                    \
-    }                                                                               \
-  } while (0)
-
-struct gs_stepper {
-  gs_config cfg;
-  gs_layout L;
-  size_t esz = 4;  // element size
-  hipStream_t s_comp = nullptr, s_comm = nullptr;
-  hipStream_t s_rem = nullptr;  // second compute stream: remote chunks beside the local ones
-  hipStream_t s_rem2 = nullptr;  // third compute stream: ring sub-steps alternate rem/rem2
-  hipEvent_t ev_rem2 = nullptr;
-  std::vector<hipEvent_t> ev_recv;  // ring: per sub-step "slice arrived" events
-  hipEvent_t ev_ready = nullptr, ev_gathered = nullptr, ev_remote = nullptr, ev_fork = nullptr;
-  hipEvent_t ev_t0 = nullptr, ev_local = nullptr, ev_end = nullptr;
-  void* X[2] = {nullptr, nullptr};
-  void* vel = nullptr;
-  void* partial = nullptr;
-  void* acc = nullptr;
-  double* mass_dev = nullptr;
-  unsigned long long* nonfinite = nullptr;
-  std::vector<double> mass_host;
-  int64_t k = 0;  // steps done; current positions live in X[k & 1]
-  bool full[2] = {true, false};
-  ncclComm_t comm = nullptr;
-  bool have_comm = false;
-  bool virt = false;  // member of a virtual-rank group (gather = device copies, gs_group_step)
-  bool emulate = false;  // GRAVSIM_EMULATE_RANK: run one rank's launch shapes, no exchange
-  // sym work beside a pending gather (GRAVSIM_SYM_OVERLAP): 0 none (wait, then one launch),
-  // 1 the diagonal units first on the compute stream, 2 diagonal + rank-local shell units
-  // concurrently with the rest on a second stream.
-  int sym_overlap = 0;
-  hipGraphExec_t graph = nullptr;
-  bool timed = false;  // eager steps record phase events
-  int own_c0 = 0, own_c1 = 0;  // this rank's chunks clipped to [0, n_chunks)
-  bool exact = true;           // hard-cutoff select vs fast core-softened path
-  double eps2 = 0.0;           // r^2 offset used by the kernels
-  int cus = 256;               // compute units
-  int occ[3] = {0, 0, 0};      // split-kernel workgroups per CU by force mode
-  // Newton-3 symmetric schedule (GS_MODE_SYM): partial slots, node sums, geometry.
-  char* sym_Pi = nullptr;  // element type: float or double (esz)
-  char* sym_Pj = nullptr;
-  char* sym_Pd = nullptr;
-  char* sym_S = nullptr;  // node sums by destination rank
-  char* sym_R = nullptr;  // node sums of every rank, global node order (== sym_S, one rank)
-  char* sym_Ti = nullptr;  // per-body i-side totals [3][n_local]
-  char* sym_Bb = nullptr;  // multi-band runs: per-block leaf sums [own blocks][3][bodies]
-  int32_t sym_NC = 0, sym_H = 0, sym_L = 0, sym_S_n = 0, sym_D = 1;
-  int32_t sym_band = 0;  // rows per band (Pi/Pj/Pd hold one band; a multiple of sym_RB)
-  // Row blocks and reduction-tree nodes (gs_sym_nodes): rank q owns blocks
-  // [blk_lo[q], blk_lo[q + 1]) = bodies [rbeg[q], rbeg[q] + rcnt[q]); it sends nn(q) nodes,
-  // the first of them global node nbase[q].
-  int32_t sym_B = 8, sym_RB = 1, sym_NN = 1;
-  int32_t blk_lo[9] = {0};
-  std::vector<int64_t> rbeg, rcnt;
-  std::vector<int32_t> nn, nbase;
-  bool uniform = true;  // every rank owns the same body count (P | B: ncclAllGather)
-  hipEvent_t ev_sym = nullptr;
-  // Per-rank emulation with modeled collectives (GRAVSIM_EMU_COMM_GBPS > 0): every all-gather
-  // and node-sum exchange becomes a comm_model_kernel of the same byte count on s_comm.
-  double emu_gbps = 0.0, emu_lat_us = 15.0;
-  int emu_wgs = 16;
-  void* emu_buf = nullptr;
-  unsigned long long* utrace = nullptr;  // GRAVSIM_UNIT_TRACE: per force workgroup timeline
-  // Dynamic unit fetch of the sym force launch (GRAVSIM_SYM_DYN_CAP; <= 1: static units):
-  // units per workgroup after the first wave, and the first wave's size (resident slots).
-  int dyn_cap = 4;
-  int sym_first_wave = 0;
-  int64_t utrace_main = 0;               // entries of the main launch (deferred ones follow)
-  size_t emu_cap = 0;
-  double clk_khz = 100000.0;  // device wall clock (wall_clock64) rate
-  // Gather gates (sym_overlap 3): [0], [1] gate of X[0] / X[1]; [3] the most units one step
-  // deferred past the gather (since the last phase_stats call). defer: count + unit list.
-  unsigned* gate_buf = nullptr;
-  unsigned* defer = nullptr;
-  int32_t* sym_lf = nullptr;  // units-6 order: unit -> row << 16 | segment (bit 31 remote)
-  // Ring strategy of the sym schedule: P-1 neighbour stages instead of one all-gather; the
-  // gated launch waits per stage (ring_gate[8 * buffer + stage], set after each stage's
-  // receive) and its unit map orders the remote units by stage.
-  bool sym_ring = false;
-  unsigned* ring_gate = nullptr;
-  int gate_probe = 0;         // GRAVSIM_GATE_PROBE (emulation timing probes only)
-  int diag_last = 1;          // GRAVSIM_SYM_DIAG_LAST=0: row-by-row unit order (A/B only)
-  int fuse_tail = -1;         // GRAVSIM_SYM_FUSED_TAIL: -1 by size (<= 256K), 0 off, 1 on
-  int parity = 1;             // GRAVSIM_SYM_PARITY=0: round-1 antipodal rule (A/B only)
-  // Phase timing of eager steps (timed): one event set per step, summed by phase_stats.
-  struct PhaseEv {
-    hipEvent_t t0, end, g0, g1, w0, w1, x0, x1, j0, j1;
-    bool g, w, x, j;
-  };
-  std::vector<PhaseEv> pev;
-  int pev_used = 0;
-  PhaseEv* pe = nullptr;  // the step being enqueued
-  // Progress events (one per enqueued step or graph period) for the bounded wait: its
-  // deadline restarts whenever one more completes, so it bounds progress, not the run.
-  std::vector<hipEvent_t> prog;
-  int64_t prog_rec = 0, prog_done = 0;
-  double step_timeout_s = 0.0;  // 0: unbounded
-  bool graph_failed = false;    // multi-rank capture refused: eager fallback
-  bool work_zero = true;        // sym dynamic unit counter (gate_buf[4]) known to be 0
-  // Work audit of the sym force launches: +1 per unit run (nbody_sym.hip audit_unit); a step
-  // runs rows x (S + D) units on this rank whatever the launch split or fetch order.
-  unsigned long long* audit = nullptr;
-  // Fault injection for the audit's own test (GRAVSIM_FAULT_SKIP_UNITS=k): every dynamic
-  // force launch starts its unit counter at k instead of 0, so units 0 .. k-1 never run,
-  // exactly the failure class of a stale re-armed counter (a memset node when captured).
-  unsigned fault_skip = 0;
-  bool rearm_lastwg = false;  // GRAVSIM_SYM_REARM=lastwg: round 2's in-kernel counter re-arm
-  // GRAVSIM_SYM_FORK_ROW=1 (A/B only): the row reduce on a second stream beside the node
-  // reduce. Measured slower: the two streaming sums contend (reduce phase at 1M 1533-1592 us
-  // per step against 1342-1381 in sequence; profiles/r3_reduce_fork_split_ab.txt).
-  bool fork_row = false;
-  // Segmented step graph of multi-rank runs (use_graph 1): the compute stream's work between
-  // two cross-stream points is captured as one graph segment; the collectives (RCCL, or the
-  // emulation's modeled ones) and the event record/wait that order them against the compute
-  // stream are issued eagerly between the segments on replay. RCCL is never captured, so the
-  // socket-transport capture crash (profiles/r2_graph_comm_root_cause.txt) cannot occur.
-  struct PlanOp {
-    enum Kind { kGraph, kRecord, kWait, kHost } kind;
-    hipGraphExec_t g;
-    hipEvent_t ev;
-    std::function<int()> fn;
-  };
-  std::vector<PlanOp> plan;  // one ping-pong period (two steps)
-  bool rec = false;          // recording a plan: s_comp is capturing a segment
-  int plan_graphs = 0;       // graph segments per period (diagnostics)
-  // Device memory ledger: every HBM buffer the stepper owns, by name (gs_stepper_mem_entry);
-  // destroy frees exactly these. All of them are allocated before the first step, sized from
-  // the layout (the sym bands from the free HBM), so nothing is allocated inside the loop.
-  struct MemEntry {
-    void* p;
-    size_t bytes;
-    const char* tag;
-  };
-  std::vector<MemEntry> mem;
-};
-
-namespace {
+namespace gs::rt {
 
 // Optional roctx ranges (GRAVSIM_ROCTX=1): resolved with dlopen so the library never links a
 // profiler; under `rocprofv3 --marker-trace` the step phases show up on the timeline.
@@ -251,100 +74,9 @@ struct Range {
   }
 };
 
-size_t row_bytes(const gs_stepper* s) { return 4 * s->esz; }
 
-// hipMalloc through the ledger; on failure the error names the buffer, its size and the
-// free HBM (a 16M-body rank needs ~110 GB of partial slots).
-template <typename T>
-int dev_alloc(gs_stepper* s, T** p, size_t bytes, const char* tag) {
-  void* v = nullptr;
-  const hipError_t e = hipMalloc(&v, bytes ? bytes : 16);
-  if (e != hipSuccess) {
-    (void)hipGetLastError();
-    size_t free_b = 0, total_b = 0;
-    (void)hipMemGetInfo(&free_b, &total_b);
-    char b[320];
-    snprintf(b, sizeof(b), "device allocation of %s (%.3f GB) failed: %s (free %.3f of %.3f GB)",
-             tag, bytes / 1e9, hipGetErrorString(e), free_b / 1e9, total_b / 1e9);
-    gs_set_error(b);
-    return -1;
-  }
-  *p = static_cast<T*>(v);
-  s->mem.push_back({v, bytes, tag});
-  return 0;
-}
 
-// ---- compute-stream ordering points (eager, or cut points of a recorded plan) ----------
-// End the open capture segment and keep it as a graph if it holds any node.
-int seg_cut(gs_stepper* s) {
-  hipGraph_t g = nullptr;
-  GS_HIP(hipStreamEndCapture(s->s_comp, &g));
-  size_t nodes = 0;
-  hipError_t e = hipGraphGetNodes(g, nullptr, &nodes);
-  if (e == hipSuccess && nodes > 0) {
-    hipGraphExec_t x = nullptr;
-    e = hipGraphInstantiate(&x, g, nullptr, nullptr, 0);
-    if (e == hipSuccess) {
-      s->plan.push_back({gs_stepper::PlanOp::kGraph, x, nullptr, {}});
-      ++s->plan_graphs;
-    }
-  }
-  (void)hipGraphDestroy(g);
-  GS_HIP(e);
-  return 0;
-}
 
-int seg_open(gs_stepper* s) {
-  GS_HIP(hipStreamBeginCapture(s->s_comp, hipStreamCaptureModeThreadLocal));
-  return 0;
-}
-
-// hipEventRecord(ev, s_comp) for another stream to wait on.
-int comp_record(gs_stepper* s, hipEvent_t ev) {
-  if (!s->rec) {
-    GS_HIP(hipEventRecord(ev, s->s_comp));
-    return 0;
-  }
-  if (seg_cut(s)) return -1;
-  s->plan.push_back({gs_stepper::PlanOp::kRecord, nullptr, ev, {}});
-  return seg_open(s);
-}
-
-// hipStreamWaitEvent(s_comp, ev) on an event another stream records.
-int comp_wait(gs_stepper* s, hipEvent_t ev) {
-  if (!s->rec) {
-    GS_HIP(hipStreamWaitEvent(s->s_comp, ev, 0));
-    return 0;
-  }
-  if (seg_cut(s)) return -1;
-  s->plan.push_back({gs_stepper::PlanOp::kWait, nullptr, ev, {}});
-  return seg_open(s);
-}
-
-// Work on the comm stream (a collective and its event bookkeeping): run now, or replayed
-// eagerly at this point of the plan.
-int comm_do(gs_stepper* s, std::function<int()> fn) {
-  if (!s->rec) return fn();
-  if (seg_cut(s)) return -1;
-  s->plan.push_back({gs_stepper::PlanOp::kHost, nullptr, nullptr, std::move(fn)});
-  return seg_open(s);
-}
-
-void drop_graphs(gs_stepper* s) {
-  if (s->graph) {
-    (void)hipGraphExecDestroy(s->graph);
-    s->graph = nullptr;
-  }
-  for (auto& op : s->plan)
-    if (op.g) (void)hipGraphExecDestroy(op.g);
-  s->plan.clear();
-  s->plan_graphs = 0;
-}
-
-// A multi-rank exchange is active: a real communicator, or the per-rank emulation.
-bool xcomm(const gs_stepper* s) { return s->have_comm || s->emulate; }
-// Remote slices must be brought in before they are read (RCCL, emulation, virtual ranks).
-bool multi(const gs_stepper* s) { return s->have_comm || s->emulate || s->virt; }
 
 // Bytes one rank receives per step: the all-gather's remote slices, and the node sums the
 // other ranks send it (sym schedule).
@@ -355,19 +87,6 @@ size_t exchange_bytes(const gs_stepper* s) {
   return (size_t)(s->sym_NN - s->nn[s->cfg.rank]) * 3 * s->L.n_local * s->esz;
 }
 
-// Emulated collective on s_comm (GRAVSIM_EMU_COMM_GBPS > 0): the byte count moved through HBM
-// by emu_wgs workgroups that stay resident for latency + bytes / rate (comm_model.hip). The
-// kernel copies min(bytes, src_cap, emu_cap) bytes (src_cap: what the source buffer holds);
-// the modeled time always uses the full byte count.
-int comm_model(gs_stepper* s, const void* src, size_t bytes, size_t src_cap) {
-  if (s->emu_gbps <= 0.0 || bytes == 0) return 0;
-  const double us = s->emu_lat_us + (double)bytes / (s->emu_gbps * 1e3);
-  if (bytes > s->emu_cap) bytes = s->emu_cap;  // (sized at create for the larger collective)
-  if (bytes > src_cap) bytes = src_cap;
-  const uint64_t ticks = (uint64_t)(us * s->clk_khz / 1e3);
-  GS_HIP(gs::launch_comm_model(src, s->emu_buf, bytes, ticks, s->emu_wgs, s->s_comm));
-  return 0;
-}
 
 // Phase events of the step being enqueued (timed eager steps; at most 256 per phase_stats).
 gs_stepper::PhaseEv* phase_begin(gs_stepper* s) {
@@ -382,13 +101,6 @@ gs_stepper::PhaseEv* phase_begin(gs_stepper* s) {
   p->g = p->w = p->x = p->j = false;
   return p;
 }
-#define GS_MARK(field, flag, stream)                             \
-  do {                                                           \
-    if (s->pe) {                                                 \
-      GS_HIP(hipEventRecord(s->pe->field, (stream)));            \
-      s->pe->flag = true;                                        \
-    }                                                            \
-  } while (0)
 
 template <typename T>
 gs::KArgs<T> base_args(gs_stepper* s, int cur) {
@@ -414,8 +126,6 @@ gs::KArgs<T> base_args(gs_stepper* s, int cur) {
   return a;
 }
 
-// The sym kernels implement both cutoff paths (fast core and exact select).
-bool use_sym(const gs_stepper* s) { return s->L.mode == GS_MODE_SYM; }
 
 gs::SymArgs sym_args(gs_stepper* s, int cur) {
   gs::SymArgs a;
@@ -475,51 +185,6 @@ gs::SymArgs sym_args(gs_stepper* s, int cur) {
   return a;
 }
 
-// Group-sum exchange of the symmetric schedule: rank r sends S_g(x) of its groups for the
-// bodies of rank q to q (ncclSend/ncclRecv pairs, one group call) and keeps its own block.
-// With join = false the compute stream does not wait for it yet (the caller joins with
-// hipStreamWaitEvent(s_comp, ev_sym) after work that does not read Rbuf).
-int sym_exchange_rccl(gs_stepper* s, bool join = true) {
-  if (comp_record(s, s->ev_ready)) return -1;
-  if (comm_do(s, [s]() -> int {
-        // To rank q: this rank's nn node sums of q's bodies (Sbuf block q); from rank q: its
-        // nn(q) node sums of this rank's bodies, at its global node offset in Rbuf.
-        const int P = s->cfg.nranks, r = s->cfg.rank;
-        const size_t e = s->esz, nl = (size_t)s->L.n_local, my = (size_t)s->nn[r];
-        const ncclDataType_t dt = s->esz == 8 ? ncclFloat64 : ncclFloat32;
-        GS_HIP(hipStreamWaitEvent(s->s_comm, s->ev_ready, 0));
-        GS_MARK(x0, x, s->s_comm);
-        GS_HIP(hipMemcpyAsync(s->sym_R + (size_t)s->nbase[r] * 3 * nl * e,
-                              s->sym_S + my * 3 * (size_t)s->rbeg[r] * e, my * 3 * nl * e,
-                              hipMemcpyDeviceToDevice, s->s_comm));
-        if (s->emulate) {
-          // (the bytes this rank receives, read from its receive buffer: NN x 3 per own body)
-          if (comm_model(s, s->sym_R, exchange_bytes(s),
-                         (size_t)s->sym_NN * 3 * (size_t)s->L.n_local * s->esz))
-            return -1;
-        } else if (P > 1) {
-          GS_NCCL(ncclGroupStart());
-          for (int q = 0; q < P; ++q) {
-            if (q == r) continue;
-            GS_NCCL(ncclSend(s->sym_S + my * 3 * (size_t)s->rbeg[q] * e, my * 3 * s->rcnt[q], dt,
-                             q, s->comm, s->s_comm));
-            GS_NCCL(ncclRecv(s->sym_R + (size_t)s->nbase[q] * 3 * nl * e, (size_t)s->nn[q] * 3 * nl,
-                             dt, q, s->comm, s->s_comm));
-          }
-          GS_NCCL(ncclGroupEnd());
-        }
-        GS_MARK(x1, x, s->s_comm);
-        GS_HIP(hipEventRecord(s->ev_sym, s->s_comm));
-        return 0;
-      }))
-    return -1;
-  if (join) {
-    GS_MARK(j0, j, s->s_comp);
-    if (comp_wait(s, s->ev_sym)) return -1;
-    GS_MARK(j1, j, s->s_comp);
-  }
-  return 0;
-}
 
 int ensure_sym(gs_stepper* s) {
   if (s->L.mode != GS_MODE_SYM || s->sym_Pi) return 0;
@@ -640,106 +305,6 @@ int choose_groups(gs_stepper* s, int span, bool phi, bool concurrent = false) {
   return best;
 }
 
-int ring_xfer_rccl(gs_stepper* s, int cur, int sub);
-int ring_src(const gs_stepper* s, int sub);
-
-// Bodies [*b0, *b0 + *cnt) of rank q's slice: the sym schedule's row blocks (uneven when P
-// does not divide the block count), else equal slices.
-void rank_slice(const gs_stepper* s, int q, int64_t* b0, int64_t* cnt) {
-  if (!s->rbeg.empty()) {
-    *b0 = s->rbeg[q];
-    *cnt = s->rcnt[q];
-  } else {
-    *b0 = (int64_t)q * s->L.n_local;
-    *cnt = s->L.n_local;
-  }
-}
-
-// In-place all-gather of X[cur] on s_comm (ev_gathered marks completion). With `gate` the
-// comm stream also publishes completion to a force launch already running (units 6). The sym
-// schedule's ring strategy moves the slices in P-1 neighbour stages instead and, gated,
-// publishes each stage as it lands (ring_gate[8 * cur + k]), so the units that read only
-// slices already received can start.
-int gather(gs_stepper* s, int cur, bool gate = false) {
-  if (!xcomm(s) || s->full[cur]) return 0;
-  if (comp_record(s, s->ev_ready)) return -1;
-  s->full[cur] = true;
-  return comm_do(s, [s, cur, gate]() -> int {
-    char* buf = static_cast<char*>(s->X[cur]);
-    const size_t count = (size_t)s->L.n_local * 4;
-    GS_HIP(hipStreamWaitEvent(s->s_comm, s->ev_ready, 0));
-    GS_MARK(g0, g, s->s_comm);
-    const ncclDataType_t dt = s->esz == 4 ? ncclFloat32 : ncclFloat64;
-    if (s->sym_ring && use_sym(s)) {
-      for (int k = 1; k < s->cfg.nranks; ++k) {
-        if (s->emulate) {
-          const size_t sl = (size_t)s->rcnt[ring_src(s, k)] * row_bytes(s);
-          if (comm_model(s, buf, sl, (size_t)s->L.n_pad * row_bytes(s))) return -1;
-        } else if (ring_xfer_rccl(s, cur, k)) {
-          return -1;
-        }
-        if (gate) GS_HIP(gs::launch_gate_set(s->ring_gate + 8 * cur + k, s->s_comm));
-      }
-    } else if (s->emulate) {
-      if (comm_model(s, buf, gather_bytes(s), (size_t)s->L.n_pad * row_bytes(s))) return -1;
-    } else if (!use_sym(s) || s->uniform) {
-      GS_NCCL(ncclAllGather(buf + (size_t)s->L.local_begin * row_bytes(s), buf, count, dt,
-                            s->comm, s->s_comm));
-    } else {
-      // Uneven row blocks (P not dividing the block count): every rank broadcasts its own
-      // slice in place, all P in one group call (the Allgatherv of mpi.c:227-231).
-      GS_NCCL(ncclGroupStart());
-      for (int q = 0; q < s->cfg.nranks; ++q) {
-        char* sl = buf + (size_t)s->rbeg[q] * row_bytes(s);
-        GS_NCCL(ncclBroadcast(sl, sl, (size_t)s->rcnt[q] * 4, dt, q, s->comm, s->s_comm));
-      }
-      GS_NCCL(ncclGroupEnd());
-    }
-    GS_MARK(g1, g, s->s_comm);
-    if (gate && !(s->sym_ring && use_sym(s)))
-      GS_HIP(gs::launch_gate_set(s->gate_buf + cur, s->s_comm));
-    GS_HIP(hipEventRecord(s->ev_gathered, s->s_comm));
-    return 0;
-  });
-}
-
-// ---- ring pass (strategy 1) ------------------------------------------------------------
-// Rank r computes its own chunks first (sub-step 0), then at sub-step s the slice of rank
-// (r - s) mod P, which arrives from the left neighbour while sub-step s-1 computes; it is
-// forwarded to the right neighbour in the next sub-step. Each slice lands at its own offset
-// of X[cur], so no buffer is reused within a step; per-chunk partials + the canonical reduce
-// keep the result bit-identical to the all-gather schedule.
-int ring_src(const gs_stepper* s, int sub) {
-  const int P = s->cfg.nranks;
-  return ((s->cfg.rank - sub) % P + P) % P;
-}
-
-void rank_chunks(const gs_stepper* s, int src, int* c0, int* c1) {
-  const int64_t per = s->L.n_local / s->L.chunk;
-  int64_t a = (int64_t)src * per, b = a + per;
-  if (a > s->L.n_chunks) a = s->L.n_chunks;
-  if (b > s->L.n_chunks) b = s->L.n_chunks;
-  *c0 = (int)a;
-  *c1 = (int)b;
-}
-
-// Enqueue the transfer of ring sub-step `sub` (1..P-1) on the comm stream: send the slice
-// received at sub-step sub-1 (own slice for sub = 1) right, receive slice ring_src(sub) left.
-int ring_xfer_rccl(gs_stepper* s, int cur, int sub) {
-  const int P = s->cfg.nranks, r = s->cfg.rank;
-  char* buf = static_cast<char*>(s->X[cur]);
-  const ncclDataType_t dt = s->esz == 4 ? ncclFloat32 : ncclFloat64;
-  int64_t sb, sc, rb, rc;
-  rank_slice(s, ring_src(s, sub - 1), &sb, &sc);
-  rank_slice(s, ring_src(s, sub), &rb, &rc);
-  GS_NCCL(ncclGroupStart());
-  GS_NCCL(ncclSend(buf + (size_t)sb * row_bytes(s), (size_t)sc * 4, dt, (r + 1) % P, s->comm,
-                   s->s_comm));
-  GS_NCCL(ncclRecv(buf + (size_t)rb * row_bytes(s), (size_t)rc * 4, dt, (r - 1 + P) % P, s->comm,
-                   s->s_comm));
-  GS_NCCL(ncclGroupEnd());
-  return 0;
-}
 
 template <typename T>
 int ring_compute(gs_stepper* s, const gs::KArgs<T>& a, int sub, hipEvent_t ready) {
@@ -1026,80 +591,11 @@ int enqueue_step(gs_stepper* s, bool capturing, bool gathered_externally) {
   return 0;
 }
 
-int enqueue_step_any(gs_stepper* s, bool capturing, bool gathered_externally = false) {
+int enqueue_step_any(gs_stepper* s, bool capturing, bool gathered_externally) {
   return s->esz == 4 ? enqueue_step<float>(s, capturing, gathered_externally)
                      : enqueue_step<double>(s, capturing, gathered_externally);
 }
 
-int build_graph(gs_stepper* s) {
-  // One ping-pong period (two steps) starting from an even step with a gathered buffer.
-  const int64_t k0 = s->k;
-  const bool f0 = s->full[0], f1 = s->full[1];
-  hipGraph_t g = nullptr;
-  // A replayed graph cannot rely on the counter state at capture time: its first sym force
-  // launch always re-zeroes the unit counter (a later one may skip it after a fused tail
-  // inside the graph; the flag left by the capture then matches every replay's end state).
-  s->work_zero = false;
-  GS_HIP(hipStreamBeginCapture(s->s_comp, hipStreamCaptureModeThreadLocal));
-  int rc = enqueue_step_any(s, true);
-  if (rc == 0) rc = enqueue_step_any(s, true);
-  hipError_t e = hipStreamEndCapture(s->s_comp, &g);
-  s->k = k0;
-  s->full[0] = f0;
-  s->full[1] = f1;
-  if (rc) return rc;
-  GS_HIP(e);
-  GS_HIP(hipGraphInstantiate(&s->graph, g, nullptr, nullptr, 0));
-  GS_HIP(hipGraphDestroy(g));
-  return 0;
-}
-
-// Multi-rank steps whose cross-stream points all go through comp_record / comp_wait /
-// comm_do: the sym schedule except overlap 2 (a second compute stream forked per step).
-bool plan_ok(const gs_stepper* s) {
-  return xcomm(s) && use_sym(s) && s->sym_overlap != 2 && s->cfg.use_graph == 1 && !s->timed;
-}
-
-// Record one ping-pong period (two steps, from an even step whose buffer needs its gather)
-// as a plan: compute segments captured on s_comp, the collectives kept as eager host ops.
-int build_plan(gs_stepper* s) {
-  const int64_t k0 = s->k;
-  const bool f0 = s->full[0], f1 = s->full[1];
-  drop_graphs(s);
-  s->work_zero = false;  // (as build_graph: a replay re-zeroes the dynamic unit counter)
-  if (seg_open(s)) return -1;
-  s->rec = true;
-  int rc = enqueue_step_any(s, true);
-  if (rc == 0) rc = enqueue_step_any(s, true);
-  s->rec = false;
-  const int cut = rc == 0 ? seg_cut(s) : 0;
-  if (rc != 0) {  // abandon the open capture
-    hipGraph_t g = nullptr;
-    if (hipStreamEndCapture(s->s_comp, &g) == hipSuccess && g) (void)hipGraphDestroy(g);
-  }
-  s->k = k0;
-  s->full[0] = f0;
-  s->full[1] = f1;
-  if (rc || cut) {
-    drop_graphs(s);
-    return -1;
-  }
-  return 0;
-}
-
-int run_plan(gs_stepper* s) {
-  for (auto& op : s->plan) {
-    switch (op.kind) {
-      case gs_stepper::PlanOp::kGraph: GS_HIP(hipGraphLaunch(op.g, s->s_comp)); break;
-      case gs_stepper::PlanOp::kRecord: GS_HIP(hipEventRecord(op.ev, s->s_comp)); break;
-      case gs_stepper::PlanOp::kWait: GS_HIP(hipStreamWaitEvent(s->s_comp, op.ev, 0)); break;
-      case gs_stepper::PlanOp::kHost:
-        if (op.fn()) return -1;
-        break;
-    }
-  }
-  return 0;
-}
 
 template <typename T>
 int upload_state(gs_stepper* s, const double* pos, const double* vel, const double* mass) {
@@ -1216,76 +712,10 @@ int accel_impl(gs_stepper* s, double* acc4, bool step_path) {
   return 0;
 }
 
-// Wait until progress event `target` - 1 has completed (target == prog_rec: every stream is
-// idle). The deadline restarts whenever one more progress event completes.
-int wait_until(gs_stepper* s, int64_t target, double timeout_s) {
-  const int64_t R = (int64_t)s->prog.size();
-  const bool all = target >= s->prog_rec;
-  auto last = std::chrono::steady_clock::now();
-  for (;;) {
-    while (s->prog_done < s->prog_rec) {
-      const hipError_t q = hipEventQuery(s->prog[s->prog_done % R]);
-      if (q == hipErrorNotReady) break;
-      if (q != hipSuccess) {
-        char m[256];
-        snprintf(m, sizeof(m), "stream error: %s", hipGetErrorString(q));
-        gs_set_error(m);
-        return -1;
-      }
-      ++s->prog_done;
-      last = std::chrono::steady_clock::now();
-    }
-    bool done = s->prog_done >= target;
-    if (all) {
-      hipError_t a = hipStreamQuery(s->s_comp);
-      if (a == hipSuccess) a = hipStreamQuery(s->s_rem);
-      if (a == hipSuccess) a = hipStreamQuery(s->s_rem2);
-      const hipError_t b = hipStreamQuery(s->s_comm);
-      if ((a != hipSuccess && a != hipErrorNotReady) || (b != hipSuccess && b != hipErrorNotReady)) {
-        char m[256];
-        snprintf(m, sizeof(m), "stream error: %s / %s", hipGetErrorString(a), hipGetErrorString(b));
-        gs_set_error(m);
-        return -1;
-      }
-      done = a == hipSuccess && b == hipSuccess;
-    }
-    if (done) {
-      if (all) s->prog_done = s->prog_rec;
-      return 0;
-    }
-    if (s->have_comm && gs_stepper_comm_check(s)) return -1;
-    const double el =
-        std::chrono::duration<double>(std::chrono::steady_clock::now() - last).count();
-    if (timeout_s > 0 && el > timeout_s) {
-      char m[256];
-      snprintf(m, sizeof(m),
-               "step timeout: no step completed for %.1f s (rank %d, step %lld of %lld "
-               "enqueued); communicator aborted",
-               el, s->cfg.rank, (long long)s->prog_done, (long long)s->prog_rec);
-      if (s->have_comm) {
-        (void)ncclCommAbort(s->comm);
-        s->have_comm = false;
-      }
-      gs_set_error(m);
-      return -1;
-    }
-    std::this_thread::sleep_for(std::chrono::microseconds(200));
-  }
-}
 
-// One progress event per enqueued step / graph period. At most prog.size() are outstanding:
-// past that the host waits (bounded by step_timeout_s) for the oldest before enqueuing more.
-int note_progress(gs_stepper* s) {
-  const int64_t R = (int64_t)s->prog.size();
-  if (R == 0) return 0;
-  if (s->prog_rec - s->prog_done >= R && wait_until(s, s->prog_rec - R + 1, s->step_timeout_s))
-    return -1;
-  GS_HIP(hipEventRecord(s->prog[s->prog_rec % R], s->s_comp));
-  ++s->prog_rec;
-  return 0;
-}
+}  // namespace gs::rt
 
-}  // namespace
+using namespace gs::rt;
 
 extern "C" {
 
@@ -1907,135 +1337,6 @@ int gs_group_step(gs_stepper** sh, int32_t P, int32_t nsteps) {
   return 0;
 }
 
-int gs_rccl_unique_id(void* out128) {
-  ncclUniqueId id;
-  GS_NCCL(ncclGetUniqueId(&id));
-  static_assert(sizeof(id) == 128, "unexpected ncclUniqueId size");
-  memcpy(out128, &id, sizeof(id));
-  return 0;
-}
 
 }  // extern "C"
 
-namespace {
-// GRAVSIM_CRASH_TRACE=1: a fatal signal in any thread of a rank (ours, HIP's or RCCL's
-// proxy/socket threads) prints that thread's native stack to stderr before the default
-// action runs. Host-side diagnosis only; it was added to locate the multi-process
-// graph-capture crash over RCCL sockets (profiles/r2_graph_comm_multiprocess.txt).
-constexpr int kTraceSigs[] = {SIGSEGV, SIGBUS, SIGFPE, SIGILL, SIGABRT};
-struct sigaction g_prev_action[sizeof(kTraceSigs) / sizeof(int)];
-
-void crash_trace_handler(int sig, siginfo_t* info, void*) {
-  char head[160];
-  const int len = snprintf(head, sizeof(head),
-                           "gravsim: signal %d (addr %p) in pid %d tid %ld, native stack:\n", sig,
-                           info ? info->si_addr : nullptr, (int)getpid(), (long)gettid());
-  if (len > 0) (void)!write(2, head, (size_t)len);
-  // Deep enough for a runaway recursion: print the innermost 8 and the outermost 40 frames.
-  static void* frames[1 << 18];
-  const int n = backtrace(frames, 1 << 18);
-  if (n <= 48) {
-    backtrace_symbols_fd(frames, n, 2);
-  } else {
-    backtrace_symbols_fd(frames, 8, 2);
-    const int skipped = snprintf(head, sizeof(head), "  ... %d frames ...\n", n - 48);
-    if (skipped > 0) (void)!write(2, head, (size_t)skipped);
-    backtrace_symbols_fd(frames + n - 40, 40, 2);
-  }
-  // Chain to whatever was installed before (Python's faulthandler prints every thread's
-  // Python stack), then the default action.
-  for (size_t k = 0; k < sizeof(kTraceSigs) / sizeof(int); ++k)
-    if (kTraceSigs[k] == sig) sigaction(sig, &g_prev_action[k], nullptr);
-  raise(sig);
-}
-
-void maybe_install_crash_trace() {
-  static bool done = false;
-  if (done || !getenv("GRAVSIM_CRASH_TRACE")) return;
-  done = true;
-  void* warm[1];
-  (void)backtrace(warm, 1);  // loads libgcc's unwinder now, not inside the handler
-  struct sigaction sa;
-  memset(&sa, 0, sizeof(sa));
-  sa.sa_sigaction = crash_trace_handler;
-  sa.sa_flags = SA_SIGINFO | SA_RESETHAND | SA_ONSTACK;
-  // An alternate stack for this (the host's main) thread, so a stack overflow still reports.
-  static char alt[1 << 16];
-  stack_t ss;
-  memset(&ss, 0, sizeof(ss));
-  ss.ss_sp = alt;
-  ss.ss_size = sizeof(alt);
-  (void)sigaltstack(&ss, nullptr);
-  sigemptyset(&sa.sa_mask);
-  for (size_t k = 0; k < sizeof(kTraceSigs) / sizeof(int); ++k)
-    sigaction(kTraceSigs[k], &sa, &g_prev_action[k]);
-}
-}  // namespace
-
-extern "C" {
-
-int gs_stepper_comm_init(gs_stepper* s, const void* id128, int32_t rank, int32_t nranks) {
-  maybe_install_crash_trace();
-  if (rank != s->cfg.rank || nranks != s->cfg.nranks) {
-    gs_set_error("comm_init: rank/nranks differ from the stepper's layout");
-    return -1;
-  }
-  GS_HIP(hipSetDevice(s->cfg.device));
-  ncclUniqueId id;
-  memcpy(&id, id128, sizeof(id));
-  // The one-sided multi-rank schedule is always split (the sym schedule has its own slots).
-  if (s->L.mode != GS_MODE_SYM && ensure_partial(s)) return -1;
-  GS_NCCL(ncclCommInitRank(&s->comm, nranks, id, rank));
-  // GRAVSIM_FORCE_COMM keeps a 1-rank communicator live so the full multi-rank schedule
-  // (in-place ncclAllGather, local/remote split on two streams, events) runs on one GPU.
-  s->have_comm = nranks > 1 || getenv("GRAVSIM_FORCE_COMM") != nullptr;
-  if (!s->have_comm) {
-    (void)ncclCommDestroy(s->comm);
-    s->comm = nullptr;
-  }
-  drop_graphs(s);
-  if (s->have_comm) {
-    // Warm-up: RCCL builds its transports lazily on the first collective and on the first
-    // send/recv to each peer. Do both here on scratch memory (the accel buffer holds
-    // n_local * 4 >= P elements) so that no timed or captured step pays for it.
-    char* buf = static_cast<char*>(s->acc);
-    const ncclDataType_t dt = s->esz == 4 ? ncclFloat32 : ncclFloat64;
-    GS_NCCL(ncclAllGather(buf + (size_t)rank * s->esz, buf, 1, dt, s->comm, s->s_comm));
-    if (nranks > 1 && s->cfg.strategy == GS_STRATEGY_RING) {
-      GS_NCCL(ncclGroupStart());
-      GS_NCCL(ncclSend(buf, 1, dt, (rank + 1) % nranks, s->comm, s->s_comm));
-      GS_NCCL(ncclRecv(buf + (size_t)nranks * s->esz, 1, dt, (rank - 1 + nranks) % nranks,
-                       s->comm, s->s_comm));
-      GS_NCCL(ncclGroupEnd());
-    }
-    if (nranks > 1 && s->L.mode == GS_MODE_SYM) {
-      // The sym schedule's node-sum exchange talks to every peer: connect them all now.
-      GS_NCCL(ncclGroupStart());
-      for (int q = 0; q < nranks; ++q) {
-        if (q == rank) continue;
-        GS_NCCL(ncclSend(buf + (size_t)q * s->esz, 1, dt, q, s->comm, s->s_comm));
-        GS_NCCL(ncclRecv(buf + (size_t)(nranks + q) * s->esz, 1, dt, q, s->comm, s->s_comm));
-      }
-      GS_NCCL(ncclGroupEnd());
-    }
-    GS_HIP(hipStreamSynchronize(s->s_comm));
-  }
-  return 0;
-}
-
-int gs_stepper_comm_check(gs_stepper* s) {
-  if (!s->have_comm) return 0;
-  ncclResult_t async = ncclSuccess;
-  GS_NCCL(ncclCommGetAsyncError(s->comm, &async));
-  if (async != ncclSuccess && async != ncclInProgress) {
-    char b[256];
-    snprintf(b, sizeof(b), "RCCL async error: %s; communicator aborted", ncclGetErrorString(async));
-    (void)ncclCommAbort(s->comm);
-    s->have_comm = false;
-    gs_set_error(b);
-    return -1;
-  }
-  return 0;
-}
-
-}  // extern "C"

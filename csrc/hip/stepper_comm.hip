@@ -1,0 +1,311 @@
+// Collectives of the native Stepper: the per-step all-gather of positions (in-place
+// ncclAllGather, or a group of in-place ncclBroadcasts for uneven slices), the ring pass,
+// the sym schedule's node-sum exchange, the per-rank emulation's modeled collectives, and
+// the RCCL communicator's bootstrap, warm-up and failure checks.
+//
+// Reference parity:
+//   mpi.c:142-182  MPI_Init / Bcast / Type_create_struct -> ncclCommInitRank from a 128-byte
+//                  unique id (the launcher broadcasts it over the gloo control plane)
+//   mpi.c:227-236  MPI_Allgatherv (aliased buffers) + MPI_Barrier every step -> gather():
+//                  in place on the comm stream, ordered by events, no barrier
+#include "gs_stepper.h"
+
+namespace gs::rt {
+
+// Emulated collective on s_comm (GRAVSIM_EMU_COMM_GBPS > 0): the byte count moved through HBM
+// by emu_wgs workgroups that stay resident for latency + bytes / rate (comm_model.hip). The
+// kernel copies min(bytes, src_cap, emu_cap) bytes (src_cap: what the source buffer holds);
+// the modeled time always uses the full byte count.
+int comm_model(gs_stepper* s, const void* src, size_t bytes, size_t src_cap) {
+  if (s->emu_gbps <= 0.0 || bytes == 0) return 0;
+  const double us = s->emu_lat_us + (double)bytes / (s->emu_gbps * 1e3);
+  if (bytes > s->emu_cap) bytes = s->emu_cap;  // (sized at create for the larger collective)
+  if (bytes > src_cap) bytes = src_cap;
+  const uint64_t ticks = (uint64_t)(us * s->clk_khz / 1e3);
+  GS_HIP(gs::launch_comm_model(src, s->emu_buf, bytes, ticks, s->emu_wgs, s->s_comm));
+  return 0;
+}
+
+// Bodies [*b0, *b0 + *cnt) of rank q's slice: the sym schedule's row blocks (uneven when P
+// does not divide the block count), else equal slices.
+void rank_slice(const gs_stepper* s, int q, int64_t* b0, int64_t* cnt) {
+  if (!s->rbeg.empty()) {
+    *b0 = s->rbeg[q];
+    *cnt = s->rcnt[q];
+  } else {
+    *b0 = (int64_t)q * s->L.n_local;
+    *cnt = s->L.n_local;
+  }
+}
+
+// In-place all-gather of X[cur] on s_comm (ev_gathered marks completion). With `gate` the
+// comm stream also publishes completion to a force launch already running (units 6). The sym
+// schedule's ring strategy moves the slices in P-1 neighbour stages instead and, gated,
+// publishes each stage as it lands (ring_gate[8 * cur + k]), so the units that read only
+// slices already received can start.
+int gather(gs_stepper* s, int cur, bool gate) {
+  if (!xcomm(s) || s->full[cur]) return 0;
+  if (comp_record(s, s->ev_ready)) return -1;
+  s->full[cur] = true;
+  return comm_do(s, [s, cur, gate]() -> int {
+    char* buf = static_cast<char*>(s->X[cur]);
+    const size_t count = (size_t)s->L.n_local * 4;
+    GS_HIP(hipStreamWaitEvent(s->s_comm, s->ev_ready, 0));
+    GS_MARK(g0, g, s->s_comm);
+    const ncclDataType_t dt = s->esz == 4 ? ncclFloat32 : ncclFloat64;
+    if (s->sym_ring && use_sym(s)) {
+      for (int k = 1; k < s->cfg.nranks; ++k) {
+        if (s->emulate) {
+          const size_t sl = (size_t)s->rcnt[ring_src(s, k)] * row_bytes(s);
+          if (comm_model(s, buf, sl, (size_t)s->L.n_pad * row_bytes(s))) return -1;
+        } else if (ring_xfer_rccl(s, cur, k)) {
+          return -1;
+        }
+        if (gate) GS_HIP(gs::launch_gate_set(s->ring_gate + 8 * cur + k, s->s_comm));
+      }
+    } else if (s->emulate) {
+      if (comm_model(s, buf, gather_bytes(s), (size_t)s->L.n_pad * row_bytes(s))) return -1;
+    } else if (!use_sym(s) || s->uniform) {
+      GS_NCCL(ncclAllGather(buf + (size_t)s->L.local_begin * row_bytes(s), buf, count, dt,
+                            s->comm, s->s_comm));
+    } else {
+      // Uneven row blocks (P not dividing the block count): every rank broadcasts its own
+      // slice in place, all P in one group call (the Allgatherv of mpi.c:227-231).
+      GS_NCCL(ncclGroupStart());
+      for (int q = 0; q < s->cfg.nranks; ++q) {
+        char* sl = buf + (size_t)s->rbeg[q] * row_bytes(s);
+        GS_NCCL(ncclBroadcast(sl, sl, (size_t)s->rcnt[q] * 4, dt, q, s->comm, s->s_comm));
+      }
+      GS_NCCL(ncclGroupEnd());
+    }
+    GS_MARK(g1, g, s->s_comm);
+    if (gate && !(s->sym_ring && use_sym(s)))
+      GS_HIP(gs::launch_gate_set(s->gate_buf + cur, s->s_comm));
+    GS_HIP(hipEventRecord(s->ev_gathered, s->s_comm));
+    return 0;
+  });
+}
+
+// ---- ring pass (strategy 1) ------------------------------------------------------------
+// Rank r computes its own chunks first (sub-step 0), then at sub-step s the slice of rank
+// (r - s) mod P, which arrives from the left neighbour while sub-step s-1 computes; it is
+// forwarded to the right neighbour in the next sub-step. Each slice lands at its own offset
+// of X[cur], so no buffer is reused within a step; per-chunk partials + the canonical reduce
+// keep the result bit-identical to the all-gather schedule.
+int ring_src(const gs_stepper* s, int sub) {
+  const int P = s->cfg.nranks;
+  return ((s->cfg.rank - sub) % P + P) % P;
+}
+
+void rank_chunks(const gs_stepper* s, int src, int* c0, int* c1) {
+  const int64_t per = s->L.n_local / s->L.chunk;
+  int64_t a = (int64_t)src * per, b = a + per;
+  if (a > s->L.n_chunks) a = s->L.n_chunks;
+  if (b > s->L.n_chunks) b = s->L.n_chunks;
+  *c0 = (int)a;
+  *c1 = (int)b;
+}
+
+// Enqueue the transfer of ring sub-step `sub` (1..P-1) on the comm stream: send the slice
+// received at sub-step sub-1 (own slice for sub = 1) right, receive slice ring_src(sub) left.
+int ring_xfer_rccl(gs_stepper* s, int cur, int sub) {
+  const int P = s->cfg.nranks, r = s->cfg.rank;
+  char* buf = static_cast<char*>(s->X[cur]);
+  const ncclDataType_t dt = s->esz == 4 ? ncclFloat32 : ncclFloat64;
+  int64_t sb, sc, rb, rc;
+  rank_slice(s, ring_src(s, sub - 1), &sb, &sc);
+  rank_slice(s, ring_src(s, sub), &rb, &rc);
+  GS_NCCL(ncclGroupStart());
+  GS_NCCL(ncclSend(buf + (size_t)sb * row_bytes(s), (size_t)sc * 4, dt, (r + 1) % P, s->comm,
+                   s->s_comm));
+  GS_NCCL(ncclRecv(buf + (size_t)rb * row_bytes(s), (size_t)rc * 4, dt, (r - 1 + P) % P, s->comm,
+                   s->s_comm));
+  GS_NCCL(ncclGroupEnd());
+  return 0;
+}
+
+// Node-sum exchange of the symmetric schedule: rank r sends the sums of its reduction-tree
+// nodes for the bodies of rank q to q (ncclSend/ncclRecv pairs, one group call) and keeps
+// its own block.
+// With join = false the compute stream does not wait for it yet (the caller joins with
+// hipStreamWaitEvent(s_comp, ev_sym) after work that does not read Rbuf).
+int sym_exchange_rccl(gs_stepper* s, bool join) {
+  if (comp_record(s, s->ev_ready)) return -1;
+  if (comm_do(s, [s]() -> int {
+        // To rank q: this rank's nn node sums of q's bodies (Sbuf block q); from rank q: its
+        // nn(q) node sums of this rank's bodies, at its global node offset in Rbuf.
+        const int P = s->cfg.nranks, r = s->cfg.rank;
+        const size_t e = s->esz, nl = (size_t)s->L.n_local, my = (size_t)s->nn[r];
+        const ncclDataType_t dt = s->esz == 8 ? ncclFloat64 : ncclFloat32;
+        GS_HIP(hipStreamWaitEvent(s->s_comm, s->ev_ready, 0));
+        GS_MARK(x0, x, s->s_comm);
+        GS_HIP(hipMemcpyAsync(s->sym_R + (size_t)s->nbase[r] * 3 * nl * e,
+                              s->sym_S + my * 3 * (size_t)s->rbeg[r] * e, my * 3 * nl * e,
+                              hipMemcpyDeviceToDevice, s->s_comm));
+        if (s->emulate) {
+          // (the bytes this rank receives, read from its receive buffer: NN x 3 per own body)
+          if (comm_model(s, s->sym_R, exchange_bytes(s),
+                         (size_t)s->sym_NN * 3 * (size_t)s->L.n_local * s->esz))
+            return -1;
+        } else if (P > 1) {
+          GS_NCCL(ncclGroupStart());
+          for (int q = 0; q < P; ++q) {
+            if (q == r) continue;
+            GS_NCCL(ncclSend(s->sym_S + my * 3 * (size_t)s->rbeg[q] * e, my * 3 * s->rcnt[q], dt,
+                             q, s->comm, s->s_comm));
+            GS_NCCL(ncclRecv(s->sym_R + (size_t)s->nbase[q] * 3 * nl * e, (size_t)s->nn[q] * 3 * nl,
+                             dt, q, s->comm, s->s_comm));
+          }
+          GS_NCCL(ncclGroupEnd());
+        }
+        GS_MARK(x1, x, s->s_comm);
+        GS_HIP(hipEventRecord(s->ev_sym, s->s_comm));
+        return 0;
+      }))
+    return -1;
+  if (join) {
+    GS_MARK(j0, j, s->s_comp);
+    if (comp_wait(s, s->ev_sym)) return -1;
+    GS_MARK(j1, j, s->s_comp);
+  }
+  return 0;
+}
+
+}  // namespace gs::rt
+
+extern "C" {
+
+int gs_rccl_unique_id(void* out128) {
+  ncclUniqueId id;
+  GS_NCCL(ncclGetUniqueId(&id));
+  static_assert(sizeof(id) == 128, "unexpected ncclUniqueId size");
+  memcpy(out128, &id, sizeof(id));
+  return 0;
+}
+
+}  // extern "C"
+
+namespace gs::rt {
+// GRAVSIM_CRASH_TRACE=1: a fatal signal in any thread of a rank (ours, HIP's or RCCL's
+// proxy/socket threads) prints that thread's native stack to stderr before the default
+// action runs. Host-side diagnosis only; it was added to locate the multi-process
+// graph-capture crash over RCCL sockets (profiles/r2_graph_comm_multiprocess.txt).
+constexpr int kTraceSigs[] = {SIGSEGV, SIGBUS, SIGFPE, SIGILL, SIGABRT};
+struct sigaction g_prev_action[sizeof(kTraceSigs) / sizeof(int)];
+
+void crash_trace_handler(int sig, siginfo_t* info, void*) {
+  char head[160];
+  const int len = snprintf(head, sizeof(head),
+                           "gravsim: signal %d (addr %p) in pid %d tid %ld, native stack:\n", sig,
+                           info ? info->si_addr : nullptr, (int)getpid(), (long)gettid());
+  if (len > 0) (void)!write(2, head, (size_t)len);
+  // Deep enough for a runaway recursion: print the innermost 8 and the outermost 40 frames.
+  static void* frames[1 << 18];
+  const int n = backtrace(frames, 1 << 18);
+  if (n <= 48) {
+    backtrace_symbols_fd(frames, n, 2);
+  } else {
+    backtrace_symbols_fd(frames, 8, 2);
+    const int skipped = snprintf(head, sizeof(head), "  ... %d frames ...\n", n - 48);
+    if (skipped > 0) (void)!write(2, head, (size_t)skipped);
+    backtrace_symbols_fd(frames + n - 40, 40, 2);
+  }
+  // Chain to whatever was installed before (Python's faulthandler prints every thread's
+  // Python stack), then the default action.
+  for (size_t k = 0; k < sizeof(kTraceSigs) / sizeof(int); ++k)
+    if (kTraceSigs[k] == sig) sigaction(sig, &g_prev_action[k], nullptr);
+  raise(sig);
+}
+
+void maybe_install_crash_trace() {
+  static bool done = false;
+  if (done || !getenv("GRAVSIM_CRASH_TRACE")) return;
+  done = true;
+  void* warm[1];
+  (void)backtrace(warm, 1);  // loads libgcc's unwinder now, not inside the handler
+  struct sigaction sa;
+  memset(&sa, 0, sizeof(sa));
+  sa.sa_sigaction = crash_trace_handler;
+  sa.sa_flags = SA_SIGINFO | SA_RESETHAND | SA_ONSTACK;
+  // An alternate stack for this (the host's main) thread, so a stack overflow still reports.
+  static char alt[1 << 16];
+  stack_t ss;
+  memset(&ss, 0, sizeof(ss));
+  ss.ss_sp = alt;
+  ss.ss_size = sizeof(alt);
+  (void)sigaltstack(&ss, nullptr);
+  sigemptyset(&sa.sa_mask);
+  for (size_t k = 0; k < sizeof(kTraceSigs) / sizeof(int); ++k)
+    sigaction(kTraceSigs[k], &sa, &g_prev_action[k]);
+}
+}  // namespace gs::rt
+
+using namespace gs::rt;
+
+extern "C" {
+
+int gs_stepper_comm_init(gs_stepper* s, const void* id128, int32_t rank, int32_t nranks) {
+  maybe_install_crash_trace();
+  if (rank != s->cfg.rank || nranks != s->cfg.nranks) {
+    gs_set_error("comm_init: rank/nranks differ from the stepper's layout");
+    return -1;
+  }
+  GS_HIP(hipSetDevice(s->cfg.device));
+  ncclUniqueId id;
+  memcpy(&id, id128, sizeof(id));
+  // The one-sided multi-rank schedule is always split (the sym schedule has its own slots).
+  if (s->L.mode != GS_MODE_SYM && ensure_partial(s)) return -1;
+  GS_NCCL(ncclCommInitRank(&s->comm, nranks, id, rank));
+  // GRAVSIM_FORCE_COMM keeps a 1-rank communicator live so the full multi-rank schedule
+  // (in-place ncclAllGather, local/remote split on two streams, events) runs on one GPU.
+  s->have_comm = nranks > 1 || getenv("GRAVSIM_FORCE_COMM") != nullptr;
+  if (!s->have_comm) {
+    (void)ncclCommDestroy(s->comm);
+    s->comm = nullptr;
+  }
+  drop_graphs(s);
+  if (s->have_comm) {
+    // Warm-up: RCCL builds its transports lazily on the first collective and on the first
+    // send/recv to each peer. Do both here on scratch memory (the accel buffer holds
+    // n_local * 4 >= P elements) so that no timed or captured step pays for it.
+    char* buf = static_cast<char*>(s->acc);
+    const ncclDataType_t dt = s->esz == 4 ? ncclFloat32 : ncclFloat64;
+    GS_NCCL(ncclAllGather(buf + (size_t)rank * s->esz, buf, 1, dt, s->comm, s->s_comm));
+    if (nranks > 1 && s->cfg.strategy == GS_STRATEGY_RING) {
+      GS_NCCL(ncclGroupStart());
+      GS_NCCL(ncclSend(buf, 1, dt, (rank + 1) % nranks, s->comm, s->s_comm));
+      GS_NCCL(ncclRecv(buf + (size_t)nranks * s->esz, 1, dt, (rank - 1 + nranks) % nranks,
+                       s->comm, s->s_comm));
+      GS_NCCL(ncclGroupEnd());
+    }
+    if (nranks > 1 && s->L.mode == GS_MODE_SYM) {
+      // The sym schedule's node-sum exchange talks to every peer: connect them all now.
+      GS_NCCL(ncclGroupStart());
+      for (int q = 0; q < nranks; ++q) {
+        if (q == rank) continue;
+        GS_NCCL(ncclSend(buf + (size_t)q * s->esz, 1, dt, q, s->comm, s->s_comm));
+        GS_NCCL(ncclRecv(buf + (size_t)(nranks + q) * s->esz, 1, dt, q, s->comm, s->s_comm));
+      }
+      GS_NCCL(ncclGroupEnd());
+    }
+    GS_HIP(hipStreamSynchronize(s->s_comm));
+  }
+  return 0;
+}
+
+int gs_stepper_comm_check(gs_stepper* s) {
+  if (!s->have_comm) return 0;
+  ncclResult_t async = ncclSuccess;
+  GS_NCCL(ncclCommGetAsyncError(s->comm, &async));
+  if (async != ncclSuccess && async != ncclInProgress) {
+    char b[256];
+    snprintf(b, sizeof(b), "RCCL async error: %s; communicator aborted", ncclGetErrorString(async));
+    (void)ncclCommAbort(s->comm);
+    s->have_comm = false;
+    gs_set_error(b);
+    return -1;
+  }
+  return 0;
+}
+
+}  // extern "C"

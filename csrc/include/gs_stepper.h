@@ -1,0 +1,257 @@
+// Internal to the native runtime (stepper.hip, stepper_comm.hip, stepper_plan.hip): the
+// Stepper's state and the helpers its translation units share. Not part of the C API
+// (gravsim.h).
+#pragma once
+#include <dlfcn.h>
+#include <execinfo.h>
+#include <hip/hip_runtime.h>
+#include <signal.h>
+#include <unistd.h>
+#include <math.h>
+#include <rccl/rccl.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <chrono>
+#include <functional>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "gravsim.h"
+#include "gs_common.h"
+#include "gs_kernels.h"
+
+void gs_set_error(const char* msg);
+
+#define GS_HIP(call)                                                                \
+  do {                                                                              \
+    hipError_t e_ = (call);                                                         \
+    if (e_ != hipSuccess) {                                                         \
+      char b_[384];                                                                 \
+      snprintf(b_, sizeof(b_), "%s:%d %s: %s", __FILE__, __LINE__, #call,           \
+               hipGetErrorString(e_));                                              \
+      gs_set_error(b_);                                                             \
+      return -1;                                                                    \
+    }                                                                               \
+  } while (0)
+
+#define GS_NCCL(call)                                                               \
+  do {                                                                              \
+    ncclResult_t r_ = (call);                                                       \
+    if (r_ != ncclSuccess) {                                                        \
+      char b_[384];                                                                 \
+      snprintf(b_, sizeof(b_), "%s:%d %s: %s", __FILE__, __LINE__, #call,           \
+               ncclGetErrorString(r_));                                             \
+      gs_set_error(b_);                                                             \
+      return -1;                                                                    \
+    }                                                                               \
+  } while (0)
+
+struct gs_stepper {
+  gs_config cfg;
+  gs_layout L;
+  size_t esz = 4;  // element size
+  hipStream_t s_comp = nullptr, s_comm = nullptr;
+  hipStream_t s_rem = nullptr;  // second compute stream: remote chunks beside the local ones
+  hipStream_t s_rem2 = nullptr;  // third compute stream: ring sub-steps alternate rem/rem2
+  hipEvent_t ev_rem2 = nullptr;
+  std::vector<hipEvent_t> ev_recv;  // ring: per sub-step "slice arrived" events
+  hipEvent_t ev_ready = nullptr, ev_gathered = nullptr, ev_remote = nullptr, ev_fork = nullptr;
+  hipEvent_t ev_t0 = nullptr, ev_local = nullptr, ev_end = nullptr;
+  void* X[2] = {nullptr, nullptr};
+  void* vel = nullptr;
+  void* partial = nullptr;
+  void* acc = nullptr;
+  double* mass_dev = nullptr;
+  unsigned long long* nonfinite = nullptr;
+  std::vector<double> mass_host;
+  int64_t k = 0;  // steps done; current positions live in X[k & 1]
+  bool full[2] = {true, false};
+  ncclComm_t comm = nullptr;
+  bool have_comm = false;
+  bool virt = false;  // member of a virtual-rank group (gather = device copies, gs_group_step)
+  bool emulate = false;  // GRAVSIM_EMULATE_RANK: run one rank's launch shapes, no exchange
+  // sym work beside a pending gather (GRAVSIM_SYM_OVERLAP): 0 none (wait, then one launch),
+  // 1 the diagonal units first on the compute stream, 2 diagonal + rank-local shell units
+  // concurrently with the rest on a second stream.
+  int sym_overlap = 0;
+  hipGraphExec_t graph = nullptr;
+  bool timed = false;  // eager steps record phase events
+  int own_c0 = 0, own_c1 = 0;  // this rank's chunks clipped to [0, n_chunks)
+  bool exact = true;           // hard-cutoff select vs fast core-softened path
+  double eps2 = 0.0;           // r^2 offset used by the kernels
+  int cus = 256;               // compute units
+  int occ[3] = {0, 0, 0};      // split-kernel workgroups per CU by force mode
+  // Newton-3 symmetric schedule (GS_MODE_SYM): partial slots, node sums, geometry.
+  char* sym_Pi = nullptr;  // element type: float or double (esz)
+  char* sym_Pj = nullptr;
+  char* sym_Pd = nullptr;
+  char* sym_S = nullptr;  // node sums by destination rank
+  char* sym_R = nullptr;  // node sums of every rank, global node order (== sym_S, one rank)
+  char* sym_Ti = nullptr;  // per-body i-side totals [3][n_local]
+  char* sym_Bb = nullptr;  // multi-band runs: per-block leaf sums [own blocks][3][bodies]
+  int32_t sym_NC = 0, sym_H = 0, sym_L = 0, sym_S_n = 0, sym_D = 1;
+  int32_t sym_band = 0;  // rows per band (Pi/Pj/Pd hold one band; a multiple of sym_RB)
+  // Row blocks and reduction-tree nodes (gs_sym_nodes): rank q owns blocks
+  // [blk_lo[q], blk_lo[q + 1]) = bodies [rbeg[q], rbeg[q] + rcnt[q]); it sends nn(q) nodes,
+  // the first of them global node nbase[q].
+  int32_t sym_B = 8, sym_RB = 1, sym_NN = 1;
+  int32_t blk_lo[9] = {0};
+  std::vector<int64_t> rbeg, rcnt;
+  std::vector<int32_t> nn, nbase;
+  bool uniform = true;  // every rank owns the same body count (P | B: ncclAllGather)
+  hipEvent_t ev_sym = nullptr;
+  // Per-rank emulation with modeled collectives (GRAVSIM_EMU_COMM_GBPS > 0): every all-gather
+  // and node-sum exchange becomes a comm_model_kernel of the same byte count on s_comm.
+  double emu_gbps = 0.0, emu_lat_us = 15.0;
+  int emu_wgs = 16;
+  void* emu_buf = nullptr;
+  unsigned long long* utrace = nullptr;  // GRAVSIM_UNIT_TRACE: per force workgroup timeline
+  // Dynamic unit fetch of the sym force launch (GRAVSIM_SYM_DYN_CAP; <= 1: static units):
+  // units per workgroup after the first wave, and the first wave's size (resident slots).
+  int dyn_cap = 4;
+  int sym_first_wave = 0;
+  int64_t utrace_main = 0;               // entries of the main launch (deferred ones follow)
+  size_t emu_cap = 0;
+  double clk_khz = 100000.0;  // device wall clock (wall_clock64) rate
+  // Gather gates (sym_overlap 3): [0], [1] gate of X[0] / X[1]; [3] the most units one step
+  // deferred past the gather (since the last phase_stats call). defer: count + unit list.
+  unsigned* gate_buf = nullptr;
+  unsigned* defer = nullptr;
+  int32_t* sym_lf = nullptr;  // units-6 order: unit -> row << 16 | segment (bit 31 remote)
+  // Ring strategy of the sym schedule: P-1 neighbour stages instead of one all-gather; the
+  // gated launch waits per stage (ring_gate[8 * buffer + stage], set after each stage's
+  // receive) and its unit map orders the remote units by stage.
+  bool sym_ring = false;
+  unsigned* ring_gate = nullptr;
+  int gate_probe = 0;         // GRAVSIM_GATE_PROBE (emulation timing probes only)
+  int diag_last = 1;          // GRAVSIM_SYM_DIAG_LAST=0: row-by-row unit order (A/B only)
+  int fuse_tail = -1;         // GRAVSIM_SYM_FUSED_TAIL: -1 by size (<= 256K), 0 off, 1 on
+  int parity = 1;             // GRAVSIM_SYM_PARITY=0: round-1 antipodal rule (A/B only)
+  // Phase timing of eager steps (timed): one event set per step, summed by phase_stats.
+  struct PhaseEv {
+    hipEvent_t t0, end, g0, g1, w0, w1, x0, x1, j0, j1;
+    bool g, w, x, j;
+  };
+  std::vector<PhaseEv> pev;
+  int pev_used = 0;
+  PhaseEv* pe = nullptr;  // the step being enqueued
+  // Progress events (one per enqueued step or graph period) for the bounded wait: its
+  // deadline restarts whenever one more completes, so it bounds progress, not the run.
+  std::vector<hipEvent_t> prog;
+  int64_t prog_rec = 0, prog_done = 0;
+  double step_timeout_s = 0.0;  // 0: unbounded
+  bool graph_failed = false;    // multi-rank capture refused: eager fallback
+  bool work_zero = true;        // sym dynamic unit counter (gate_buf[4]) known to be 0
+  // Work audit of the sym force launches: +1 per unit run (nbody_sym.hip audit_unit); a step
+  // runs rows x (S + D) units on this rank whatever the launch split or fetch order.
+  unsigned long long* audit = nullptr;
+  // Fault injection for the audit's own test (GRAVSIM_FAULT_SKIP_UNITS=k): every dynamic
+  // force launch starts its unit counter at k instead of 0, so units 0 .. k-1 never run,
+  // exactly the failure class of a stale re-armed counter (a memset node when captured).
+  unsigned fault_skip = 0;
+  bool rearm_lastwg = false;  // GRAVSIM_SYM_REARM=lastwg: round 2's in-kernel counter re-arm
+  // GRAVSIM_SYM_FORK_ROW=1 (A/B only): the row reduce on a second stream beside the node
+  // reduce. Measured slower: the two streaming sums contend (reduce phase at 1M 1533-1592 us
+  // per step against 1342-1381 in sequence; profiles/r3_reduce_fork_split_ab.txt).
+  bool fork_row = false;
+  // Segmented step graph of multi-rank runs (use_graph 1): the compute stream's work between
+  // two cross-stream points is captured as one graph segment; the collectives (RCCL, or the
+  // emulation's modeled ones) and the event record/wait that order them against the compute
+  // stream are issued eagerly between the segments on replay. RCCL is never captured, so the
+  // socket-transport capture crash (profiles/r2_graph_comm_root_cause.txt) cannot occur.
+  struct PlanOp {
+    enum Kind { kGraph, kRecord, kWait, kHost } kind;
+    hipGraphExec_t g;
+    hipEvent_t ev;
+    std::function<int()> fn;
+  };
+  std::vector<PlanOp> plan;  // one ping-pong period (two steps)
+  bool rec = false;          // recording a plan: s_comp is capturing a segment
+  int plan_graphs = 0;       // graph segments per period (diagnostics)
+  // Device memory ledger: every HBM buffer the stepper owns, by name (gs_stepper_mem_entry);
+  // destroy frees exactly these. All of them are allocated before the first step, sized from
+  // the layout (the sym bands from the free HBM), so nothing is allocated inside the loop.
+  struct MemEntry {
+    void* p;
+    size_t bytes;
+    const char* tag;
+  };
+  std::vector<MemEntry> mem;
+};
+
+#define GS_MARK(field, flag, stream)                             \
+  do {                                                           \
+    if (s->pe) {                                                 \
+      GS_HIP(hipEventRecord(s->pe->field, (stream)));            \
+      s->pe->flag = true;                                        \
+    }                                                            \
+  } while (0)
+
+namespace gs::rt {
+
+inline size_t row_bytes(const gs_stepper* s) { return 4 * s->esz; }
+
+// hipMalloc through the ledger; on failure the error names the buffer, its size and the
+// free HBM (a 16M-body rank needs ~110 GB of partial slots).
+template <typename T>
+inline int dev_alloc(gs_stepper* s, T** p, size_t bytes, const char* tag) {
+  void* v = nullptr;
+  const hipError_t e = hipMalloc(&v, bytes ? bytes : 16);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    size_t free_b = 0, total_b = 0;
+    (void)hipMemGetInfo(&free_b, &total_b);
+    char b[320];
+    snprintf(b, sizeof(b), "device allocation of %s (%.3f GB) failed: %s (free %.3f of %.3f GB)",
+             tag, bytes / 1e9, hipGetErrorString(e), free_b / 1e9, total_b / 1e9);
+    gs_set_error(b);
+    return -1;
+  }
+  *p = static_cast<T*>(v);
+  s->mem.push_back({v, bytes, tag});
+  return 0;
+}
+
+// A multi-rank exchange is active: a real communicator, or the per-rank emulation.
+inline bool xcomm(const gs_stepper* s) { return s->have_comm || s->emulate; }
+// Remote slices must be brought in before they are read (RCCL, emulation, virtual ranks).
+inline bool multi(const gs_stepper* s) { return s->have_comm || s->emulate || s->virt; }
+// The sym kernels implement both cutoff paths (fast core and exact select).
+inline bool use_sym(const gs_stepper* s) { return s->L.mode == GS_MODE_SYM; }
+
+// ---- shared by the runtime's translation units -----------------------------------------
+// stepper_plan.hip: compute-stream ordering points (eager, or cut points of a recorded
+// segmented plan), step graphs, the progress-bounded wait.
+int seg_cut(gs_stepper* s);
+int seg_open(gs_stepper* s);
+int comp_record(gs_stepper* s, hipEvent_t ev);
+int comp_wait(gs_stepper* s, hipEvent_t ev);
+int comm_do(gs_stepper* s, std::function<int()> fn);
+void drop_graphs(gs_stepper* s);
+int build_graph(gs_stepper* s);
+bool plan_ok(const gs_stepper* s);
+int build_plan(gs_stepper* s);
+int run_plan(gs_stepper* s);
+int wait_until(gs_stepper* s, int64_t target, double timeout_s);
+int note_progress(gs_stepper* s);
+
+// stepper_comm.hip: the collectives (RCCL, the per-rank emulation's modeled ones).
+int comm_model(gs_stepper* s, const void* src, size_t bytes, size_t src_cap);
+void rank_slice(const gs_stepper* s, int q, int64_t* b0, int64_t* cnt);
+int gather(gs_stepper* s, int cur, bool gate = false);
+int ring_src(const gs_stepper* s, int sub);
+void rank_chunks(const gs_stepper* s, int src, int* c0, int* c1);
+int ring_xfer_rccl(gs_stepper* s, int cur, int sub);
+int sym_exchange_rccl(gs_stepper* s, bool join = true);
+void maybe_install_crash_trace();
+
+// stepper.hip: buffers, step enqueue.
+size_t gather_bytes(const gs_stepper* s);
+size_t exchange_bytes(const gs_stepper* s);
+int ensure_partial(gs_stepper* s);
+int enqueue_step_any(gs_stepper* s, bool capturing, bool gathered_externally = false);
+
+}  // namespace gs::rt
