@@ -306,6 +306,14 @@ __device__ __forceinline__ int staged_entry(int lane_src, int copy) {
   return g * 32 + (copy ? 31 - c : 15 - c);
 }
 
+// Scheduling regions of the fp64 hot block (GS_SYM_PIPE64, as GS_SYM_PIPE for fp32 below):
+// 1 (default) reads the next step's j-body from LDS one step ahead and keeps LDS reads inside
+// their step: 512K fp64 99.62-99.66 vs 100.09-100.19 ms, same bits; 2 also closes a region
+// after every i-body (100.08-100.11 ms: the f64 chains then need s_nops); 0 neither
+// (profiles/r3s2_sched_barrier_fp64_ab.jsonl).
+#ifndef GS_SYM_PIPE64
+#define GS_SYM_PIPE64 1
+#endif
 // fp64 pair arithmetic (no packed f64 VALU on gfx950): the integrator's own fp64 formula
 // (nbody_kernels.hip interact, step path): y0 = v_rsq_f64(r^2), e = 1 - r^2 y0^2,
 // r^-3 = y0^3 (1 + 3/2 e + 15/8 e^2) with |e| <= 1.1e-7, i.e. double-precision r^-3;
@@ -345,6 +353,9 @@ __device__ __forceinline__ void meet_j(ISetT<double, I>& a, double xj, double yj
         tz = __builtin_fma(sj, dz, tz);
       }
     }
+#if GS_SYM_PIPE64 >= 2
+    __builtin_amdgcn_sched_barrier(0);  // one i-body's temporaries in flight at a time
+#endif
   }
 }
 
@@ -395,6 +406,18 @@ struct ISetP {
 // i-bodies per stage group: each group's rsq burst is followed by an s_nop (trans-use
 // hazard); 4 halves the groups. 1M: U 4 169.42 ms, U 2 170.6, U 8 170.2 (alternating runs,
 // profiles/r1_sym_ab_jpack.jsonl).
+// Scheduling regions of the hot block (GS_SYM_PIPE). LLVM's max-ILP scheduler, left alone
+// with the unrolled 16-step block, hoists LDS reads of many steps to its top and interleaves
+// the stage groups freely. 2 (default): each step reads the next step's j-pair from LDS and a
+// barrier keeps LDS reads inside their step (ALU may cross it), and a full barrier closes every
+// stage group, so one group's temporaries are in flight at a time: same instructions and bits,
+// 1M 159.6-159.9 vs 162.4-162.5 ms (alternating runs, profiles/r3s2_sched_barrier_ab.jsonl).
+// 1: the step barrier only (-0.8 %). 0: no barriers. A software pipeline that ran group n's
+// geometry + rsq beside group n-1's accumulations in one region measured -0.5 % (not kept),
+// groups of 2 i-bodies -0.6 %, and no form reaches 3 waves/SIMD without spilling.
+#ifndef GS_SYM_PIPE
+#define GS_SYM_PIPE 2
+#endif
 #ifndef GS_SYM_UP
 #define GS_SYM_UP 4
 #endif
@@ -466,6 +489,9 @@ __device__ __forceinline__ void meet_jp(ISetP<I>& a, f2 xj, f2 yj, f2 zj, f2 mj,
         }
       }
     }
+#if GS_SYM_PIPE >= 2
+    __builtin_amdgcn_sched_barrier(0);  // one i-group's temporaries live at a time
+#endif
   }
 }
 
@@ -486,11 +512,45 @@ __device__ __forceinline__ void lds_step_jp(ISetP<I>& a, CSetT<float, 2>& c, con
   }
 }
 
+// GS_SYM_PIPE >= 1: step K reads step K+1's j-pair from LDS before its own arithmetic, and a
+// scheduling barrier keeps every ds_read inside its step (ALU may still cross it).
+template <int I, bool SYM, bool EXACT, int K>
+__device__ __forceinline__ void lds_step_jp_pipe(ISetP<I>& a, CSetT<float, 2>& c,
+                                                 const float4* base, float4& p, float4& q,
+                                                 float eps2, float cut2) {
+  float4 pn, qn;
+  if constexpr (K + 1 < 16) {
+    pn = base[2 * (K + 1)];
+    qn = base[2 * (K + 1) + 1];
+  }
+  f2 tx, ty, tz;
+  meet_jp<I, SYM, EXACT>(a, f2{p.x, p.y}, f2{p.z, p.w}, f2{q.x, q.y}, f2{q.z, q.w}, eps2, tx,
+                         ty, tz, cut2);
+  if constexpr (SYM) {
+    c.cx[0] = row_from<1>(c.cx[0]) - tx.x;
+    c.cx[1] = row_from<1>(c.cx[1]) - tx.y;
+    c.cy[0] = row_from<1>(c.cy[0]) - ty.x;
+    c.cy[1] = row_from<1>(c.cy[1]) - ty.y;
+    c.cz[0] = row_from<1>(c.cz[0]) - tz.x;
+    c.cz[1] = row_from<1>(c.cz[1]) - tz.y;
+  }
+  if constexpr (K + 1 < 16) {
+    p = pn;
+    q = qn;
+  }
+  __builtin_amdgcn_sched_barrier(0x0406);  // VALU, SALU, TRANS may cross; LDS and VMEM not
+}
+
 template <int I, bool SYM, bool EXACT, int... Ks>
 __device__ __forceinline__ void lds_row_pass_jp(ISetP<I>& a, CSetT<float, 2>& c,
                                                 const float4* base, float eps2, float cut2,
                                                 std::integer_sequence<int, Ks...>) {
+#if GS_SYM_PIPE
+  float4 p = base[0], q = base[1];
+  (lds_step_jp_pipe<I, SYM, EXACT, Ks>(a, c, base, p, q, eps2, cut2), ...);
+#else
   (lds_step_jp<I, SYM, EXACT, Ks>(a, c, base, eps2, cut2), ...);
+#endif
 }
 
 // All (64 I) x 128 pairs against the pair-staged j-tile (LDS). Carriers return home.
@@ -516,10 +576,34 @@ __device__ __forceinline__ void tile_lds_jp(ISetP<I>& a, CSetT<float, 2>& c, con
   }
 }
 
+// fp64, J = 1, GS_SYM_PIPE64 >= 1: step K holds its j-body in q and reads step K + 1's.
+template <typename T, int I, bool SYM, bool EXACT, int K>
+__device__ __forceinline__ void lds_step_pipe(ISetT<T, I>& a, CSetT<T, 1>& c, const Vec4<T>* base,
+                                              Vec4<T>& q, T eps2, T cut2) {
+  Vec4<T> qn;
+  if constexpr (K + 1 < 16) qn = base[K + 1];
+  T tx, ty, tz;
+  meet_j<I, SYM, EXACT>(a, q.x, q.y, q.z, q.w, eps2, tx, ty, tz, cut2);
+  if constexpr (SYM) {
+    c.cx[0] = row_from<1>(c.cx[0]) - tx;
+    c.cy[0] = row_from<1>(c.cy[0]) - ty;
+    c.cz[0] = row_from<1>(c.cz[0]) - tz;
+  }
+  if constexpr (K + 1 < 16) q = qn;
+  __builtin_amdgcn_sched_barrier(0x0406);  // VALU, SALU, TRANS may cross; LDS and VMEM not
+}
+
 template <typename T, int I, int J, bool SYM, bool EXACT, int... Ks>
 __device__ __forceinline__ void lds_row_pass(ISetT<T, I>& a, CSetT<T, J>& c,
                                              const Vec4<T>* base, T eps2, T cut2,
                                              std::integer_sequence<int, Ks...>) {
+#if GS_SYM_PIPE64
+  if constexpr (sizeof(T) == 8 && J == 1) {
+    Vec4<T> q = base[0];
+    (lds_step_pipe<T, I, SYM, EXACT, Ks>(a, c, base, q, eps2, cut2), ...);
+    return;
+  }
+#endif
   (lds_step<T, I, J, SYM, EXACT, Ks>(a, c, base, eps2, cut2), ...);
 }
 
