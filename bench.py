@@ -31,7 +31,8 @@ Audits of the timed work (outside the timed region; the run exits non-zero if on
     schedule (eager launches, one static unit per workgroup, ungated) and must give the
     same bits on every rank.
 Also outside it: the sampled accuracy of the step's own accelerations at step 0 and after
-the last timed step, the relative drift of total momentum over the run, a few eager steps
+the last timed step, the relative drift of total momentum over the run, the drift of total
+energy (kinetic + exact-cutoff potential) and angular momentum (two O(N^2) passes), a few eager steps
 with phase events for the comm split, and the reference's exact hard-cutoff select timed
 on its own (exact_cutoff_ms_per_step). Multi-rank runs record per rank the device it bound
 and the RCCL transports its connections used (parsed from RCCL's INFO log, sent to a file).
@@ -85,6 +86,9 @@ def parse(argv=None) -> argparse.Namespace:
                     help="eager steps with phase events after the timed loop (comm split)")
     ap.add_argument("--no-replay-audit", dest="replay_audit", action="store_false",
                     help="skip the independent-schedule re-run of the timed steps")
+    ap.add_argument("--no-energy", dest="energy", action="store_false",
+                    help="skip the conserved-quantity passes (total energy with the exact-cutoff "
+                         "potential, momenta) before the warmup and after the timed steps")
     ap.add_argument("--exact-steps", type=int, default=3,
                     help="steps timed with the reference's exact cutoff select after the "
                          "headline (0 = skip)")
@@ -264,6 +268,7 @@ def main(argv=None) -> int:
     from gravsim.ops import _native
     from gravsim.parallel import comm, launch
     from gravsim.runtime.engines import HipEngine
+    from gravsim.runtime.simulation import conservation_summary, engine_conserved
 
     dist = comm.init()
     world, rank = dist.world, dist.rank
@@ -304,6 +309,7 @@ def main(argv=None) -> int:
         err = comm.allreduce_max(dist, err)
     _, vel0, mass = own_state(eng)
     p0, pscale = momentum(dist, comm, vel0, mass)
+    cons0 = engine_conserved(eng, dist) if a.energy else None  # exact-cutoff potential pass
 
     eng.step(a.warmup)
     eng.sync()
@@ -343,6 +349,10 @@ def main(argv=None) -> int:
     err_end = sampled_error(eng, cfg, a.check_samples) if a.check_samples > 0 else None
     if err_end is not None:
         err_end = comm.allreduce_max(dist, err_end)
+    conservation = None
+    if cons0 is not None:
+        conservation = conservation_summary(cons0, engine_conserved(eng, dist))
+        conservation.pop("samples")
 
     # Comm/compute split (untimed): a few eager steps with per-step phase events.
     phase = None
@@ -448,6 +458,10 @@ def main(argv=None) -> int:
                 "sampled_rel_err": err,
                 "sampled_rel_err_final": err_end,
                 "momentum_rel_drift": drift,
+                # total energy (kinetic + exact-cutoff potential), momentum and angular momentum
+                # before the warmup and after the timed steps (KD is first order: the energy
+                # drift is the integrator's, at dt = 3600 s)
+                "conservation": conservation,
                 "exact_cutoff_ms_per_step": exact_ms,
                 "nonfinite": int(bad),
                 "hbm": {"gb_per_rank_max": round(hbm_max / 1e9, 3),

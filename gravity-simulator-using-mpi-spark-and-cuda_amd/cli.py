@@ -88,6 +88,13 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--nproc", "--gpus", dest="nproc", type=int, default=0,
                    help="launch this many ranks (one per GPU) on this node through "
                         "torch.distributed.run, like `mpirun -np N` (mpi.c); 0 = as launched")
+    p.add_argument("--diagnostics", action="store_true",
+                   help="conserved quantities (total energy with the exact-cutoff potential, "
+                        "linear and angular momentum) at the start and end of the run, and "
+                        "their relative drift in the metrics JSON")
+    p.add_argument("--diag-every", type=int, default=0,
+                   help="also sample them every k steps (implies --diagnostics; each sample is "
+                        "an O(N^2) pass, excluded from the timed wall)")
     p.add_argument("--quiet", action="store_true")
     return p
 
@@ -113,7 +120,9 @@ def config_from_args(a: argparse.Namespace) -> SimConfig:
                      checkpoint_dir=a.checkpoint_dir, checkpoint_every=a.checkpoint_every,
                      resume=resume, record_every=a.record_every, record_path=a.record_path,
                      nan_check_every=a.nan_check_every, metrics_json=a.metrics_json,
-                     phase_timing=a.phase_timing).validate()
+                     phase_timing=a.phase_timing,
+                     diagnostics=a.diagnostics or a.diag_every > 0,
+                     diag_every=a.diag_every).validate()
 
 
 def run_one(cfg: SimConfig, dist, log, quiet: bool = False, final: bool = True) -> dict:

@@ -67,6 +67,9 @@ class SimConfig:
     record_every: int = 0             # trajectory recorder (pyspark.py:105,114-115)
     record_path: Optional[str] = None
     nan_check_every: int = 0          # NaN/Inf guard period (0 = only at the end)
+    diagnostics: bool = False         # total energy, momentum, angular momentum at the start and
+                                      # the end of the run (exact-cutoff potential, O(N^2) pass)
+    diag_every: int = 0               # ... and every k steps (the passes are excluded from wall)
     metrics_json: Optional[str] = None
     phase_timing: bool = False        # GPU: per-step phase events (comm/compute split in the
                                       # metrics; eager steps, no graph replay)
@@ -105,6 +108,8 @@ class SimConfig:
             raise ValueError("strategy must be allgather or ring")
         if self.overlap not in (-1, 0, 1, 2, 3):
             raise ValueError("overlap must be -1 (default) or 0..3")
+        if self.diag_every < 0:
+            raise ValueError("diag_every must be >= 0")
         if self.step_timeout_s < 0:
             raise ValueError("step_timeout_s must be >= 0 (0 = unbounded)")
         if self.cutoff < 0 or self.softening < 0:

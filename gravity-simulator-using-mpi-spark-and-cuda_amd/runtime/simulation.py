@@ -9,6 +9,8 @@ design:
   but ends with a device sync so the number is real;
 * NaN/Inf guard (the reference silently produced non-finite output, D1-D3) and RCCL health
   checks run at a configurable period;
+* optional conserved-quantity diagnostics (--diagnostics / --diag-every): total energy with
+  the exact-cutoff potential, linear and angular momentum, and their relative drift;
 * checkpoints are rank-agnostic and a resumed run continues bit-exactly;
 * integrator "kd" is the reference's kick-drift update (cuda.cu:73-76, mpi.c:207-215);
   "leapfrog" runs the very same per-step kernel on velocities staggered by half a step
@@ -37,6 +39,48 @@ from .engines import CpuEngine, HipEngine, gpu_available
 
 class NonFiniteError(RuntimeError):
     pass
+
+
+def engine_conserved(engine, dist, step: int = 0, staggered: bool = False,
+                     dt: float = 0.0) -> dict:
+    """Total energy, linear and angular momentum of an engine's current state (collective).
+
+    Each rank sums over its own bodies: kinetic 1/2 m v^2, potential 1/2 m phi with phi the
+    exact-cutoff potential of the engine's diagnostic force path (the same pass returns the
+    accelerations that synchronise leapfrog's half-step velocities v_{k-1/2} + a dt/2),
+    p = sum m v and L = sum m x cross v; the sums are all-reduced. The reference has no such
+    check (it only prints positions); it is the standard correctness gauge of an N-body
+    integrator (bench.py reports the drift over its timed steps)."""
+    rows = engine.layout.real_local
+    b = engine.state()
+    sl = slice(rows.start, rows.stop)
+    m, x, v = b.mass[sl], b.pos[sl], b.vel[sl]
+    a4 = engine.accel()[: len(rows)] if len(rows) else np.zeros((0, 4))
+    if staggered:
+        v = v + 0.5 * dt * a4[:, :3]
+    xv = np.cross(x, v) if len(rows) else np.zeros((0, 3))
+    red = lambda y: comm.allreduce_sum(dist, float(y))  # noqa: E731
+    ke = red(0.5 * (m * (v * v).sum(1)).sum())
+    pe = red(0.5 * (m * a4[:, 3]).sum())
+    return {"step": int(step), "kinetic": ke, "potential": pe, "energy": ke + pe,
+            "momentum": [red(c) for c in (m[:, None] * v).sum(0)],
+            "angular_momentum": [red(c) for c in (m[:, None] * xv).sum(0)],
+            "momentum_scale": red((m * np.linalg.norm(v, axis=1)).sum()),
+            "angular_momentum_scale": red((m * np.linalg.norm(xv, axis=1)).sum())}
+
+
+def conservation_summary(c0: dict, c1: dict, samples: list = ()) -> dict:
+    """Relative drifts of the conserved quantities between two engine_conserved() records."""
+    def rel(a, b, scale):
+        d = float(np.linalg.norm(np.asarray(b, dtype=float) - np.asarray(a, dtype=float)))
+        return d / scale if scale > 0 else (0.0 if d == 0 else float("inf"))
+
+    return {"energy_start": c0["energy"], "energy_end": c1["energy"],
+            "energy_rel_drift": rel(c0["energy"], c1["energy"], abs(c0["energy"])),
+            "momentum_rel_drift": rel(c0["momentum"], c1["momentum"], c0["momentum_scale"]),
+            "angular_momentum_rel_drift": rel(c0["angular_momentum"], c1["angular_momentum"],
+                                              c0["angular_momentum_scale"]),
+            "samples": [{"step": c["step"], "energy": c["energy"]} for c in samples]}
 
 
 class Simulation:
@@ -130,6 +174,11 @@ class Simulation:
             b.vel = b.vel + 0.5 * self.cfg.dt * acc
         return b
 
+    def conserved(self) -> dict:
+        """Total energy, linear and angular momentum of the current state (collective);
+        see engine_conserved."""
+        return engine_conserved(self.engine, self.dist, self.step, self.staggered, self.cfg.dt)
+
     def check_finite(self) -> None:
         bad = comm.allreduce_sum(self.dist, self.engine.nonfinite())
         if bad:
@@ -154,9 +203,12 @@ class Simulation:
         cfg = self.cfg
         steps = cfg.steps if steps is None else int(steps)
         periods = [p for p in (cfg.progress_every if log else 0, cfg.checkpoint_every,
-                               cfg.record_every, cfg.nan_check_every, cfg.dump_every)
+                               cfg.record_every, cfg.nan_check_every, cfg.dump_every,
+                               cfg.diag_every)
                    if p and p > 0]
         gpu = isinstance(self.engine, HipEngine)
+        c0 = self.conserved() if cfg.diagnostics else None
+        samples, diag_s = [], 0.0
         timing = cfg.phase_timing and gpu
         if timing:
             self.engine.set_timing(True)
@@ -179,8 +231,13 @@ class Simulation:
                 self.save_checkpoint()
             if cfg.dump_every and s % cfg.dump_every == 0:
                 self.dump_positions()
+            if cfg.diag_every and s % cfg.diag_every == 0 and s < steps:
+                self.engine.sync()  # the steps so far stay inside the wall ...
+                td = time.perf_counter()
+                samples.append(self.conserved())
+                diag_s += time.perf_counter() - td  # ... the O(N^2) sample does not
         self.engine.sync()
-        wall = time.perf_counter() - t0
+        wall = time.perf_counter() - t0 - diag_s
         wall = comm.allreduce_max(self.dist, wall)
         extra = {}
         if timing:  # the comm/compute split, max over ranks
@@ -202,6 +259,8 @@ class Simulation:
             extra.update(work_audit="ok" if per else "n/a (one-sided schedule)",
                          overlap=self.engine.overlap, graph=gi["mode"],
                          graph_segments=gi["segments"] or None)
+        if c0 is not None:
+            extra["conservation"] = conservation_summary(c0, self.conserved(), samples)
         lay = getattr(self.engine, "native_layout", {})
         from ..ops._native import KERNEL_NAMES, MODE_NAMES
 

@@ -2,7 +2,7 @@
 # One parameterised GPU recipe (run on the MI355X box through gpurun):
 #   bash scripts/gpu.sh <task> [<task> ...]
 # tasks (each step under its own time limit; the first failure ends the call):
-#   tests[:<pytest -k expr>]  GPU test suite (or a subset), one process, per-test timeout
+#   tests[:<pytest -k expr>]  GPU test suite (or a subset; "+" -> space), one process
 #   smoke                     __graft_entry__.smoke()
 #   bench[:<args>]            bench.py ("+" in <args> becomes a space)
 #   prof[:<args>]             rocprofv3 kernel-trace stats of bench.py -> gpurun_out/prof
@@ -42,7 +42,7 @@ for task in "$@"; do
   a=$(args_of "$task")
   case "$name" in
     tests)
-      if [ -n "${task#tests}" ]; then k="${task#tests:}"; else k=""; fi
+      if [ -n "${task#tests}" ]; then k="${task#tests:}"; k="${k//+/ }"; else k=""; fi
       step 1500 $out/pytest_gpu${k:+_sel}.log python -u -m pytest tests -x -v -m gpu \
         --timeout 300 --timeout-method thread --durations=30 ${k:+-k "$k"} ;;
     smoke) step 300 $out/smoke.log python __graft_entry__.py smoke ;;

@@ -88,6 +88,10 @@ def test_bench_audit_ok_and_reports_physics(hip):
     assert c["momentum_rel_drift"] < 1e-5
     assert c["exact_cutoff_ms_per_step"] > 0
     assert c["hbm"]["gb_per_rank_max"] > 0 and "sym_Pj" in c["hbm"]["by_buffer_gb_rank0"]
+    k = c["conservation"]  # energy with the exact-cutoff potential, before warmup / after
+    assert k["energy_start"] < 0 and k["energy_end"] < 0  # bound system (solar + random)
+    assert 0 <= k["energy_rel_drift"] < 1e-2 and k["momentum_rel_drift"] < 1e-5
+    assert k["angular_momentum_rel_drift"] < 1e-5
 
 
 def test_bench_audit_catches_skipped_units(hip):
