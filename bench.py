@@ -6,10 +6,10 @@ N is fixed as the GPU count grows (strong scaling). The default (mode auto) at t
 the Newton-3 schedule: every unordered pair is evaluated once and applied to both bodies
 (csrc/hip/nbody_sym.hip). Each rank owns N/P bodies (a block of 2048-body chunk rows), joins
 an in-place RCCL all-gather of positions, evaluates its rows' cyclic half-shell of chunk
-pairs, exchanges its reduction-tree node sums of the far sides with ncclSend/ncclRecv, and integrates its
-own bodies (kick-drift). Single-rank steps replay a hipGraph; multi-rank steps replay a
-segmented plan: the compute work between two collectives as graph segments, the RCCL calls
-issued eagerly between them (--graph-comm captures the collectives too, opt-in).
+pairs, exchanges its reduction-tree node sums of the far sides with ncclSend/ncclRecv, and
+integrates its own bodies (kick-drift). Single-rank steps replay a hipGraph; multi-rank steps
+replay a segmented plan: the compute work between two collectives as graph segments, the RCCL
+calls issued eagerly between them (--graph-comm captures the collectives too, opt-in).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--n BODIES] [--dtype fp32|fp64]
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
@@ -30,12 +30,16 @@ Audits of the timed work (outside the timed region; the run exits non-zero if on
   * replay: the same warmup + K steps are re-run from the same ICs on an independent
     schedule (eager launches, one static unit per workgroup, ungated) and must give the
     same bits on every rank.
+If the gated local-first launch (--overlap auto picked 3 after its 2-step self-check) fails
+them, the run says so in config.overlap_fallback and times the ungated schedule from the
+same ICs instead, which must pass the same audits.
 Also outside it: the sampled accuracy of the step's own accelerations at step 0 and after
 the last timed step, the relative drift of total momentum over the run, the drift of total
-energy (kinetic + exact-cutoff potential) and angular momentum (two O(N^2) passes), a few eager steps
-with phase events for the comm split, and the reference's exact hard-cutoff select timed
-on its own (exact_cutoff_ms_per_step). Multi-rank runs record per rank the device it bound
-and the RCCL transports its connections used (parsed from RCCL's INFO log, sent to a file).
+energy (kinetic + exact-cutoff potential) and angular momentum (two O(N^2) passes), a few
+eager steps with phase events for the comm split, and the reference's exact hard-cutoff
+select timed on its own (exact_cutoff_ms_per_step). Multi-rank runs record per rank the device
+it bound and the RCCL transports its connections used (parsed from RCCL's INFO log, sent to a
+file).
 """
 from __future__ import annotations
 
@@ -311,77 +315,103 @@ def main(argv=None) -> int:
     p0, pscale = momentum(dist, comm, vel0, mass)
     cons0 = engine_conserved(eng, dist) if a.energy else None  # exact-cutoff potential pass
 
-    eng.step(a.warmup)
-    eng.sync()
-    eng.audit_reset()
-    torch.cuda.synchronize()
-    comm.barrier(dist)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    eng.step(a.steps)
-    eng.sync()
-    torch.cuda.synchronize()
-    comm.barrier(dist)
-    t1 = time.perf_counter()
-    wall = comm.allreduce_max(dist, t1 - t0)
-    ginfo = eng.graph_info()
-    # HBM the stepper holds (its allocation ledger; RCCL's own buffers excluded), max over ranks
-    mem = eng.mem_info() if hasattr(eng, "mem_info") else {}
-    hbm_max = comm.allreduce_max(dist, float(sum(mem.values())))
+    def measure(overlap: int) -> dict:
+        """Warmup + the K timed steps from the ICs already loaded, then the audits of that
+        work and the end-of-run physics (all untimed)."""
+        eng.step(a.warmup)
+        eng.sync()
+        eng.audit_reset()
+        torch.cuda.synchronize()
+        comm.barrier(dist)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        eng.step(a.steps)
+        eng.sync()
+        torch.cuda.synchronize()
+        comm.barrier(dist)
+        t1 = time.perf_counter()
+        wall = comm.allreduce_max(dist, t1 - t0)
+        ginfo = eng.graph_info()
+        # HBM the stepper holds (its allocation ledger; RCCL's own buffers excluded), max
+        # over ranks
+        mem = eng.mem_info() if hasattr(eng, "mem_info") else {}
+        hbm_max = comm.allreduce_max(dist, float(sum(mem.values())))
 
-    # ---- audits of the timed work (untimed) --------------------------------------------
-    failures = []
-    done, per_step = eng.audit()
-    if per_step:
-        short = comm.allreduce_sum(dist, 0.0 if done == per_step * a.steps else 1.0)
-        units = {"units_per_step_rank0": per_step,
-                 "units_done_rank0": done, "ranks_short": int(short)}
-        if short:
-            failures.append(f"unit count: {int(short)} rank(s) did not run rows x (S + D) "
-                            f"units per timed step (rank {rank}: {done} of "
-                            f"{per_step * a.steps})")
-    else:
-        units = None  # one-sided schedules: no unit counter, the replay audit still runs
-    bad = comm.allreduce_sum(dist, eng.nonfinite())
-    pos_t, vel_t, _ = own_state(eng)
-    p1, _ = momentum(dist, comm, vel_t, mass)
-    drift = float(np.linalg.norm(p1 - p0)) / max(pscale, 1e-300)
-    err_end = sampled_error(eng, cfg, a.check_samples) if a.check_samples > 0 else None
-    if err_end is not None:
-        err_end = comm.allreduce_max(dist, err_end)
-    conservation = None
-    if cons0 is not None:
-        conservation = conservation_summary(cons0, engine_conserved(eng, dist))
-        conservation.pop("samples")
+        # ---- audits of the timed work (untimed) ----------------------------------------
+        failures = []
+        done, per_step = eng.audit()
+        if per_step:
+            short = comm.allreduce_sum(dist, 0.0 if done == per_step * a.steps else 1.0)
+            units = {"units_per_step_rank0": per_step,
+                     "units_done_rank0": done, "ranks_short": int(short)}
+            if short:
+                failures.append(f"unit count: {int(short)} rank(s) did not run rows x (S + D) "
+                                f"units per timed step (rank {rank}: {done} of "
+                                f"{per_step * a.steps})")
+        else:
+            units = None  # one-sided schedules: no unit counter, the replay audit still runs
+        if overlap == 3 and os.environ.get("GRAVSIM_TEST_FAIL_GATED_AUDIT") == "1":
+            failures.append("injected failure (GRAVSIM_TEST_FAIL_GATED_AUDIT, test hook)")
+        bad = comm.allreduce_sum(dist, eng.nonfinite())
+        pos_t, vel_t, _ = own_state(eng)
+        p1, _ = momentum(dist, comm, vel_t, mass)
+        drift = float(np.linalg.norm(p1 - p0)) / max(pscale, 1e-300)
+        err_end = sampled_error(eng, cfg, a.check_samples) if a.check_samples > 0 else None
+        if err_end is not None:
+            err_end = comm.allreduce_max(dist, err_end)
+        conservation = None
+        if cons0 is not None:
+            conservation = conservation_summary(cons0, engine_conserved(eng, dist))
+            conservation.pop("samples")
 
-    # Comm/compute split (untimed): a few eager steps with per-step phase events.
-    phase = None
-    if a.phase_steps > 0:
-        eng.set_timing(True)
-        eng.step(a.phase_steps)
-        phase = eng.phase_stats()
-        eng.set_timing(False)
-        for k in ("step_ms", "comm_ms", "exposed_comm_ms", "gather_ms", "exchange_ms"):
-            phase[k] = comm.allreduce_max(dist, phase[k])
+        # Comm/compute split (untimed): a few eager steps with per-step phase events.
+        phase = None
+        if a.phase_steps > 0:
+            eng.set_timing(True)
+            eng.step(a.phase_steps)
+            phase = eng.phase_stats()
+            eng.set_timing(False)
+            for k in ("step_ms", "comm_ms", "exposed_comm_ms", "gather_ms", "exchange_ms"):
+                phase[k] = comm.allreduce_max(dist, phase[k])
 
-    # Replay: warmup + K steps from the same ICs on an independent schedule must give the
-    # timed run's bits (eager launches, one static unit per workgroup, no gating).
-    replay = None
-    if a.replay_audit:
-        eng.set_schedule(0, 0)
+        # Replay: warmup + K steps from the same ICs on an independent schedule must give the
+        # timed run's bits (eager launches, one static unit per workgroup, no gating).
+        replay = None
+        if a.replay_audit:
+            eng.set_schedule(0, 0)
+            eng.set_overlap(0)
+            eng.init_ics("solar+random", cfg.seed)
+            eng.step(a.warmup + a.steps)
+            eng.sync()
+            pos_r, vel_r, _ = own_state(eng)
+            same = np.array_equal(pos_r, pos_t) and np.array_equal(vel_r, vel_t)
+            diff = comm.allreduce_sum(dist, 0.0 if same else 1.0)
+            replay = "bitwise" if not diff else f"differs on {int(diff)} rank(s)"
+            if diff:
+                failures.append(f"replay: the independent schedule differs on {int(diff)} rank(s)")
+            eng.set_schedule((2 if a.graph_comm else 1) if a.graph else 0,
+                             int(os.environ.get("GRAVSIM_SYM_DYN_CAP", "4")))
+            eng.set_overlap(overlap)
+        return dict(wall=wall, ginfo=ginfo, mem=mem, hbm_max=hbm_max, failures=failures,
+                    units=units, bad=bad, drift=drift, err_end=err_end,
+                    conservation=conservation, phase=phase, replay=replay)
+
+    res = measure(overlap)
+    fallback = None
+    if res["failures"] and overlap == 3 and a.overlap == "auto":
+        # The gated local-first launch passed its 2-step self-check but the audit of the timed
+        # steps failed: report that, and time the ungated schedule from the same ICs instead
+        # (it must pass the same audits, or the run fails).
+        fallback = {"from_overlap": 3, "to_overlap": 0, "failures": res["failures"]}
+        overlap = 0
         eng.set_overlap(0)
         eng.init_ics("solar+random", cfg.seed)
-        eng.step(a.warmup + a.steps)
         eng.sync()
-        pos_r, vel_r, _ = own_state(eng)
-        same = np.array_equal(pos_r, pos_t) and np.array_equal(vel_r, vel_t)
-        diff = comm.allreduce_sum(dist, 0.0 if same else 1.0)
-        replay = "bitwise" if not diff else f"differs on {int(diff)} rank(s)"
-        if diff:
-            failures.append(f"replay: the independent schedule differs on {int(diff)} rank(s)")
-        eng.set_schedule((2 if a.graph_comm else 1) if a.graph else 0,
-                         int(os.environ.get("GRAVSIM_SYM_DYN_CAP", "4")))
-        eng.set_overlap(overlap)
+        res = measure(0)
+    wall, ginfo, mem, hbm_max = res["wall"], res["ginfo"], res["mem"], res["hbm_max"]
+    failures, units, bad, drift = res["failures"], res["units"], res["bad"], res["drift"]
+    err_end, conservation, phase, replay = (res["err_end"], res["conservation"], res["phase"],
+                                            res["replay"])
 
     # The reference's exact hard-cutoff select (cuda.cu:39, mpi.c:64), timed on its own.
     lay = eng.native_layout
@@ -451,6 +481,7 @@ def main(argv=None) -> int:
                 "graph_segments": ginfo["segments"] or None,
                 "overlap": overlap,
                 "overlap_check": overlap_check,
+                "overlap_fallback": fallback,
                 # N^2 ordered pair terms per step (what a one-sided sum evaluates) ...
                 "effective_interactions_per_s": float(cfg.n) * cfg.n * a.steps / wall,
                 # ... and the pair evaluations actually performed (sym: N(N-1)/2 per step)

@@ -202,3 +202,23 @@ def test_device_memory_ledger(hip):
         assert all(v > 0 for v in m.values())
     finally:
         e.close()
+
+
+def test_bench_two_ranks_gated_audit_falls_back_to_ungated(hip):
+    """Two RCCL ranks on one GPU (sockets, GRAVSIM_RCCL_RANK_HOSTS=1) through the production
+    launch sequence. A failed audit of the gated launch's timed steps (injected by bench.py's
+    test hook) must not end the run: it is reported in config.overlap_fallback and the ungated
+    schedule is timed from the same ICs, passing the same audits."""
+    r, out = _bench(["--gpus", "2", "--n", "65536", "--steps", "3", "--warmup", "1",
+                     "--exact-steps", "0", "--phase-steps", "0", "--check-samples", "0",
+                     "--no-energy"],
+                    {"GRAVSIM_RCCL_RANK_HOSTS": "1", "GRAVSIM_TEST_FAIL_GATED_AUDIT": "1"})
+    assert r.returncode == 0, r.stderr[-3000:]
+    c = out["config"]
+    if c["overlap_check"] and "overlap 0" in c["overlap_check"] and c["overlap_fallback"] is None:
+        pytest.skip("the race picked the ungated schedule: no gated run to fall back from")
+    fb = c["overlap_fallback"]
+    assert fb and fb["from_overlap"] == 3 and fb["to_overlap"] == 0
+    assert "injected" in fb["failures"][0]
+    assert c["overlap"] == 0 and out["work_audit"] == "ok"
+    assert out["audit"]["replay"] == "bitwise" and out["n_gpus"] == 2
