@@ -148,11 +148,17 @@ extern "C" int gs_sym_geometry(int64_t n_pad, int32_t* NC, int32_t* H, int32_t* 
     const int32_t v = atoi(e);
     if (v >= 1 && ((v <= 16 && (v & (v - 1)) == 0) || v % 16 == 0)) l = v;
   }
+  int32_t d = l < 16 ? 16 / l : 1;
+  // Tuning override (A/B only, changes the bits): parts of the diagonal chunk, 1 .. 16.
+  if (const char* e = getenv("GRAVSIM_SYM_D")) {
+    const int32_t v = atoi(e);
+    if (v >= 1 && v <= 16 && (v & (v - 1)) == 0) d = v;
+  }
   if (NC) *NC = nc;
   if (H) *H = h;
   if (L) *L = l;
   if (S) *S = (16 * h + l - 1) / l;
-  if (D) *D = l < 16 ? 16 / l : 1;
+  if (D) *D = d;
   return 0;
 }
 
@@ -257,12 +263,16 @@ extern "C" int64_t gs_sym_unit_map(int64_t n_pad, int32_t rank, int32_t nranks, 
   const int64_t total = (int64_t)rows * per;
   if (rows >= 32768 || per >= 65536) return 0;
   if (!out || cap < total) return -1;
+  // GRAVSIM_SYM_DIAG_TAIL=1 (A/B): the diagonal parts (one-sided, the shortest units) all go
+  // last instead of into the local prefix, to fill the launch's final wave.
+  const char* dte = getenv("GRAVSIM_SYM_DIAG_TAIL");
+  const bool diag_tail = dte && atoi(dte) != 0;
   std::vector<int32_t> nl(rows);
   std::vector<char> moved((size_t)total, 0);
   int64_t k = 0;
   for (int32_t r = 0; r < rows; ++r) {
     nl[r] = sym_local_segs(a0 + r, NC, a0, rows, L, S, parity);
-    for (int32_t q = 0; q < D && (fill < 0 || k < fill); ++q) {
+    for (int32_t q = 0; q < D && !diag_tail && (fill < 0 || k < fill); ++q) {
       out[k++] = (r << 16) | (S + q);
       moved[(size_t)r * per + S + q] = 1;
     }

@@ -368,9 +368,9 @@ __device__ __forceinline__ void force_sym_body(const SymArgs& a, int b) {
   const int seg_tiles = a.L * G::kTilesPerQuantum;
   TileSeq<T> seq{A, a.NC, a.real_chunks, 0, 0, diag};
   if (diag) {
-    const int q = s - a.S;
-    seq.u = q * seg_tiles;
-    seq.u1 = a.D > 1 ? seq.u + seg_tiles : G::kTilesPerChunk;
+    const int q = s - a.S, part = G::kTilesPerChunk / a.D;  // D parts of the diagonal chunk
+    seq.u = q * part;
+    seq.u1 = seq.u + part;
   } else {
     const int h_tiles = shell_len(A, a.NC, a.parity) * G::kTilesPerChunk;
     const int u0 = s * seg_tiles;
