@@ -36,14 +36,14 @@ grep '^{' $out/bench8_1m.log
 common="--n 40000 --device gpu --mode sym --log-format none --quiet"
 rm -f $out/m*.json
 timeout -k 10 240 python -m gravsim $common --steps 6 --nproc 2 --dump $out/p2.txt \
-  --checkpoint-dir $out/ck --checkpoint-every 3 --metrics-json $out/m2.json > $out/cli2.log 2>&1 \
+  --checkpoint-dir $out/ck --checkpoint-every 3 --metrics-json $out/m2.json --diagnostics > $out/cli2.log 2>&1 \
   || { tail -30 $out/cli2.log; exit 1; }
 timeout -k 10 240 python -m gravsim $common --steps 6 --dump $out/p1.txt \
   > $out/cli1.log 2>&1 || { tail -30 $out/cli1.log; exit 1; }
 timeout -k 10 240 python -m gravsim $common --steps 6 --nproc 3 --dump $out/p3.txt \
-  --metrics-json $out/m3.json > $out/cli3.log 2>&1 || { tail -30 $out/cli3.log; exit 1; }
+  --metrics-json $out/m3.json --diagnostics > $out/cli3.log 2>&1 || { tail -30 $out/cli3.log; exit 1; }
 timeout -k 10 300 python -m gravsim $common --steps 6 --nproc 8 --dump $out/p8.txt \
-  --metrics-json $out/m8.json > $out/cli8.log 2>&1 || { tail -30 $out/cli8.log; exit 1; }
+  --metrics-json $out/m8.json --diagnostics > $out/cli8.log 2>&1 || { tail -30 $out/cli8.log; exit 1; }
 ck3=$(ls $out/ck/*00000003* | head -1)
 timeout -k 10 240 python -m gravsim $common --steps 3 --resume "$ck3" --dump $out/pr.txt \
   > $out/clir.log 2>&1 || { tail -30 $out/clir.log; exit 1; }
@@ -52,10 +52,16 @@ cmp $out/p1.txt $out/p2.txt && cmp $out/p1.txt $out/p3.txt && cmp $out/p1.txt $o
   && echo "CLI dumps identical (P=1, 2, 3, 8; P=2 ckpt -> P=1 resume)" || exit 1
 python - $out/m2.json $out/m3.json $out/m8.json <<'PY' || exit 1
 import json, sys
+e0 = None
 for f in sys.argv[1:]:
     m = json.loads(open(f).read().splitlines()[-1])
     e = m["extra"]
     print(f, "nranks", m["nranks"], "overlap", e["overlap"], "graph", e["graph"],
           "segments", e["graph_segments"], "work_audit", e["work_audit"])
     assert e["overlap"] == 3 and e["graph"] == "segmented" and e["work_audit"] == "ok", e
+    c = e["conservation"]
+    print("   energy", c["energy_start"], "->", c["energy_end"], "momentum drift",
+          c["momentum_rel_drift"])
+    e0 = c["energy_start"] if e0 is None else e0
+    assert abs(c["energy_start"] - e0) <= 1e-10 * abs(e0), (c["energy_start"], e0)
 PY
