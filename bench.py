@@ -363,6 +363,11 @@ def main(argv=None) -> int:
         if cons0 is not None:
             conservation = conservation_summary(cons0, engine_conserved(eng, dist))
             conservation.pop("samples")
+            conservation["note"] = (
+                "KD (first order) at dt = 3600 s on uniform random ICs: a body passing close to "
+                "the point-mass Sun or to another body within one step changes the total energy "
+                "by orders of magnitude (the reference's configuration); the Newton-3 pairs keep "
+                "momentum and angular momentum at rounding level")
 
         # Comm/compute split (untimed): a few eager steps with per-step phase events.
         phase = None
