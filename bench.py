@@ -383,6 +383,7 @@ def main(argv=None) -> int:
         # timed run's bits (eager launches, one static unit per workgroup, no gating).
         replay = None
         if a.replay_audit:
+            cap = eng.dyn_cap
             eng.set_schedule(0, 0)
             eng.set_overlap(0)
             eng.init_ics("solar+random", cfg.seed)
@@ -394,8 +395,7 @@ def main(argv=None) -> int:
             replay = "bitwise" if not diff else f"differs on {int(diff)} rank(s)"
             if diff:
                 failures.append(f"replay: the independent schedule differs on {int(diff)} rank(s)")
-            eng.set_schedule((2 if a.graph_comm else 1) if a.graph else 0,
-                             int(os.environ.get("GRAVSIM_SYM_DYN_CAP", "4")))
+            eng.set_schedule((2 if a.graph_comm else 1) if a.graph else 0, cap)
             eng.set_overlap(overlap)
         return dict(wall=wall, ginfo=ginfo, mem=mem, hbm_max=hbm_max, failures=failures,
                     units=units, bad=bad, drift=drift, err_end=err_end,

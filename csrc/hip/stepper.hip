@@ -1052,6 +1052,7 @@ int gs_stepper_set_cutoff_mode(gs_stepper* s, int32_t mode) {
 }
 
 int32_t gs_stepper_get_overlap(gs_stepper* s) { return s->sym_overlap; }
+int32_t gs_stepper_get_dyn_cap(gs_stepper* s) { return s->dyn_cap; }
 
 int32_t gs_stepper_mem_entry(gs_stepper* s, int32_t i, const char** tag, uint64_t* bytes) {
   if (!s) return -1;

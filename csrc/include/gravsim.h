@@ -173,6 +173,8 @@ int gs_stepper_phase_stats(gs_stepper* s, double* out8);
 // (the default for nranks > 1; GRAVSIM_SYM_OVERLAP sets another initial value).
 int gs_stepper_set_overlap(gs_stepper* s, int32_t mode);
 int32_t gs_stepper_get_overlap(gs_stepper* s);
+// Units a dynamic-fetch workgroup may take after the first wave (<= 1: static units).
+int32_t gs_stepper_get_dyn_cap(gs_stepper* s);
 // Schedule knobs for an independent re-run (bench.py's replay audit): use_graph 0 eager,
 // 1 single-rank graphs, 2 multi-rank capture too; dyn_cap <= 1 static units (one per
 // workgroup), > 1 dynamic fetch with that many units per workgroup, < 0 unchanged.

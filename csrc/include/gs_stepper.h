@@ -111,7 +111,10 @@ struct gs_stepper {
   unsigned long long* utrace = nullptr;  // GRAVSIM_UNIT_TRACE: per force workgroup timeline
   // Dynamic unit fetch of the sym force launch (GRAVSIM_SYM_DYN_CAP; <= 1: static units):
   // units per workgroup after the first wave, and the first wave's size (resident slots).
-  int dyn_cap = 4;
+  // 2 (round 3): the shortest-lived dynamic workgroups shorten the launch tail; against 4:
+  // 1M / 8 per rank -1.0 %, P = 4 -0.4 %, 1M one GPU -0.2 %, 65K -1.4 %, same bits
+  // (profiles/r3s2_dyn_cap_ab.jsonl).
+  int dyn_cap = 2;
   int sym_first_wave = 0;
   int64_t utrace_main = 0;               // entries of the main launch (deferred ones follow)
   size_t emu_cap = 0;

@@ -157,6 +157,7 @@ def hip_lib():
         _sig(lib, "gs_stepper_set_overlap", c_int32, [S, c_int32])
         _sig(lib, "gs_stepper_set_schedule", c_int32, [S, c_int32, c_int32])
         _sig(lib, "gs_stepper_get_overlap", c_int32, [S])
+        _sig(lib, "gs_stepper_get_dyn_cap", c_int32, [S])
         _sig(lib, "gs_stepper_set_cutoff_mode", c_int32, [S, c_int32])
         _sig(lib, "gs_stepper_audit", c_int32, [S, POINTER(c_uint64), POINTER(c_uint64)])
         _sig(lib, "gs_stepper_audit_reset", c_int32, [S])

@@ -163,6 +163,11 @@ class HipEngine:
         """The sym schedule's overlap mode in force (3 by default for P > 1)."""
         return int(self.lib.gs_stepper_get_overlap(self._s))
 
+    @property
+    def dyn_cap(self) -> int:
+        """Units a dynamic-fetch workgroup may take after the first wave (<= 1: static)."""
+        return int(self.lib.gs_stepper_get_dyn_cap(self._s))
+
     def set_schedule(self, graph: int, dyn_cap: int = -1) -> None:
         """graph: 0 eager, 1 single-rank hipGraph replay, 2 multi-rank capture too;
         dyn_cap: <= 1 static force units (one per workgroup), > 1 dynamic unit fetch,
