@@ -748,6 +748,7 @@ int gs_stepper_create(const gs_config* cfg, gs_stepper** out) {
   if (const char* v = getenv("GRAVSIM_EMU_COMM_US")) s->emu_lat_us = atof(v);
   if (const char* v = getenv("GRAVSIM_EMU_COMM_WGS")) s->emu_wgs = atoi(v);
   if (const char* v = getenv("GRAVSIM_GATE_PROBE")) s->gate_probe = atoi(v);
+  if (s->esz == 8) s->dyn_cap = 4;  // fp64: 512K 101.9-102.0 ms at 4 vs 102.0-102.5 at 2
   if (const char* v = getenv("GRAVSIM_SYM_DYN_CAP")) s->dyn_cap = atoi(v);
   if (const char* v = getenv("GRAVSIM_SYM_DIAG_LAST")) s->diag_last = atoi(v);
   if (const char* v = getenv("GRAVSIM_SYM_FUSED_TAIL")) s->fuse_tail = atoi(v) != 0 ? 1 : 0;
