@@ -162,6 +162,17 @@ extern "C" int gs_sym_geometry(int64_t n_pad, int32_t* NC, int32_t* H, int32_t* 
   return 0;
 }
 
+extern "C" int32_t gs_sym_split_segments(int64_t n_pad) {
+  int32_t NC, H, L, S, D;
+  if (gs_sym_geometry(n_pad, &NC, &H, &L, &S, &D)) return 0;
+  int32_t kr = L >= 2 ? S / 16 : 0;
+  if (const char* e = getenv("GRAVSIM_SYM_KR")) {
+    const int32_t v = atoi(e);
+    if (v >= 0 && v <= S && (v == 0 || L >= 2)) kr = v;
+  }
+  return kr;
+}
+
 // Rows [a0, a0 + rows) of rank `rank` of `nranks` in the sym schedule: whole row blocks by
 // mpi.c's remainder rule (gs_common.h sym_blk_lo). Equal for every P dividing 8.
 extern "C" int gs_sym_rank_rows(int64_t n_pad, int32_t nranks, int32_t rank, int32_t* a0,
@@ -255,20 +266,34 @@ static int32_t sym_local_segs(int32_t A, int32_t NC, int32_t a0, int32_t rows, i
 // geometry, -1 on error (cap too small, bad arguments).
 extern "C" int64_t gs_sym_unit_map(int64_t n_pad, int32_t rank, int32_t nranks, int32_t parity,
                                    int64_t fill, int32_t* out, int64_t cap) {
+  return gs_sym_unit_map_kr(n_pad, rank, nranks, parity, fill, 0, out, cap);
+}
+
+// The same order with the last kr shell segments of every row split (gs_kernels.h SymArgs::Kr):
+// they leave the order above and are appended as two half units each (bit 30 set, bit 29 the
+// half), row by row, so the launch ends with half-length units. Rows < 8192 (13-bit field);
+// rows * (S + D + kr) entries.
+extern "C" int64_t gs_sym_unit_map_kr(int64_t n_pad, int32_t rank, int32_t nranks,
+                                      int32_t parity, int64_t fill, int32_t kr, int32_t* out,
+                                      int64_t cap) {
   int32_t NC, H, L, S, D, a0, rows;
-  if (nranks < 1 || rank < 0 || rank >= nranks || gs_sym_geometry(n_pad, &NC, &H, &L, &S, &D) ||
+  if (nranks < 1 || rank < 0 || rank >= nranks || kr < 0 ||
+      gs_sym_geometry(n_pad, &NC, &H, &L, &S, &D) ||
       gs_sym_rank_rows(n_pad, nranks, rank, &a0, &rows))
     return -1;
+  if (kr > S) return -1;
   const int32_t per = S + D;
-  const int64_t total = (int64_t)rows * per;
-  if (rows >= 32768 || per >= 65536) return 0;
+  const int64_t total = (int64_t)rows * (per + kr);
+  if (rows >= (kr > 0 ? 8192 : 32768) || per >= 65536) return 0;
   if (!out || cap < total) return -1;
   // GRAVSIM_SYM_DIAG_TAIL=1 (A/B): the diagonal parts (one-sided, the shortest units) all go
   // last instead of into the local prefix, to fill the launch's final wave.
   const char* dte = getenv("GRAVSIM_SYM_DIAG_TAIL");
   const bool diag_tail = dte && atoi(dte) != 0;
   std::vector<int32_t> nl(rows);
-  std::vector<char> moved((size_t)total, 0);
+  std::vector<char> moved((size_t)rows * per, 0);
+  for (int32_t r = 0; r < rows; ++r)  // split segments go to the end
+    for (int32_t u = S - kr; u < S; ++u) moved[(size_t)r * per + u] = 1;
   int64_t k = 0;
   for (int32_t r = 0; r < rows; ++r) {
     nl[r] = sym_local_segs(a0 + r, NC, a0, rows, L, S, parity);
@@ -276,7 +301,7 @@ extern "C" int64_t gs_sym_unit_map(int64_t n_pad, int32_t rank, int32_t nranks, 
       out[k++] = (r << 16) | (S + q);
       moved[(size_t)r * per + S + q] = 1;
     }
-    for (int32_t g = 0; g < nl[r] && (fill < 0 || k < fill); ++g) {
+    for (int32_t g = 0; g < nl[r] && g < S - kr && (fill < 0 || k < fill); ++g) {
       out[k++] = (r << 16) | g;
       moved[(size_t)r * per + g] = 1;
     }
@@ -287,6 +312,13 @@ extern "C" int64_t gs_sym_unit_map(int64_t n_pad, int32_t rank, int32_t nranks, 
         if (moved[(size_t)r * per + u]) continue;
         const bool remote = u < S && u >= nl[r];
         out[k++] = (int32_t)((remote ? 0x80000000u : 0u) | ((uint32_t)r << 16) | (uint32_t)u);
+      }
+  for (int32_t r = 0; r < rows; ++r)
+    for (int32_t u = S - kr; u < S; ++u)
+      for (uint32_t h = 0; h < 2; ++h) {
+        const bool remote = u >= nl[r];
+        out[k++] = (int32_t)((remote ? 0x80000000u : 0u) | 0x40000000u | (h << 29) |
+                             ((uint32_t)r << 16) | (uint32_t)u);
       }
   return k;
 }

@@ -265,13 +265,16 @@ __device__ __forceinline__ void run_tiles(const SymArgs& a, ISetK<T>& is, TileSe
 // a chain of dependent loads in front of every workgroup and cost 2 % of the step.
 // With the ring strategy (gate_n > 1) bits 28-30 hold the ring stage whose slice the unit
 // waits for and rows are < 4096 (layout.cpp gs_sym_unit_map_ring).
+// With split segments (Kr > 0, all-gather order) bit 30 marks a half unit, bit 29 its half,
+// and rows are < 8192 (layout.cpp gs_sym_unit_map_kr).
 __device__ __forceinline__ bool local_first_unit(const SymArgs& a, int b, int* br, int* s,
-                                                 int* stage) {
+                                                 int* stage, int* part) {
   const uint32_t m = (uint32_t)a.lf[b];
-  const bool ring = a.gate_n > 1;
-  *br = (int)((m >> 16) & (ring ? 0xfffu : 0x7fffu));
+  const bool ring = a.gate_n > 1, halves = a.Kr > 0 && !ring;
+  *br = (int)((m >> 16) & (ring ? 0xfffu : halves ? 0x1fffu : 0x7fffu));
   *s = (int)(m & 0xffffu);
   *stage = ring ? (int)((m >> 28) & 7u) : 0;
+  *part = halves && ((m >> 30) & 1u) ? (int)((m >> 29) & 1u) : -1;
   return (m >> 31) != 0u;
 }
 
@@ -311,9 +314,11 @@ __device__ __forceinline__ bool gate_open_or_defer(const SymArgs& a, int b, int 
 // was empty), from one lane, after the unit's partial stores. The host compares the count
 // with rows x (S + D) per step (bench.py work_audit), so a launch that silently skipped
 // units (a stale dynamic-fetch counter, a lost deferred unit) cannot pass as a fast step.
-__device__ __forceinline__ void audit_unit(const SymArgs& a) {
+// A split segment run whole counts its two halves (n = 2), so the count per step is
+// rows x (S + D + Kr) whichever way the segments run.
+__device__ __forceinline__ void audit_unit(const SymArgs& a, unsigned long long n = 1) {
   if (threadIdx.x == 0)
-    __hip_atomic_fetch_add(a.audit, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add(a.audit, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // One unit b (row a, segment s) per call; s == S is the row's diagonal chunk. b is the
@@ -326,12 +331,13 @@ __device__ __forceinline__ void force_sym_body(const SymArgs& a, int b) {
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   // Units per row: S shell segments, then D parts of the diagonal chunk.
   // br: row within the band (index into Pi/Pj/Pd); the rank's row is band0 + br.
-  int br, s, stage = 0;
+  // part: -1 a whole unit, 0 / 1 the first / second half of a split segment (Px).
+  int br, s, stage = 0, part = -1;
   bool gated = false;
   if (a.units == 6) {
-    gated = local_first_unit(a, b, &br, &s, &stage) && a.gate != nullptr;
+    gated = local_first_unit(a, b, &br, &s, &stage, &part) && a.gate != nullptr;
   } else if (a.units == 7) {  // deferred unit a.defer_index of the units-6 launch
-    local_first_unit(a, (int)a.defer[1 + a.defer_index], &br, &s, &stage);
+    local_first_unit(a, (int)a.defer[1 + a.defer_index], &br, &s, &stage, &part);
   } else if (a.units == 1) {
     br = b / a.D;
     s = a.S + b % a.D;
@@ -341,44 +347,55 @@ __device__ __forceinline__ void force_sym_body(const SymArgs& a, int b) {
   } else if (a.units == 0 && a.diag_last) {
     // Every unit: the shell segments row by row, then all diagonal parts. A diagonal part is
     // one-sided (about half the issue time of a shell segment), so dispatching them last fills
-    // the launch's final, partial wave of workgroups with short jobs.
-    const int shell = a.band_rows * a.S;
+    // the launch's final, partial wave of workgroups with short jobs. With split segments
+    // (Kr) the unsplit segments come first and the split ones last, as two half units each.
+    const int ns = a.S - a.Kr, shell = a.band_rows * ns, dg = a.band_rows * a.D;
     if (b < shell) {
-      br = b / a.S;
-      s = b % a.S;
-    } else {
+      br = b / ns;
+      s = b % ns;
+    } else if (b < shell + dg) {
       const int k = b - shell;
       br = k / a.D;
       s = a.S + k % a.D;
+    } else {
+      const int k = b - shell - dg;
+      part = k & 1;
+      br = (k >> 1) / a.Kr;
+      s = ns + (k >> 1) % a.Kr;
     }
   } else {  // the diagonal ones + the rank-local shell ones (5), or every unit row by row
     br = b / (a.S + a.D);
     s = b % (a.S + a.D);
   }
   const int A = a.a0 + a.band0 + br;
+  const bool diag = s >= a.S;
+  const bool split = !diag && s >= a.S - a.Kr;  // a split segment (two half sums)
+  const unsigned long long weight = split && part < 0 ? 2ull : 1ull;
   // Empty units (all-ghost row, segment past the row's shell) count as done for the work
   // audit, in exactly one of the launches that list them (units 4 and 5 both list shell
   // segments: the units-5 launch counts the empty ones).
   const bool count_empty = a.audit && a.units != 4;
   if ((int64_t)A * kSymC >= a.n_real) {  // all-ghost row: never read
-    if (count_empty) audit_unit(a);
+    if (count_empty) audit_unit(a, weight);
     return;
   }
-  const bool diag = s >= a.S;
   const int seg_tiles = a.L * G::kTilesPerQuantum;
   TileSeq<T> seq{A, a.NC, a.real_chunks, 0, 0, diag};
+  int u_lo = 0, u_mid = 0;  // shell: the segment's first tile and (split) its half point
   if (diag) {
-    const int q = s - a.S, part = G::kTilesPerChunk / a.D;  // D parts of the diagonal chunk
-    seq.u = q * part;
-    seq.u1 = seq.u + part;
+    const int q = s - a.S, plen = G::kTilesPerChunk / a.D;  // D parts of the diagonal chunk
+    seq.u = q * plen;
+    seq.u1 = seq.u + plen;
   } else {
     const int h_tiles = shell_len(A, a.NC, a.parity) * G::kTilesPerChunk;
     const int u0 = s * seg_tiles;
     if (u0 >= h_tiles) {  // past this row's shell: never read
-      if (count_empty) audit_unit(a);
+      if (count_empty) audit_unit(a, weight);
       return;
     }
     seq.u1 = min(u0 + seg_tiles, h_tiles);
+    u_lo = u0;
+    u_mid = min(u0 + seg_tiles / 2, seq.u1);
     if (a.units == 4 || a.units == 5) {
       // Rank-local: every j-chunk of the segment is one of the rank's own rows, so it needs
       // no gathered positions (chunks A+1 .. < a0 + rows: no wrap below NC).
@@ -398,30 +415,55 @@ __device__ __forceinline__ void force_sym_body(const SymArgs& a, int b) {
     is.x[i] = q.x; is.y[i] = q.y; is.z[i] = q.z; is.mu[i] = q.w;
     is.ax[i] = is.ay[i] = is.az[i] = std::remove_reference_t<decltype(is.ax[i])>(0);
   }
-  T* out;
+  // The i-side sum of the lane's bodies over the tiles just visited -> out; then restart.
+  auto store_i = [&](T* out) {
+#pragma unroll
+    for (int i = 0; i < G::I; ++i) {
+      const int b = w * G::kTileI + i * 64 + lane;
+      if constexpr (kJpack<T>) {  // slot-0 half + slot-1 half
+        out[b] = is.ax[i].x + is.ax[i].y;
+        out[kSymC + b] = is.ay[i].x + is.ay[i].y;
+        out[2 * kSymC + b] = is.az[i].x + is.az[i].y;
+      } else {
+        out[b] = is.ax[i];
+        out[kSymC + b] = is.ay[i];
+        out[2 * kSymC + b] = is.az[i];
+      }
+    }
+  };
   if (diag) {
     // Part of the 2048-body diagonal chunk, one-sided (self term 0 through the core, or
     // through the cutoff select in the exact path).
     run_tiles<T, false, EXACT>(a, is, seq, br, sm);
-    out = static_cast<T*>(a.Pd) + ((int64_t)br * a.D + (s - a.S)) * 3 * kSymC;
+    store_i(static_cast<T*>(a.Pd) + ((int64_t)br * a.D + (s - a.S)) * 3 * kSymC);
   } else {
-    run_tiles<T, true, EXACT>(a, is, seq, br, sm);
-    out = static_cast<T*>(a.Pi) + ((int64_t)br * a.S + s) * 3 * kSymC;
-  }
+    // One piece (the segment), or for a split segment its halves [u_lo, u_mid) -> Pi and
+    // [u_mid, end) -> Px: both (whole) or the one `part` names. One inlined copy of the tile.
+    T* const pi = static_cast<T*>(a.Pi) + ((int64_t)br * a.S + s) * 3 * kSymC;
+    T* const px = split ? static_cast<T*>(a.Px) +
+                              ((int64_t)br * a.Kr + (s - (a.S - a.Kr))) * 3 * kSymC
+                        : nullptr;
+    const int pc0 = split && part == 1 ? 1 : 0, pc1 = split && part != 0 ? 2 : 1;
+    const int u_end = seq.u1;
+#pragma unroll 1
+    for (int pc = pc0; pc < pc1; ++pc) {
+      TileSeq<T> sq = seq;
+      if (split) {
+        sq.u1 = pc == 0 ? u_mid : u_end;
+        sq.u = sq.valid(pc == 0 ? u_lo : u_mid);
+      }
+      if (pc > pc0) {
 #pragma unroll
-  for (int i = 0; i < G::I; ++i) {
-    const int b = w * G::kTileI + i * 64 + lane;
-    if constexpr (kJpack<T>) {  // slot-0 half + slot-1 half
-      out[b] = is.ax[i].x + is.ax[i].y;
-      out[kSymC + b] = is.ay[i].x + is.ay[i].y;
-      out[2 * kSymC + b] = is.az[i].x + is.az[i].y;
-    } else {
-      out[b] = is.ax[i];
-      out[kSymC + b] = is.ay[i];
-      out[2 * kSymC + b] = is.az[i];
+        for (int i = 0; i < G::I; ++i)
+          is.ax[i] = is.ay[i] = is.az[i] = std::remove_reference_t<decltype(is.ax[i])>(0);
+      }
+      run_tiles<T, true, EXACT>(a, is, sq, br, sm);
+      store_i(pc == 0 ? pi : px);
+      if (pc + 1 < pc1) __syncthreads();  // the next piece restages the LDS tiles and slots
+
     }
   }
-  if (a.audit) audit_unit(a);
+  if (a.audit) audit_unit(a, weight);
   if (a.utrace && threadIdx.x == 0) {
     // hwreg(HW_ID) whole register, hwreg(XCC_ID) bits 3:0 (ids 4 and 20 on gfx9.4+)
     const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);
@@ -706,16 +748,23 @@ __global__ __launch_bounds__(256) void sym_row_reduce_kernel(SymArgs a) {
   const int segs = (16 * h + a.L - 1) / a.L;  // shell length in 128-body quanta / L
   const T* __restrict__ p = static_cast<const T*>(a.Pi) + (int64_t)br * a.S * 3 * kSymC +
                             k * kSymC + c;
+  const int ns = min(segs, a.S - a.Kr);  // unsplit segments; then split ones: Pi + Px
   constexpr int U = 8;
   int s = 0;
-  for (; s + U <= segs; s += U) {
+  for (; s + U <= ns; s += U) {
     T v[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) v[u] = __builtin_nontemporal_load(p + (int64_t)(s + u) * 3 * kSymC);
 #pragma unroll
     for (int u = 0; u < U; ++u) acc += v[u];
   }
-  for (; s < segs; ++s) acc += __builtin_nontemporal_load(p + (int64_t)s * 3 * kSymC);
+  for (; s < ns; ++s) acc += __builtin_nontemporal_load(p + (int64_t)s * 3 * kSymC);
+  if (s < segs) {
+    const T* __restrict__ px = static_cast<const T*>(a.Px) + (int64_t)br * a.Kr * 3 * kSymC +
+                               k * kSymC + c - (int64_t)(a.S - a.Kr) * 3 * kSymC;
+    for (; s < segs; ++s)
+      acc += p[(int64_t)s * 3 * kSymC] + px[(int64_t)s * 3 * kSymC];
+  }
   static_cast<T*>(a.Ti)[(int64_t)k * a.n_local + (int64_t)(a.band0 + br) * kSymC + c] = acc;
 }
 
@@ -798,16 +847,22 @@ __global__ __launch_bounds__(192) void sym_tail_kernel(SymArgs a) {
     for (int q = 1; q < a.D; ++q) ti += pd[q * 3 * kSymC];
     const int segs = (16 * shell_len(X, a.NC, a.parity) + a.L - 1) / a.L;
     const T* pi = static_cast<const T*>(a.Pi) + (int64_t)br * a.S * 3 * kSymC + k * kSymC + c;
+    const int ns = min(segs, a.S - a.Kr);
     constexpr int U = 8;
     int sg = 0;
-    for (; sg + U <= segs; sg += U) {
+    for (; sg + U <= ns; sg += U) {
       T v[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) v[u] = __builtin_nontemporal_load(pi + (int64_t)(sg + u) * 3 * kSymC);
 #pragma unroll
       for (int u = 0; u < U; ++u) ti += v[u];
     }
-    for (; sg < segs; ++sg) ti += __builtin_nontemporal_load(pi + (int64_t)sg * 3 * kSymC);
+    for (; sg < ns; ++sg) ti += __builtin_nontemporal_load(pi + (int64_t)sg * 3 * kSymC);
+    if (sg < segs) {  // split segments: the two half sums (sym_row_reduce_kernel order)
+      const T* px = static_cast<const T*>(a.Px) + (int64_t)br * a.Kr * 3 * kSymC + k * kSymC + c -
+                    (int64_t)(a.S - a.Kr) * 3 * kSymC;
+      for (; sg < segs; ++sg) ti += pi[(int64_t)sg * 3 * kSymC] + px[(int64_t)sg * 3 * kSymC];
+    }
     // + S: the tree over the B row blocks (sym_node_reduce_kernel's single node [0, B))
     TreeAcc<T, 1> t;
     t.pos = 0;
@@ -860,6 +915,10 @@ template <typename T>
 hipError_t launch_force_sym_t(const SymArgs& a, hipStream_t s) {
   int units = a.band_rows * (a.units == 1 ? a.D : (a.units == 2 || a.units == 4) ? a.S
                                                                                  : a.S + a.D);
+  // units 0 (diagonal parts last) and the all-gather units 6 order list every split segment
+  // as two half units at their end
+  if (a.Kr > 0 && ((a.units == 0 && a.diag_last) || (a.units == 6 && a.gate_n <= 1)))
+    units += a.band_rows * a.Kr;
   if (a.units >= 6 && (a.band_rows != a.rows || !a.lf)) return hipErrorInvalidValue;
   if (a.units == 7) units = a.defer_grid;  // strided walk over the deferred list
   if (units <= 0) return hipSuccess;

@@ -105,6 +105,12 @@ int32_t gs_sym_shell_len(int32_t A, int32_t NC, int32_t parity);
 // Unit order of the gated sym launch for one rank (see layout.cpp); returns the entry count.
 int64_t gs_sym_unit_map(int64_t n_pad, int32_t rank, int32_t nranks, int32_t parity,
                         int64_t fill, int32_t* out, int64_t cap);
+// ... with the last kr shell segments of every row split into two half units at the end.
+int64_t gs_sym_unit_map_kr(int64_t n_pad, int32_t rank, int32_t nranks, int32_t parity,
+                           int64_t fill, int32_t kr, int32_t* out, int64_t cap);
+// Split shell segments per row (SymArgs::Kr) for a geometry: S / 16 when a segment has at
+// least 2 tiles of 128 bodies (L >= 2), else 0; GRAVSIM_SYM_KR overrides (changes the bits).
+int32_t gs_sym_split_segments(int64_t n_pad);
 // The same for the ring strategy: entries carry the ring stage (bits 28-30) at which the last
 // slice a unit reads arrives, and units are ordered by stage (rows < 4096, nranks <= 8).
 int64_t gs_sym_unit_map_ring(int64_t n_pad, int32_t rank, int32_t nranks, int32_t parity,

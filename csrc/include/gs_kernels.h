@@ -60,6 +60,13 @@ struct SymArgs {
   void* Pi;            // [rows][S][3][kSymC] i-side partials (segment = L quanta of 128)
   void* Pj;            // [rows][H][3][kSymC] j-side partials, H = NC / 2
   void* Pd;            // [rows][D][3][kSymC] diagonal-chunk partials
+  // Split segments (the launch tail): the last Kr shell segments of every row are summed as
+  // two halves of their tiles, h1 in Pi and h2 in Px[rows][Kr][3][kSymC]; the row reduce adds
+  // Pi + Px for them. A designated segment runs whole (both halves, one workgroup) or as two
+  // half units (entries at the end of the units 0 / units 6 orders, so the launch's last
+  // units are half as long); either way the same two sums, so the same bits.
+  void* Px;
+  int32_t Kr;
   void* Ti;            // [3][n_local] per-body i-side total: sum_q Pd[q] + sum_s Pi[s]
   void* Sbuf;          // [dest rank q][own node k < nn][3][n_local(q)] node sums by destination
   const void* Rbuf;    // [node j, all ranks' nodes in global order][3][n_local] received

@@ -88,11 +88,13 @@ struct gs_stepper {
   char* sym_Pi = nullptr;  // element type: float or double (esz)
   char* sym_Pj = nullptr;
   char* sym_Pd = nullptr;
+  char* sym_Px = nullptr;  // second halves of the split segments [band][Kr][3][kSymC]
   char* sym_S = nullptr;  // node sums by destination rank
   char* sym_R = nullptr;  // node sums of every rank, global node order (== sym_S, one rank)
   char* sym_Ti = nullptr;  // per-body i-side totals [3][n_local]
   char* sym_Bb = nullptr;  // multi-band runs: per-block leaf sums [own blocks][3][bodies]
   int32_t sym_NC = 0, sym_H = 0, sym_L = 0, sym_S_n = 0, sym_D = 1;
+  int32_t sym_Kr = 0;    // split shell segments per row (gs_sym_split_segments)
   int32_t sym_band = 0;  // rows per band (Pi/Pj/Pd hold one band; a multiple of sym_RB)
   // Row blocks and reduction-tree nodes (gs_sym_nodes): rank q owns blocks
   // [blk_lo[q], blk_lo[q + 1]) = bodies [rbeg[q], rbeg[q] + rcnt[q]); it sends nn(q) nodes,

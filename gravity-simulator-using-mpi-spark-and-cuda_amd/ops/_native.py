@@ -94,6 +94,9 @@ def _declare_common(lib) -> None:
                                            POINTER(c_int32), c_int64])
     _sig(lib, "gs_sym_unit_map_ring", c_int64, [c_int64, c_int32, c_int32, c_int32, c_int64,
                                                 POINTER(c_int32), c_int64])
+    _sig(lib, "gs_sym_unit_map_kr", c_int64, [c_int64, c_int32, c_int32, c_int32, c_int64,
+                                              c_int32, POINTER(c_int32), c_int64])
+    _sig(lib, "gs_sym_split_segments", c_int32, [c_int64])
     _sig(lib, "gs_auto_chunk", c_int32, [c_int64])
     _sig(lib, "gs_ic_fill_host", None, [c_int32, c_uint64, c_int64, c_int64, c_int64, _PD, _PD,
                                         _PD])

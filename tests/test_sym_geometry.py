@@ -197,3 +197,43 @@ def test_node_merge_equals_full_tree_bitwise_for_every_P(B):
                 for rn in partition.sym_nodes(n_pad, P) for lo, l in rn]
         got = _counter_merge(vals)
         assert np.array_equal(got.view(np.uint32), full.view(np.uint32)), P
+
+
+@pytest.mark.parametrize("n_pad,P", [(65536, 1), (65536, 8), (1 << 20, 1), (1 << 20, 8),
+                                     (1 << 20, 3), (262144, 6)])
+def test_split_segment_map(n_pad, P):
+    """The last Kr shell segments of every row (Kr = S / 16 when a segment has >= 2 tiles) are
+    split: the gated order lists every other unit once and each split segment as two half
+    units (bit 30, half in bit 29) at the very end, with the segment's locality flag."""
+    lib, g = _geo(n_pad)
+    S, D = g["S"], g["D"]
+    kr = lib.gs_sym_split_segments(n_pad)
+    assert kr == (S // 16 if g["L"] >= 2 else 0)
+    for rank in (0, P - 1):
+        a0, rows = partition.sym_rank_rows(n_pad, P, rank)
+        plain = (ctypes.c_int32 * (rows * (S + D)))()
+        assert lib.gs_sym_unit_map(n_pad, rank, P, 1, 1024, plain, len(plain)) == rows * (S + D)
+        out = (ctypes.c_int32 * (rows * (S + D + kr)))()
+        n = lib.gs_sym_unit_map_kr(n_pad, rank, P, 1, 1024, kr, out, len(out))
+        assert n == rows * (S + D + kr)
+        m = np.frombuffer(out, dtype=np.uint32)
+        half = ((m >> 30) & 1).astype(bool)
+        part = (m >> 29) & 1
+        row = (m >> 16) & 0x1FFF
+        unit = m & 0xFFFF
+        n_half = rows * kr * 2
+        assert half[len(m) - n_half:].all() and not half[:len(m) - n_half].any()  # at the end
+        whole = unit[~half].astype(np.int64) + row[~half].astype(np.int64) * (S + D)
+        expect = [r * (S + D) + u for r in range(rows) for u in range(S + D)
+                  if not (S - kr <= u < S)]
+        assert np.array_equal(np.sort(whole), np.array(expect, dtype=np.int64))
+        hk = (row[half].astype(np.int64) * S + unit[half]) * 2 + part[half]
+        want = sorted((r * S + u) * 2 + h for r in range(rows) for u in range(S - kr, S)
+                      for h in (0, 1))
+        assert np.array_equal(np.sort(hk), np.array(want, dtype=np.int64))
+        # a split segment's halves carry its locality (remote = reads gathered rows)
+        pm = np.frombuffer(plain, dtype=np.uint32)
+        rem_plain = {(int((x >> 16) & 0x7FFF), int(x & 0xFFFF)): bool(x >> 31) for x in pm}
+        for x in m[half]:
+            key = (int((x >> 16) & 0x1FFF), int(x & 0xFFFF))
+            assert bool(x >> 31) == rem_plain[key]
