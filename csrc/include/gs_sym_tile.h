@@ -418,6 +418,17 @@ struct ISetP {
 #ifndef GS_SYM_PIPE
 #define GS_SYM_PIPE 2
 #endif
+// Instruction kinds that may cross the group / step barriers (0: none; 0x0406: VALU, SALU,
+// TRANS). Closing the step regions completely measured -1.0 % against letting ALU work cross
+// them (1M 159.98-160.00 vs 161.48-161.66 ms, 65K 0.694 vs 0.700-0.702 ms, same bits;
+// letting TRANS cross the group barriers instead: 159.7 vs 161.2 ms;
+// profiles/r3s2_barrier_mask_ab.jsonl).
+#ifndef GS_SYM_GROUP_MASK
+#define GS_SYM_GROUP_MASK 0
+#endif
+#ifndef GS_SYM_STEP_MASK
+#define GS_SYM_STEP_MASK 0
+#endif
 #ifndef GS_SYM_UP
 #define GS_SYM_UP 4
 #endif
@@ -490,7 +501,7 @@ __device__ __forceinline__ void meet_jp(ISetP<I>& a, f2 xj, f2 yj, f2 zj, f2 mj,
       }
     }
 #if GS_SYM_PIPE >= 2
-    __builtin_amdgcn_sched_barrier(0);  // one i-group's temporaries live at a time
+    __builtin_amdgcn_sched_barrier(GS_SYM_GROUP_MASK);  // one i-group's temporaries at a time
 #endif
   }
 }
@@ -513,7 +524,7 @@ __device__ __forceinline__ void lds_step_jp(ISetP<I>& a, CSetT<float, 2>& c, con
 }
 
 // GS_SYM_PIPE >= 1: step K reads step K+1's j-pair from LDS before its own arithmetic, and a
-// scheduling barrier keeps every ds_read inside its step (ALU may still cross it).
+// scheduling barrier closes the step (GS_SYM_STEP_MASK), so every ds_read stays inside it.
 template <int I, bool SYM, bool EXACT, int K>
 __device__ __forceinline__ void lds_step_jp_pipe(ISetP<I>& a, CSetT<float, 2>& c,
                                                  const float4* base, float4& p, float4& q,
@@ -538,7 +549,7 @@ __device__ __forceinline__ void lds_step_jp_pipe(ISetP<I>& a, CSetT<float, 2>& c
     p = pn;
     q = qn;
   }
-  __builtin_amdgcn_sched_barrier(0x0406);  // VALU, SALU, TRANS may cross; LDS and VMEM not
+  __builtin_amdgcn_sched_barrier(GS_SYM_STEP_MASK);  // closes the step (LDS reads stay in it)
 }
 
 template <int I, bool SYM, bool EXACT, int... Ks>
