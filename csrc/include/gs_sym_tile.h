@@ -314,6 +314,10 @@ __device__ __forceinline__ int staged_entry(int lane_src, int copy) {
 #ifndef GS_SYM_PIPE64
 #define GS_SYM_PIPE64 1
 #endif
+// (A/B) what may cross the fp64 step barrier: 0x0406 VALU, SALU, TRANS (default); 0 nothing
+#ifndef GS_SYM_STEP_MASK64
+#define GS_SYM_STEP_MASK64 0x0406
+#endif
 // fp64 pair arithmetic (no packed f64 VALU on gfx950): the integrator's own fp64 formula
 // (nbody_kernels.hip interact, step path): y0 = v_rsq_f64(r^2), e = 1 - r^2 y0^2,
 // r^-3 = y0^3 (1 + 3/2 e + 15/8 e^2) with |e| <= 1.1e-7, i.e. double-precision r^-3;
@@ -601,7 +605,7 @@ __device__ __forceinline__ void lds_step_pipe(ISetT<T, I>& a, CSetT<T, 1>& c, co
     c.cz[0] = row_from<1>(c.cz[0]) - tz;
   }
   if constexpr (K + 1 < 16) q = qn;
-  __builtin_amdgcn_sched_barrier(0x0406);  // VALU, SALU, TRANS may cross; LDS and VMEM not
+  __builtin_amdgcn_sched_barrier(GS_SYM_STEP_MASK64);  // LDS and VMEM stay in the step
 }
 
 template <typename T, int I, int J, bool SYM, bool EXACT, int... Ks>
