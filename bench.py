@@ -26,20 +26,29 @@ N * K / max_rank(wall).
 
 Audits of the timed work (outside the timed region; the run exits non-zero if one fails):
   * unit count: the sym force kernels count every unit they run on device; after the loop
-    each rank must have run exactly rows x (S + D) units per timed step;
+    each rank must have run exactly rows x (S + D + Kr) units per timed step (a split segment
+    counts as its two halves);
   * replay: the same warmup + K steps are re-run from the same ICs on an independent
     schedule (eager launches, one static unit per workgroup, ungated) and must give the
     same bits on every rank.
 If the gated local-first launch (--overlap auto picked 3 after its 2-step self-check) fails
-them, the run says so in config.overlap_fallback and times the ungated schedule from the
-same ICs instead, which must pass the same audits.
+them, that is a failure of the multi-rank default: the ungated schedule is timed from the same
+ICs (config.overlap_fallback), but work_audit reports the failure and the run exits 1.
 Also outside it: the sampled accuracy of the step's own accelerations at step 0 and after
 the last timed step, the relative drift of total momentum over the run, the drift of total
 energy (kinetic + exact-cutoff potential) and angular momentum (two O(N^2) passes), a few
-eager steps with phase events for the comm split, and the reference's exact hard-cutoff
-select timed on its own (exact_cutoff_ms_per_step). Multi-rank runs record per rank the device
-it bound and the RCCL transports its connections used (parsed from RCCL's INFO log, sent to a
-file).
+steps with phase events for the comm split (multi-rank: replayed from the same segmented plan
+as the timed loop), and the reference's exact hard-cutoff select timed on its own
+(exact_cutoff_ms_per_step). Multi-rank runs record per rank the device it bound and the RCCL
+transports its connections used (parsed from RCCL's INFO log, sent to a file).
+
+Bounded and self-reporting (gravsim/parallel/guard.py): every stage (gloo init, device,
+engine, RCCL init + warm-up, first step, overlap check, warmup, timed, audits, ...) has a
+deadline (--init-timeout for start-up; afterwards derived from the first measured step), and
+the native step timeout is max(60 s, 20 x the first step), at most 240 s. A stall or a failure
+on any rank ends the job within that budget with ONE error JSON line from rank 0 ("status":
+"error", the stage reached, each rank's stage, device, RCCL transports and communicator init
+stage, HSA_ENABLE_IPC_MODE_LEGACY) and exit code 70, after aborting the RCCL communicator.
 """
 from __future__ import annotations
 
@@ -86,8 +95,9 @@ def parse(argv=None) -> argparse.Namespace:
     ap.add_argument("--check-samples", type=int, default=256,
                     help="bodies whose step-0 accelerations are checked against an fp64 row "
                          "sum on the host (0 = skip)")
-    ap.add_argument("--phase-steps", type=int, default=3,
-                    help="eager steps with phase events after the timed loop (comm split)")
+    ap.add_argument("--phase-steps", type=int, default=4,
+                    help="steps with phase events after the timed loop (the comm split), on "
+                         "the timed loop's schedule (multi-rank: the segmented plan)")
     ap.add_argument("--no-replay-audit", dest="replay_audit", action="store_false",
                     help="skip the independent-schedule re-run of the timed steps")
     ap.add_argument("--no-energy", dest="energy", action="store_false",
@@ -96,55 +106,48 @@ def parse(argv=None) -> argparse.Namespace:
     ap.add_argument("--exact-steps", type=int, default=3,
                     help="steps timed with the reference's exact cutoff select after the "
                          "headline (0 = skip)")
+    ap.add_argument("--init-timeout", type=float, default=180.0,
+                    help="seconds each start-up stage (gloo, device, engine, RCCL init and "
+                         "warm-up, the first step) may take before the run is stopped with an "
+                         "error JSON line")
+    ap.add_argument("--step-timeout", type=float, default=0.0,
+                    help="native progress bound: abort RCCL and stop with an error JSON line "
+                         "when no step completes for this long (0: max(--step-timeout-min, "
+                         "20 x the first measured step), at most 240 s)")
+    ap.add_argument("--step-timeout-min", type=float, default=60.0,
+                    help="floor of the derived step timeout")
     return ap.parse_args(argv)
 
 
-def rccl_log_setup() -> str | None:
-    """Route RCCL's INFO log to a private per-rank file (before any RCCL call; stdout stays
-    rank 0's JSON line) so the transport each connection used can be reported. A level the
-    user set (NCCL_DEBUG=WARN...) is raised to INFO for the file; its WARN lines are echoed
-    to stderr afterwards. Left alone when the user already chose a log file."""
+def rccl_log_setup(directory: str, rank: int) -> str | None:
+    """Route RCCL's INFO log to a per-rank file in the job's guard directory (before any RCCL
+    call; stdout stays rank 0's JSON line), so the transport each connection used can be
+    reported, by this rank after init and by rank 0's guard if the run stalls. A level the
+    user set (NCCL_DEBUG=WARN...) is raised to INFO for the file; its WARN lines are echoed to
+    stderr afterwards. Left alone when the user already chose a log file."""
     if "NCCL_DEBUG_FILE" in os.environ:
         return None
-    d = tempfile.mkdtemp(prefix="gravsim_rccl_")
     os.environ["GRAVSIM_USER_NCCL_DEBUG"] = os.environ.get("NCCL_DEBUG", "")
     os.environ["NCCL_DEBUG"] = "INFO"
     os.environ["NCCL_DEBUG_SUBSYS"] = "INIT,P2P,NET"
-    os.environ["NCCL_DEBUG_FILE"] = os.path.join(d, "rccl.log")
+    os.environ["NCCL_DEBUG_FILE"] = os.path.join(directory, f"rccl.{rank}.log")
     return os.environ["NCCL_DEBUG_FILE"]
 
 
 def rccl_transports(path: str | None) -> dict:
     """Transports of this rank's RCCL connections ("Channel .. via P2P/IPC", "NET/Socket",
-    "SHM"...) and the RCCL version, from the INFO log; the file is removed afterwards."""
-    out = {"transports": None, "rccl_version": None, "net": None}
+    "SHM"...) and the RCCL version, from the INFO log; its WARN lines go to stderr."""
+    from gravsim.parallel.guard import parse_rccl_log
+
     if not path:
-        out["rccl_log"] = "NCCL_DEBUG_FILE set by the user: not parsed"
-        return out
-    if not os.path.exists(path):
-        out["rccl_log"] = f"no RCCL log written at {path}"
-        return out
-    seen, net = set(), set()
-    lines = 0
-    with open(path, errors="replace") as f:
-        for line in f:
-            lines += 1
-            if " WARN " in line:
-                sys.stderr.write(line)
-            m = re.search(r" via (\S+)", line)
-            if m and "Channel" in line:
-                seen.add(re.sub(r"/\d+$", "", m.group(1)))
-            m = re.search(r"(?:RCCL|NCCL) version[ :]+(\S+)", line)
-            if m and out["rccl_version"] is None:
-                out["rccl_version"] = m.group(1)
-            m = re.search(r"Using network (\S+)", line)
-            if m:
-                net.add(m.group(1))
-    out["transports"] = sorted(seen)
-    out["net"] = sorted(net) or None
-    out["rccl_log"] = f"{lines} lines"
-    shutil.rmtree(os.path.dirname(path), ignore_errors=True)
-    return out
+        return {"transports": None, "rccl_version": None, "net": None,
+                "rccl_log": "NCCL_DEBUG_FILE set by the user: not parsed"}
+    if os.path.exists(path):
+        with open(path, errors="replace") as f:
+            for line in f:
+                if " WARN " in line:
+                    sys.stderr.write(line)
+    return parse_rccl_log(path)
 
 
 def device_record(dev: int) -> dict:
@@ -211,43 +214,42 @@ def sampled_error(eng, cfg, samples: int, seed: int = 7) -> float:
 
 
 def overlap_self_check(eng, cfg, dist, comm, steps: int = 2):
-    """Run `steps` steps from the benchmark ICs with the ungated sym schedule (overlap 0) and
-    with the gated local-first launch (overlap 3), on every rank; if both give the same bits
-    everywhere (they evaluate the same units into the same slots: docs/DESIGN.md §7), keep
-    the faster of the two in an alternating race. Untimed. Returns (mode, verdict)."""
-    import numpy as np
+    """The gated local-first launch (overlap 3) against the ungated schedule (0): same bits
+    from the benchmark ICs on every rank after `steps` steps, then the faster of the two in an
+    alternating race (runtime/selfcheck.py). Untimed. Returns (mode, verdict)."""
+    from gravsim.runtime.selfcheck import gated_self_check
 
-    out = []
-    for ov in (0, 3):
-        eng.set_overlap(ov)
-        eng.init_ics("solar+random", cfg.seed)
-        eng.step(steps)
-        eng.sync()
-        b = eng.state()
-        own = eng.layout.real_local
-        out.append((b.pos[own.start:own.stop].copy(), b.vel[own.start:own.stop].copy()))
-    same = all(np.array_equal(x, y) for x, y in zip(out[0], out[1]))
-    bad = comm.allreduce_sum(dist, 0.0 if same else 1.0)
-    if bad:
-        return 0, f"gated launch differed from the ungated one on {int(bad)} rank(s): overlap 0"
-    # Same bits either way, so keep whichever is faster on THIS node's interconnect (the
-    # gated launch won under modeled comm, but real RCCL kernels compete for CUs
-    # differently): alternating untimed races, slowest rank's wall per mode.
     race = 3 if cfg.n <= (4 << 20) else 1
-    wall = {0: 0.0, 3: 0.0}
-    for ov in (0, 3, 0, 3):
-        eng.set_overlap(ov)
-        eng.step(1)
-        eng.sync()
-        comm.barrier(dist)
-        t0 = time.perf_counter()
-        eng.step(race)
-        eng.sync()
-        wall[ov] += comm.allreduce_max(dist, time.perf_counter() - t0)
-    ms = {ov: 1e3 * w / (2 * race) for ov, w in wall.items()}
-    pick = 3 if ms[3] <= ms[0] else 0
-    return pick, (f"gated == ungated bitwise after {steps} steps on every rank; race "
-                  f"{ms[0]:.3f} ms ungated vs {ms[3]:.3f} ms gated per step: overlap {pick}")
+    mode, verdict, _ = gated_self_check(eng, dist, comm,
+                                        lambda: eng.init_ics("solar+random", cfg.seed),
+                                        steps=steps, race=race)
+    return mode, verdict
+
+
+def launch_info() -> dict:
+    from gravsim.parallel import launch
+
+    return {"probe_devices": int(os.environ[launch.PROBE_ENV])
+            if os.environ.get(launch.PROBE_ENV) else None,
+            "rehearsal_rank_hosts": os.environ.get("GRAVSIM_RCCL_RANK_HOSTS") == "1",
+            "HSA_ENABLE_IPC_MODE_LEGACY": os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY")}
+
+
+DATA = "synthetic: seeded Sun/Earth/Mars + uniform random bodies (device RNG)"
+MODEL = "direct-sum N-body, KD (symplectic Euler) integrator, cutoff 1e-10 m"
+
+
+def error_line(a, world: int, reason: str, records: list) -> dict:
+    """Rank 0's JSON line when the run is stopped (parallel/guard.py): the metric line with no
+    value, "status": "error", the stage reached and every rank's record (stage, seconds in it,
+    device, RCCL transports so far, the native communicator's init stage, error)."""
+    return {"metric": METRIC, "value": None, "unit": "body-updates/s", "n_gpus": world,
+            "steps": a.steps, "warmup": a.warmup, "ms_per_step": None, "higher_is_better": True,
+            "scaling": "strong", "vs_baseline": None, "dtype": a.dtype, "data": DATA,
+            "status": "error", "error": reason,
+            "stage": records[0].get("stage") if records else None, "work_audit": "not run",
+            "config": {"model": MODEL, "n_bodies": a.n, "global_batch": a.n, "seq_len": 1,
+                       "dt": a.dt, "ranks": records, "launch": launch_info()}}
 
 
 def main(argv=None) -> int:
@@ -264,20 +266,42 @@ def main(argv=None) -> int:
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE {world_env}: run one rank per GPU "
                          "(torch.distributed.run --nproc-per-node must equal --gpus)")
 
+    import gravsim  # noqa: F401
+    from gravsim.parallel import guard as gd
+
+    world = max(1, world_env)
+    # Every stage of the run has a deadline; a stall or a failure on any rank ends the job
+    # with rank 0's error JSON line instead of an external kill with no record.
+    g = gd.RunGuard(int(os.environ.get("RANK", "0") or 0), world,
+                    lambda reason, recs: error_line(a, world, reason, recs))
+    try:
+        rc = run(a, g)
+    except (Exception, SystemExit) as e:  # noqa: BLE001 - every failure becomes a report
+        if isinstance(e, SystemExit) and e.code in (0, None):
+            raise
+        g.fail(f"{type(e).__name__}: {e}")
+    g.close()
+    return rc
+
+
+def run(a, g) -> int:
     import numpy as np
     import torch
 
-    import gravsim  # noqa: F401
     from gravsim.config import SimConfig
     from gravsim.ops import _native
-    from gravsim.parallel import comm, launch
+    from gravsim.parallel import comm
+    from gravsim.parallel import guard as gd
     from gravsim.runtime.engines import HipEngine
     from gravsim.runtime.simulation import conservation_summary, engine_conserved
 
-    dist = comm.init()
+    init_b = a.init_timeout
+    g.stage("gloo_init", init_b)
+    dist = comm.init(timeout_s=max(init_b, 120.0))
     world, rank = dist.world, dist.rank
     if world != a.gpus:
         raise SystemExit(f"--gpus {a.gpus} but the job has {world} rank(s)")
+    g.stage("device", init_b)
     if not torch.cuda.is_available():
         raise SystemExit("bench.py needs a HIP device (MI355X)")
     ndev = torch.cuda.device_count()
@@ -285,45 +309,80 @@ def main(argv=None) -> int:
         raise SystemExit(f"{world} ranks but {ndev} visible GPU(s)")
     dev = dist.local_rank % ndev
     torch.cuda.set_device(dev)
+    g.note(**device_record(dev))
 
     cfg = SimConfig(n=a.n, dt=a.dt, dtype=a.dtype, device="gpu", kernel=a.kernel, mode=a.mode,
                     ipl=a.ipl, graph=a.graph, graph_comm=a.graph_comm,
-                    cutoff_mode=a.cutoff_mode, strategy=a.strategy).validate()
-    rccl_log = rccl_log_setup() if world > 1 else None  # before the first RCCL call
+                    cutoff_mode=a.cutoff_mode, strategy=a.strategy,
+                    step_timeout_s=init_b).validate()
+    rccl_log = rccl_log_setup(g.dir, rank) if world > 1 else None  # before the first RCCL call
+    g.note(rccl_log_path=rccl_log)
+    g.stage("engine", init_b)
     eng = HipEngine(cfg, rank, world, device=dev, dist=dist)
+    g.on_abort(eng.abort)
+    g.probe(lambda: {"comm_stage": eng.comm_stage()})
     ranks_info = None
     if world > 1:
+        g.stage("rccl_uid", init_b)
         uid = HipEngine.unique_id() if rank == 0 else None
-        eng.comm_init(comm.broadcast_bytes(dist, uid))
+        uid = comm.broadcast_bytes(dist, uid)
+        g.stage("comm_init", init_b)  # ncclCommInitRank + warm-up of every connection
+        eng.comm_init(uid)
+        g.stage("rank_info", init_b)
         rec = {"rank": rank, **device_record(dev), **rccl_transports(rccl_log)}
         ranks_info = comm.allgather_object(dist, rec)
+
+    # One eager step from the ICs: its time bounds every later stage, and the native step
+    # timeout becomes max(60 s, 20 x step), at most 240 s (a 16M / 8-rank step is ~5 s).
+    g.stage("first_step", init_b)
+    eng.init_ics("solar+random", cfg.seed)
+    eng.sync()
+    comm.barrier(dist)
+    t0 = time.perf_counter()
+    eng.step(1)
+    eng.sync()
+    first_s = comm.allreduce_max(dist, time.perf_counter() - t0)
+    step_to = a.step_timeout or gd.step_timeout(first_s, floor_s=a.step_timeout_min)
+    eng.set_step_timeout(step_to)
+    g.note(first_step_s=round(first_s, 4), step_timeout_s=step_to)
+
+    def budget(steps: float, host_s: float = 60.0) -> float:
+        """Deadline of a stage that runs `steps` steps plus host work."""
+        return step_to + 4.0 * first_s * steps + host_s
+
     sym = _native.MODE_NAMES.get(eng.native_layout["mode"]) == "sym"
     overlap, overlap_check = (0, None)
     if a.overlap != "auto":
         overlap = int(a.overlap)
     elif world > 1 and sym:
+        g.stage("overlap_check", budget(4 + 4 * 4))
         overlap, overlap_check = overlap_self_check(eng, cfg, dist, comm)
     eng.set_overlap(overlap)
+    g.stage("ics", budget(0))
     eng.init_ics("solar+random", cfg.seed)
     eng.sync()
 
     # Accuracy of the step's own force path at step 0, and the initial momentum (untimed).
+    g.stage("accuracy", budget(2, 180))
     err = sampled_error(eng, cfg, a.check_samples) if a.check_samples > 0 else None
     if err is not None:
         err = comm.allreduce_max(dist, err)
     _, vel0, mass = own_state(eng)
     p0, pscale = momentum(dist, comm, vel0, mass)
+    g.stage("energy", budget(4, 180))
     cons0 = engine_conserved(eng, dist) if a.energy else None  # exact-cutoff potential pass
 
     def measure(overlap: int) -> dict:
         """Warmup + the K timed steps from the ICs already loaded, then the audits of that
         work and the end-of-run physics (all untimed)."""
+        g.stage("warmup", budget(a.warmup))
         eng.step(a.warmup)
         eng.sync()
         eng.audit_reset()
         torch.cuda.synchronize()
         comm.barrier(dist)
         torch.cuda.synchronize()
+        g.stage("timed", budget(a.steps))
         t0 = time.perf_counter()
         eng.step(a.steps)
         eng.sync()
@@ -331,6 +390,7 @@ def main(argv=None) -> int:
         comm.barrier(dist)
         t1 = time.perf_counter()
         wall = comm.allreduce_max(dist, t1 - t0)
+        g.stage("audits", budget(4, 180))
         ginfo = eng.graph_info()
         # HBM the stepper holds (its allocation ledger; RCCL's own buffers excluded), max
         # over ranks
@@ -345,9 +405,10 @@ def main(argv=None) -> int:
             units = {"units_per_step_rank0": per_step,
                      "units_done_rank0": done, "ranks_short": int(short)}
             if short:
-                failures.append(f"unit count: {int(short)} rank(s) did not run rows x (S + D) "
-                                f"units per timed step (rank {rank}: {done} of "
-                                f"{per_step * a.steps})")
+                S, D, Kr = eng.sym_geometry()
+                failures.append(f"unit count: {int(short)} rank(s) did not run rows x (S + D + "
+                                f"Kr) units per timed step (S {S}, D {D}, Kr {Kr}; rank {rank}: "
+                                f"{done} of {per_step * a.steps})")
         else:
             units = None  # one-sided schedules: no unit counter, the replay audit still runs
         if overlap == 3 and os.environ.get("GRAVSIM_TEST_FAIL_GATED_AUDIT") == "1":
@@ -372,6 +433,12 @@ def main(argv=None) -> int:
         # Comm/compute split (untimed): a few eager steps with per-step phase events.
         phase = None
         if a.phase_steps > 0:
+            g.stage("phase", budget(a.phase_steps + 2))
+            if ginfo["mode"] == "segmented":
+                # whole plan periods: from an even step whose buffer still needs its gather
+                # (the state reads above gathered the current one), so the phase events come
+                # from the same segmented plan the timed loop replayed
+                eng.step(2 if eng.steps_done % 2 == 0 else 1)
             eng.set_timing(True)
             eng.step(a.phase_steps)
             phase = eng.phase_stats()
@@ -383,6 +450,7 @@ def main(argv=None) -> int:
         # timed run's bits (eager launches, one static unit per workgroup, no gating).
         replay = None
         if a.replay_audit:
+            g.stage("replay", budget(a.warmup + a.steps))
             cap = eng.dyn_cap
             eng.set_schedule(0, 0)
             eng.set_overlap(0)
@@ -404,15 +472,20 @@ def main(argv=None) -> int:
     res = measure(overlap)
     fallback = None
     if res["failures"] and overlap == 3 and a.overlap == "auto":
-        # The gated local-first launch passed its 2-step self-check but the audit of the timed
-        # steps failed: report that, and time the ungated schedule from the same ICs instead
-        # (it must pass the same audits, or the run fails).
+        # The gated local-first launch (the multi-rank default) passed its 2-step self-check
+        # but the audit of its timed steps failed. That is a failure of the default schedule:
+        # the ungated schedule is timed from the same ICs so the run still has a (labelled)
+        # number, but work_audit reports the failure and the run exits non-zero.
         fallback = {"from_overlap": 3, "to_overlap": 0, "failures": res["failures"]}
         overlap = 0
         eng.set_overlap(0)
+        g.stage("ics", budget(0))
         eng.init_ics("solar+random", cfg.seed)
         eng.sync()
         res = measure(0)
+        res["failures"] = ["gated schedule (the multi-rank default) failed its audit, fell back "
+                           "to the ungated one: " + "; ".join(fallback["failures"])] + \
+            res["failures"]
     wall, ginfo, mem, hbm_max = res["wall"], res["ginfo"], res["mem"], res["hbm_max"]
     failures, units, bad, drift = res["failures"], res["units"], res["bad"], res["drift"]
     err_end, conservation, phase, replay = (res["err_end"], res["conservation"], res["phase"],
@@ -423,6 +496,7 @@ def main(argv=None) -> int:
     fmode = eng.force_mode()
     exact_ms = None
     if a.exact_steps > 0:
+        g.stage("exact", budget(2 + 2 * a.exact_steps))
         eng.set_cutoff_mode("exact")
         eng.step(2)
         eng.sync()
@@ -432,6 +506,7 @@ def main(argv=None) -> int:
         eng.sync()
         comm.barrier(dist)
         exact_ms = 1e3 * comm.allreduce_max(dist, time.perf_counter() - t0) / a.exact_steps
+    g.stage("close", budget(0))
     eng.close()
     if rank == 0:
         value = cfg.n * a.steps / wall
@@ -465,9 +540,10 @@ def main(argv=None) -> int:
             "scaling": "strong",
             "vs_baseline": None,  # the reference publishes no numbers
             "dtype": a.dtype,
-            "data": "synthetic: seeded Sun/Earth/Mars + uniform random bodies (device RNG)",
+            "data": DATA,
+            "status": "ok" if not failures else "audit failed",
             "config": {
-                "model": "direct-sum N-body, KD (symplectic Euler) integrator, cutoff 1e-10 m",
+                "model": MODEL,
                 "n_bodies": cfg.n,
                 "global_batch": cfg.n,
                 "seq_len": 1,
@@ -487,6 +563,8 @@ def main(argv=None) -> int:
                 "overlap": overlap,
                 "overlap_check": overlap_check,
                 "overlap_fallback": fallback,
+                "step_timeout_s": step_to,
+                "first_step_ms": 1e3 * first_s,
                 # N^2 ordered pair terms per step (what a one-sided sum evaluates) ...
                 "effective_interactions_per_s": float(cfg.n) * cfg.n * a.steps / wall,
                 # ... and the pair evaluations actually performed (sym: N(N-1)/2 per step)
@@ -507,20 +585,16 @@ def main(argv=None) -> int:
             "audit": {"units": units, "replay": replay},
         }
         if world > 1:
-            out["config"]["launch"] = {
-                "probe_devices": int(os.environ[launch.PROBE_ENV])
-                if os.environ.get(launch.PROBE_ENV) else None,
-                "rehearsal_rank_hosts": os.environ.get("GRAVSIM_RCCL_RANK_HOSTS") == "1",
-                "HSA_ENABLE_IPC_MODE_LEGACY": os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY"),
-            }
+            out["config"]["launch"] = launch_info()
             out["config"]["ranks"] = ranks_info
         if phase is not None:
             out["comm_ms"] = phase["comm_ms"]
             out["exposed_comm_ms"] = phase["exposed_comm_ms"]
             out["config"]["phase"] = {k: phase[k] for k in (
                 "steps", "step_ms", "gather_ms", "exchange_ms", "exposed_gather_ms",
-                "exposed_exchange_ms", "deferred_units")}
+                "exposed_exchange_ms", "deferred_units", "graph")}
         print(json.dumps(out), flush=True)
+    g.stage("shutdown", init_b)
     comm.shutdown(dist)
     if failures:
         print("bench.py: work audit FAILED: " + "; ".join(failures), file=sys.stderr, flush=True)

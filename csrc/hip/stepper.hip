@@ -90,6 +90,8 @@ size_t exchange_bytes(const gs_stepper* s) {
 
 // Phase events of the step being enqueued (timed eager steps; at most 256 per phase_stats).
 gs_stepper::PhaseEv* phase_begin(gs_stepper* s) {
+  // (never reallocates: run_plan holds two of these pointers at once)
+  if (s->pev.capacity() < 256) s->pev.reserve(256);
   if (s->pev_used >= (int)s->pev.size()) {
     if (s->pev.size() >= 256) return nullptr;
     gs_stepper::PhaseEv e{};
@@ -400,9 +402,7 @@ int sym_force(gs_stepper* s, gs::SymArgs a, bool overlap_gather, bool exchange =
       // published, or are deferred to a second launch queued behind the gather event.
       a.units = 6;
       GS_HIP(force_sym_launch(s, a, s->s_comp));
-      GS_MARK(w0, w, s->s_comp);
-      if (comp_wait(s, s->ev_gathered)) return -1;
-      GS_MARK(w1, w, s->s_comp);
+      if (comp_wait(s, s->ev_gathered, kMarkGather)) return -1;
       a.units = 7;
       GS_HIP(force_sym_launch(s, a, s->s_comp));
       a.units = 0;
@@ -410,7 +410,7 @@ int sym_force(gs_stepper* s, gs::SymArgs a, bool overlap_gather, bool exchange =
       gs::SymArgs d = a;
       d.units = 1;  // diagonal chunks beside the gather
       GS_HIP(force_sym_launch(s, d, s->s_comp));
-      if (comp_wait(s, s->ev_gathered)) return -1;
+      if (comp_wait(s, s->ev_gathered, kMarkGather)) return -1;
       a.units = 2;
       GS_HIP(force_sym_launch(s, a, s->s_comp));
     } else if (overlap_gather && b0 == 0 && one_band && ov == 2) {
@@ -427,9 +427,7 @@ int sym_force(gs_stepper* s, gs::SymArgs a, bool overlap_gather, bool exchange =
       GS_HIP(hipStreamWaitEvent(s->s_comp, s->ev_remote, 0));  // join
     } else {
       if (overlap_gather && b0 == 0) {
-        GS_MARK(w0, w, s->s_comp);
-        if (comp_wait(s, s->ev_gathered)) return -1;
-        GS_MARK(w1, w, s->s_comp);
+        if (comp_wait(s, s->ev_gathered, kMarkGather)) return -1;
       }
       GS_HIP(force_sym_launch(s, a, s->s_comp));
     }
@@ -454,9 +452,7 @@ int sym_force(gs_stepper* s, gs::SymArgs a, bool overlap_gather, bool exchange =
       GS_HIP(gs::launch_sym_row_reduce(a, s->s_comp));
     }
     if (exchange && last) {
-      GS_MARK(j0, j, s->s_comp);
-      if (comp_wait(s, s->ev_sym)) return -1;
-      GS_MARK(j1, j, s->s_comp);
+      if (comp_wait(s, s->ev_sym, kMarkExchange)) return -1;
     }
   }
   return 0;
@@ -904,7 +900,8 @@ int gs_stepper_destroy(gs_stepper* s) {
   if (s->s_rem) (void)hipStreamSynchronize(s->s_rem);
   if (s->s_rem2) (void)hipStreamSynchronize(s->s_rem2);
   drop_graphs(s);
-  if (s->have_comm) (void)ncclCommDestroy(s->comm);
+  // (a communicator aborted by a watchdog, a timeout or an async error is not destroyed)
+  if (s->have_comm && s->comm_live.exchange(nullptr)) (void)ncclCommDestroy(s->comm);
   for (const auto& m : s->mem) (void)hipFree(m.p);
   s->mem.clear();
   for (hipEvent_t e : {s->ev_ready, s->ev_gathered, s->ev_t0, s->ev_local, s->ev_end,
@@ -1031,6 +1028,7 @@ int gs_stepper_step(gs_stepper* s, int32_t nsteps) {
 int gs_stepper_set_timing(gs_stepper* s, int32_t on) {
   s->timed = on != 0;
   s->pev_used = 0;
+  s->pev_plan = 0;
   return 0;
 }
 
@@ -1165,7 +1163,8 @@ int gs_stepper_phase_stats(gs_stepper* s, double* out8) {
   unsigned d[2] = {0, 0};
   GS_HIP(hipMemcpy(d, s->gate_buf + 2, sizeof(d), hipMemcpyDeviceToHost));
   out8[6] = d[1];
-  out8[7] = 0.0;
+  out8[7] = s->pev_plan;  // of them replayed from the segmented plan (the rest eager)
+  s->pev_plan = 0;
   // (on s_comp: a legacy-stream memset is not ordered against the non-blocking compute
   // stream, so the next gated launch could race it)
   GS_HIP(hipMemsetAsync(s->gate_buf + 2, 0, sizeof(d), s->s_comp));

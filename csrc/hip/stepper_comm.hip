@@ -92,6 +92,14 @@ int gather(gs_stepper* s, int cur, bool gate) {
 // forwarded to the right neighbour in the next sub-step. Each slice lands at its own offset
 // of X[cur], so no buffer is reused within a step; per-chunk partials + the canonical reduce
 // keep the result bit-identical to the all-gather schedule.
+bool abort_comm(gs_stepper* s) {
+  ncclComm_t c = s->comm_live.exchange(nullptr);
+  if (!c) return false;
+  s->comm_stage.store(-1);
+  (void)ncclCommAbort(c);
+  return true;
+}
+
 int ring_src(const gs_stepper* s, int sub) {
   const int P = s->cfg.nranks;
   return ((s->cfg.rank - sub) % P + P) % P;
@@ -163,11 +171,7 @@ int sym_exchange_rccl(gs_stepper* s, bool join) {
         return 0;
       }))
     return -1;
-  if (join) {
-    GS_MARK(j0, j, s->s_comp);
-    if (comp_wait(s, s->ev_sym)) return -1;
-    GS_MARK(j1, j, s->s_comp);
-  }
+  if (join && comp_wait(s, s->ev_sym, kMarkExchange)) return -1;
   return 0;
 }
 
@@ -255,11 +259,16 @@ int gs_stepper_comm_init(gs_stepper* s, const void* id128, int32_t rank, int32_t
   memcpy(&id, id128, sizeof(id));
   // The one-sided multi-rank schedule is always split (the sym schedule has its own slots).
   if (s->L.mode != GS_MODE_SYM && ensure_partial(s)) return -1;
+  // Stages for a watchdog on another thread (gs_stepper_comm_stage): a rank stuck here is
+  // reported as "in ncclCommInitRank" / "in the warm-up", not just "in comm_init".
+  s->comm_stage.store(1);
   GS_NCCL(ncclCommInitRank(&s->comm, nranks, id, rank));
+  s->comm_live.store(s->comm);
   // GRAVSIM_FORCE_COMM keeps a 1-rank communicator live so the full multi-rank schedule
   // (in-place ncclAllGather, local/remote split on two streams, events) runs on one GPU.
   s->have_comm = nranks > 1 || getenv("GRAVSIM_FORCE_COMM") != nullptr;
   if (!s->have_comm) {
+    s->comm_live.store(nullptr);
     (void)ncclCommDestroy(s->comm);
     s->comm = nullptr;
   }
@@ -270,8 +279,10 @@ int gs_stepper_comm_init(gs_stepper* s, const void* id128, int32_t rank, int32_t
     // n_local * 4 >= P elements) so that no timed or captured step pays for it.
     char* buf = static_cast<char*>(s->acc);
     const ncclDataType_t dt = s->esz == 4 ? ncclFloat32 : ncclFloat64;
+    s->comm_stage.store(2);
     GS_NCCL(ncclAllGather(buf + (size_t)rank * s->esz, buf, 1, dt, s->comm, s->s_comm));
     if (nranks > 1 && s->cfg.strategy == GS_STRATEGY_RING) {
+      s->comm_stage.store(3);
       GS_NCCL(ncclGroupStart());
       GS_NCCL(ncclSend(buf, 1, dt, (rank + 1) % nranks, s->comm, s->s_comm));
       GS_NCCL(ncclRecv(buf + (size_t)nranks * s->esz, 1, dt, (rank - 1 + nranks) % nranks,
@@ -280,6 +291,7 @@ int gs_stepper_comm_init(gs_stepper* s, const void* id128, int32_t rank, int32_t
     }
     if (nranks > 1 && s->L.mode == GS_MODE_SYM) {
       // The sym schedule's node-sum exchange talks to every peer: connect them all now.
+      s->comm_stage.store(4);
       GS_NCCL(ncclGroupStart());
       for (int q = 0; q < nranks; ++q) {
         if (q == rank) continue;
@@ -288,10 +300,19 @@ int gs_stepper_comm_init(gs_stepper* s, const void* id128, int32_t rank, int32_t
       }
       GS_NCCL(ncclGroupEnd());
     }
-    GS_HIP(hipStreamSynchronize(s->s_comm));
+    // Bounded like a step: a peer that never joins the warm-up aborts the communicator after
+    // the step timeout instead of blocking here forever.
+    s->comm_stage.store(5);
+    const int64_t rec = s->prog_rec;
+    if (note_progress(s) || wait_until(s, rec + 1, s->step_timeout_s)) return -1;
   }
+  s->comm_stage.store(6);
   return 0;
 }
+
+int32_t gs_stepper_comm_stage(gs_stepper* s) { return s ? s->comm_stage.load() : 0; }
+
+int32_t gs_stepper_abort(gs_stepper* s) { return s && abort_comm(s) ? 1 : 0; }
 
 int gs_stepper_comm_check(gs_stepper* s) {
   if (!s->have_comm) return 0;
@@ -300,7 +321,7 @@ int gs_stepper_comm_check(gs_stepper* s) {
   if (async != ncclSuccess && async != ncclInProgress) {
     char b[256];
     snprintf(b, sizeof(b), "RCCL async error: %s; communicator aborted", ncclGetErrorString(async));
-    (void)ncclCommAbort(s->comm);
+    abort_comm(s);
     s->have_comm = false;
     gs_set_error(b);
     return -1;

@@ -26,7 +26,9 @@ int seg_cut(gs_stepper* s) {
     hipGraphExec_t x = nullptr;
     e = hipGraphInstantiate(&x, g, nullptr, nullptr, 0);
     if (e == hipSuccess) {
-      s->plan.push_back({gs_stepper::PlanOp::kGraph, x, nullptr, {}});
+      gs_stepper::PlanOp op{gs_stepper::PlanOp::kGraph, x, nullptr, {}};
+      op.step = s->seg_step;  // the segment holds work of the step it began in
+      s->plan.push_back(std::move(op));
       ++s->plan_graphs;
     }
   }
@@ -36,9 +38,43 @@ int seg_cut(gs_stepper* s) {
 }
 
 int seg_open(gs_stepper* s) {
+  s->seg_step = s->rec_step;
   GS_HIP(hipStreamBeginCapture(s->s_comp, hipStreamCaptureModeThreadLocal));
   return 0;
 }
+
+namespace {
+int plan_push(gs_stepper* s, gs_stepper::PlanOp op) {
+  if (seg_cut(s)) return -1;
+  op.step = s->rec_step;
+  s->plan.push_back(std::move(op));
+  return seg_open(s);
+}
+
+// The events of a measured stall on s_comp (exposed gather w0/w1, exposed exchange j0/j1).
+struct MarkEv {
+  hipEvent_t gs_stepper::PhaseEv::*a;
+  hipEvent_t gs_stepper::PhaseEv::*b;
+  bool gs_stepper::PhaseEv::*flag;
+};
+MarkEv mark_events(int mark) {
+  return mark == kMarkExchange
+             ? MarkEv{&gs_stepper::PhaseEv::j0, &gs_stepper::PhaseEv::j1, &gs_stepper::PhaseEv::j}
+             : MarkEv{&gs_stepper::PhaseEv::w0, &gs_stepper::PhaseEv::w1, &gs_stepper::PhaseEv::w};
+}
+
+// hipStreamWaitEvent(s_comp, ev), bracketed by the stall's phase events of `pe` (if any).
+int timed_wait(gs_stepper* s, hipEvent_t ev, int mark, gs_stepper::PhaseEv* pe) {
+  const MarkEv m = mark_events(mark);
+  if (pe && mark != kMarkNone) GS_HIP(hipEventRecord(pe->*m.a, s->s_comp));
+  GS_HIP(hipStreamWaitEvent(s->s_comp, ev, 0));
+  if (pe && mark != kMarkNone) {
+    GS_HIP(hipEventRecord(pe->*m.b, s->s_comp));
+    pe->*m.flag = true;
+  }
+  return 0;
+}
+}  // namespace
 
 // hipEventRecord(ev, s_comp) for another stream to wait on.
 int comp_record(gs_stepper* s, hipEvent_t ev) {
@@ -46,29 +82,23 @@ int comp_record(gs_stepper* s, hipEvent_t ev) {
     GS_HIP(hipEventRecord(ev, s->s_comp));
     return 0;
   }
-  if (seg_cut(s)) return -1;
-  s->plan.push_back({gs_stepper::PlanOp::kRecord, nullptr, ev, {}});
-  return seg_open(s);
+  return plan_push(s, {gs_stepper::PlanOp::kRecord, nullptr, ev, {}});
 }
 
-// hipStreamWaitEvent(s_comp, ev) on an event another stream records.
-int comp_wait(gs_stepper* s, hipEvent_t ev) {
-  if (!s->rec) {
-    GS_HIP(hipStreamWaitEvent(s->s_comp, ev, 0));
-    return 0;
-  }
-  if (seg_cut(s)) return -1;
-  s->plan.push_back({gs_stepper::PlanOp::kWait, nullptr, ev, {}});
-  return seg_open(s);
+// hipStreamWaitEvent(s_comp, ev) on an event another stream records. `mark` names the stall
+// for the phase timing (eager timed steps, or a replayed plan with timing on).
+int comp_wait(gs_stepper* s, hipEvent_t ev, int mark) {
+  if (!s->rec) return timed_wait(s, ev, mark, s->pe);
+  gs_stepper::PlanOp op{gs_stepper::PlanOp::kWait, nullptr, ev, {}};
+  op.mark = mark;
+  return plan_push(s, std::move(op));
 }
 
 // Work on the comm stream (a collective and its event bookkeeping): run now, or replayed
 // eagerly at this point of the plan.
 int comm_do(gs_stepper* s, std::function<int()> fn) {
   if (!s->rec) return fn();
-  if (seg_cut(s)) return -1;
-  s->plan.push_back({gs_stepper::PlanOp::kHost, nullptr, nullptr, std::move(fn)});
-  return seg_open(s);
+  return plan_push(s, {gs_stepper::PlanOp::kHost, nullptr, nullptr, std::move(fn)});
 }
 
 void drop_graphs(gs_stepper* s) {
@@ -108,7 +138,7 @@ int build_graph(gs_stepper* s) {
 // Multi-rank steps whose cross-stream points all go through comp_record / comp_wait /
 // comm_do: the sym schedule except overlap 2 (a second compute stream forked per step).
 bool plan_ok(const gs_stepper* s) {
-  return xcomm(s) && use_sym(s) && s->sym_overlap != 2 && s->cfg.use_graph == 1 && !s->timed;
+  return xcomm(s) && use_sym(s) && s->sym_overlap != 2 && s->cfg.use_graph == 1;
 }
 
 // Record one ping-pong period (two steps, from an even step whose buffer needs its gather)
@@ -118,11 +148,14 @@ int build_plan(gs_stepper* s) {
   const bool f0 = s->full[0], f1 = s->full[1];
   drop_graphs(s);
   s->work_zero = false;  // (as build_graph: a replay re-zeroes the dynamic unit counter)
+  s->rec_step = 0;
   if (seg_open(s)) return -1;
   s->rec = true;
   int rc = enqueue_step_any(s, true);
+  s->rec_step = 1;
   if (rc == 0) rc = enqueue_step_any(s, true);
   s->rec = false;
+  s->rec_step = 0;
   const int cut = rc == 0 ? seg_cut(s) : 0;
   if (rc != 0) {  // abandon the open capture
     hipGraph_t g = nullptr;
@@ -139,16 +172,39 @@ int build_plan(gs_stepper* s) {
 }
 
 int run_plan(gs_stepper* s) {
+  // Phase timing (gs_stepper_set_timing): one event set per step of the period. Step 0 starts
+  // before the first op, step 1 at its first op (a segment belongs to the step it began in);
+  // the collectives' spans are recorded on s_comm by the host ops (GS_MARK with `pe` set).
+  gs_stepper::PhaseEv* pe[2] = {nullptr, nullptr};
+  if (s->timed) {
+    for (auto& p : pe)
+      if (!(p = phase_begin(s))) break;
+    if (pe[0]) GS_HIP(hipEventRecord(pe[0]->t0, s->s_comp));
+  }
+  int at = 0;
   for (auto& op : s->plan) {
+    if (op.step != at) {
+      if (pe[at]) GS_HIP(hipEventRecord(pe[at]->end, s->s_comp));
+      at = op.step;
+      if (pe[at]) GS_HIP(hipEventRecord(pe[at]->t0, s->s_comp));
+    }
     switch (op.kind) {
       case gs_stepper::PlanOp::kGraph: GS_HIP(hipGraphLaunch(op.g, s->s_comp)); break;
       case gs_stepper::PlanOp::kRecord: GS_HIP(hipEventRecord(op.ev, s->s_comp)); break;
-      case gs_stepper::PlanOp::kWait: GS_HIP(hipStreamWaitEvent(s->s_comp, op.ev, 0)); break;
-      case gs_stepper::PlanOp::kHost:
-        if (op.fn()) return -1;
+      case gs_stepper::PlanOp::kWait:
+        if (timed_wait(s, op.ev, op.mark, pe[at])) return -1;
         break;
+      case gs_stepper::PlanOp::kHost: {
+        s->pe = pe[at];
+        const int rc = op.fn();
+        s->pe = nullptr;
+        if (rc) return -1;
+        break;
+      }
     }
   }
+  if (pe[at]) GS_HIP(hipEventRecord(pe[at]->end, s->s_comp));
+  if (pe[0] && pe[1]) s->pev_plan += 2;
   return 0;
 }
 
@@ -199,7 +255,7 @@ int wait_until(gs_stepper* s, int64_t target, double timeout_s) {
                "enqueued); communicator aborted",
                el, s->cfg.rank, (long long)s->prog_done, (long long)s->prog_rec);
       if (s->have_comm) {
-        (void)ncclCommAbort(s->comm);
+        abort_comm(s);
         s->have_comm = false;
       }
       gs_set_error(m);

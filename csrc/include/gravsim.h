@@ -188,8 +188,9 @@ int gs_stepper_set_schedule(gs_stepper* s, int32_t use_graph, int32_t dyn_cap);
 // Re-resolve the force path with a new cutoff mode (0 auto, 1 exact select, 2 fast core).
 int gs_stepper_set_cutoff_mode(gs_stepper* s, int32_t mode);
 // Work audit of the sym schedule: force units completed since the last reset (waits for the
-// compute stream) and the units one step must run on this rank (rows x (S + D)); both 0 for
-// the one-sided schedules.
+// compute stream) and the units one step must run on this rank (rows x (S + D + Kr): a split
+// segment counts as its two halves, whichever way it runs); both 0 for the one-sided
+// schedules.
 int gs_stepper_audit(gs_stepper* s, uint64_t* units_done, uint64_t* units_per_step);
 int gs_stepper_audit_reset(gs_stepper* s);
 // What the last replayed steps ran from: *mode 0 eager, 1 one hipGraph per two steps, 2 a
@@ -219,6 +220,13 @@ int gs_rccl_unique_id(void* out128);
 int gs_stepper_comm_init(gs_stepper* s, const void* id128, int32_t rank, int32_t nranks);
 // Poll RCCL async errors; aborts the communicator on error. Returns 0 if healthy.
 int gs_stepper_comm_check(gs_stepper* s);
+// How far gs_stepper_comm_init got (safe to call from another thread, e.g. a watchdog):
+// 0 not started, 1 in ncclCommInitRank, 2 warm-up all-gather, 3 warm-up ring send/recv,
+// 4 warm-up peer send/recv, 5 waiting for the warm-up, 6 done, -1 aborted.
+int32_t gs_stepper_comm_stage(gs_stepper* s);
+// Abort the live RCCL communicator once (ncclCommAbort; callable from another thread to
+// unblock collectives that will never complete). Returns 1 if it aborted, 0 if there was none.
+int32_t gs_stepper_abort(gs_stepper* s);
 
 int gs_hip_device_count(void);
 const char* gs_hip_kernel_info(void);

@@ -13,6 +13,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <atomic>
 #include <chrono>
 #include <functional>
 #include <string>
@@ -71,6 +72,10 @@ struct gs_stepper {
   bool full[2] = {true, false};
   ncclComm_t comm = nullptr;
   bool have_comm = false;
+  // Watchdog view of the communicator (gs_stepper_comm_stage / gs_stepper_abort may run on
+  // another thread): the handle once ncclCommInitRank returned it, and the init stage.
+  std::atomic<ncclComm_t> comm_live{nullptr};
+  std::atomic<int> comm_stage{0};
   bool virt = false;  // member of a virtual-rank group (gather = device copies, gs_group_step)
   bool emulate = false;  // GRAVSIM_EMULATE_RANK: run one rank's launch shapes, no exchange
   // sym work beside a pending gather (GRAVSIM_SYM_OVERLAP): 0 none (wait, then one launch),
@@ -167,15 +172,25 @@ struct gs_stepper {
   // emulation's modeled ones) and the event record/wait that order them against the compute
   // stream are issued eagerly between the segments on replay. RCCL is never captured, so the
   // socket-transport capture crash (profiles/r2_graph_comm_root_cause.txt) cannot occur.
+  // Phase timing of a replayed plan (gs_stepper_set_timing): every op carries the step of
+  // the period it belongs to (0 / 1) and a kWait op the stall it measures (mark: kMarkGather
+  // = exposed gather, kMarkExchange = exposed node exchange); run_plan records the step's
+  // t0 / end and the stall's events eagerly between the segments, and points `pe` at the
+  // step's event set while the eager collectives run (their spans on s_comm).
   struct PlanOp {
     enum Kind { kGraph, kRecord, kWait, kHost } kind;
     hipGraphExec_t g;
     hipEvent_t ev;
     std::function<int()> fn;
+    int step = 0;
+    int mark = 0;
   };
   std::vector<PlanOp> plan;  // one ping-pong period (two steps)
   bool rec = false;          // recording a plan: s_comp is capturing a segment
+  int rec_step = 0;          // recording: the step of the period being enqueued
+  int seg_step = 0;          // recording: the step in which the open segment began
   int plan_graphs = 0;       // graph segments per period (diagnostics)
+  int pev_plan = 0;          // timed steps that ran from a replayed plan (phase_stats)
   // Device memory ledger: every HBM buffer the stepper owns, by name (gs_stepper_mem_entry);
   // destroy frees exactly these. All of them are allocated before the first step, sized from
   // the layout (the sym bands from the free HBM), so nothing is allocated inside the loop.
@@ -196,6 +211,9 @@ struct gs_stepper {
   } while (0)
 
 namespace gs::rt {
+
+// What a compute-stream wait on another stream's event stands for, in the phase timing.
+enum : int { kMarkNone = 0, kMarkGather = 1, kMarkExchange = 2 };
 
 inline size_t row_bytes(const gs_stepper* s) { return 4 * s->esz; }
 
@@ -233,7 +251,7 @@ inline bool use_sym(const gs_stepper* s) { return s->L.mode == GS_MODE_SYM; }
 int seg_cut(gs_stepper* s);
 int seg_open(gs_stepper* s);
 int comp_record(gs_stepper* s, hipEvent_t ev);
-int comp_wait(gs_stepper* s, hipEvent_t ev);
+int comp_wait(gs_stepper* s, hipEvent_t ev, int mark = kMarkNone);
 int comm_do(gs_stepper* s, std::function<int()> fn);
 void drop_graphs(gs_stepper* s);
 int build_graph(gs_stepper* s);
@@ -252,8 +270,11 @@ void rank_chunks(const gs_stepper* s, int src, int* c0, int* c1);
 int ring_xfer_rccl(gs_stepper* s, int cur, int sub);
 int sym_exchange_rccl(gs_stepper* s, bool join = true);
 void maybe_install_crash_trace();
+// ncclCommAbort once (the watchdog thread, a timeout or an async error may all ask for it).
+bool abort_comm(gs_stepper* s);
 
-// stepper.hip: buffers, step enqueue.
+// stepper.hip: buffers, step enqueue, phase events.
+gs_stepper::PhaseEv* phase_begin(gs_stepper* s);
 size_t gather_bytes(const gs_stepper* s);
 size_t exchange_bytes(const gs_stepper* s);
 int ensure_partial(gs_stepper* s);

@@ -53,7 +53,8 @@ def build_parser() -> argparse.ArgumentParser:
                    help=argparse.SUPPRESS)
     p.add_argument("--step-timeout", dest="step_timeout_s", type=float, default=d.step_timeout_s,
                    help="multi-rank hang detection: abort the RCCL communicator when no step "
-                        "completes for this many seconds (0 = wait forever)")
+                        "completes for this many seconds (default: max(60, 20 x the measured "
+                        "step time), at most 240; 0 = wait forever)")
     p.add_argument("--overlap", type=int, choices=[-1, 0, 1, 2, 3], default=d.overlap,
                    help="multi-rank sym schedule: work beside the all-gather (3: one launch, "
                         "rank-local units first, remote units once the gather is published, "
@@ -125,15 +126,20 @@ def config_from_args(a: argparse.Namespace) -> SimConfig:
                      diag_every=a.diag_every).validate()
 
 
-def run_one(cfg: SimConfig, dist, log, quiet: bool = False, final: bool = True) -> dict:
+def run_one(cfg: SimConfig, dist, log, quiet: bool = False, final: bool = True,
+            guard=None) -> dict:
     from .runtime.simulation import Simulation
     from .utils.logs import format_positions_mpi
 
-    sim = Simulation(cfg, dist)
+    sim = Simulation(cfg, dist, guard=guard)
     try:
         if log and dist.is_root:
             log.header(dist.world, cfg.n, cfg.steps, cfg.dt)
+        if guard:
+            guard.stage("run", None)  # bounded by the native step timeout (progress)
         m = sim.run(cfg.steps, log if dist.is_root else None)
+        if guard:
+            guard.stage("output", None)
         state = sim.global_state()  # collective
         if cfg.dump_path and cfg.dump_path.endswith(".gsck"):
             sim.save_checkpoint(cfg.dump_path)  # collective; rank 0 writes
@@ -187,7 +193,19 @@ def main(argv: Optional[list[str]] = None) -> int:
     if a.nproc > 0 and int(os.environ.get("WORLD_SIZE", "1")) != a.nproc:
         raise SystemExit(f"--gpus/--nproc {a.nproc} but WORLD_SIZE {os.environ.get('WORLD_SIZE')}")
     cfg = config_from_args(a)
-    dist = comm.init()
+    guard = None
+    world = int(os.environ.get("WORLD_SIZE", "1") or 1)
+    if world > 1:
+        # Multi-rank: a stalled or failed rank ends the job with rank 0's error JSON line
+        # (stage, every rank's record) and exit code 70 instead of a hang (parallel/guard.py).
+        from .parallel.guard import INIT_TIMEOUT_S, RunGuard
+
+        guard = RunGuard(int(os.environ.get("RANK", "0") or 0), world,
+                         lambda reason, recs: {"status": "error", "error": reason,
+                                               "stage": recs[0].get("stage") if recs else None,
+                                               "n": cfg.n, "nranks": world, "ranks": recs})
+        guard.stage("gloo_init", INIT_TIMEOUT_S)
+    dist = comm.init(timeout_s=180.0 if guard else 600.0)
     from .runtime.simulation import NonFiniteError
 
     try:
@@ -196,18 +214,25 @@ def main(argv: Optional[list[str]] = None) -> int:
             fmt = cfg.log_format if a.log_format != "mpi" else "spark"
             log = RunLog(fmt, cfg.log_dir if dist.is_root else None, echo=dist.is_root)
             for n in sizes:
-                run_one(cfg.replace(n=n, log_format=fmt), dist, log, a.quiet, final=False)
+                run_one(cfg.replace(n=n, log_format=fmt), dist, log, a.quiet, final=False,
+                        guard=guard)
             if dist.is_root:
                 log.completed()
         else:
             log = RunLog(cfg.log_format, cfg.log_dir if dist.is_root else None,
                          echo=dist.is_root and not a.quiet)
-            run_one(cfg, dist, log, a.quiet)
+            run_one(cfg, dist, log, a.quiet, guard=guard)
     except NonFiniteError as e:  # the NaN/Inf guard (--nan-check-every): fail loudly
         print(f"gravsim: error: {e}", file=sys.stderr, flush=True)
         return 3
+    except Exception as e:  # noqa: BLE001 - multi-rank: every failure becomes a report
+        if guard is None:
+            raise
+        guard.fail(f"{type(e).__name__}: {e}")
     finally:
         comm.shutdown(dist)
+    if guard:
+        guard.close()
     return 0
 
 

@@ -52,8 +52,10 @@ class SimConfig:
                                   # default (3 for P > 1, as bench.py runs; GRAVSIM_SYM_OVERLAP
                                   # overrides)
     threads: int = 0              # CPU engine OpenMP threads (0 = default)
-    step_timeout_s: float = 600.0 # multi-rank hang detection: abort RCCL when no step completes
-                                  # for this long
+    step_timeout_s: Optional[float] = None  # multi-rank hang detection: abort RCCL when no
+                                  # step completes for this long; None = derived from the
+                                  # measured step time (max(60 s, 20 x step), at most 240 s;
+                                  # start-up is bounded by 180 s); 0 = unbounded
     # observability / IO
     log_dir: Optional[str] = None     # directory for the text log (None = no file)
     log_format: str = "mpi"           # mpi | spark | cuda | none
@@ -110,8 +112,8 @@ class SimConfig:
             raise ValueError("overlap must be -1 (default) or 0..3")
         if self.diag_every < 0:
             raise ValueError("diag_every must be >= 0")
-        if self.step_timeout_s < 0:
-            raise ValueError("step_timeout_s must be >= 0 (0 = unbounded)")
+        if self.step_timeout_s is not None and self.step_timeout_s < 0:
+            raise ValueError("step_timeout_s must be None (derived), or >= 0 (0 = unbounded)")
         if self.cutoff < 0 or self.softening < 0:
             raise ValueError("cutoff and softening must be >= 0")
         return self

@@ -175,6 +175,8 @@ def hip_lib():
         _sig(lib, "gs_rccl_unique_id", c_int32, [c_void_p])
         _sig(lib, "gs_stepper_comm_init", c_int32, [S, c_void_p, c_int32, c_int32])
         _sig(lib, "gs_stepper_comm_check", c_int32, [S])
+        _sig(lib, "gs_stepper_comm_stage", c_int32, [S])
+        _sig(lib, "gs_stepper_abort", c_int32, [S])
         _sig(lib, "gs_hip_device_count", c_int32, [])
         VP = POINTER(c_void_p)
         _sig(lib, "gs_dev_alloc", c_int32, [c_int32, c_uint64, VP])

@@ -65,8 +65,17 @@ class HipEngine:
         L = _native.GsLayout()
         _native.check(self.lib, self.lib.gs_stepper_layout(self._s, ctypes.byref(L)), "layout")
         self.native_layout = L.as_dict()
-        if nranks > 1 and cfg.step_timeout_s:
-            self.lib.gs_stepper_set_timeout(self._s, float(cfg.step_timeout_s))
+        # P > 1: a progress bound from the start (the RCCL warm-up included); a derived
+        # timeout (cfg None) starts at the start-up budget until a step has been measured
+        if nranks > 1:
+            from ..parallel.guard import INIT_TIMEOUT_S
+
+            self.step_timeout_s = (INIT_TIMEOUT_S if cfg.step_timeout_s is None
+                                   else float(cfg.step_timeout_s))
+        else:
+            self.step_timeout_s = 0.0
+        if self.step_timeout_s:
+            self.lib.gs_stepper_set_timeout(self._s, self.step_timeout_s)
         if cfg.overlap >= 0:
             self.set_overlap(cfg.overlap)
         self.layout: Layout = make_layout(cfg.n, rank, nranks, L.chunk,
@@ -90,6 +99,27 @@ class HipEngine:
     def comm_check(self) -> None:
         _native.check(self.lib, self.lib.gs_stepper_comm_check(self._s), "rccl health")
 
+    COMM_STAGES = {0: "not started", 1: "in ncclCommInitRank", 2: "warm-up all-gather",
+                   3: "warm-up ring send/recv", 4: "warm-up peer send/recv",
+                   5: "waiting for the warm-up", 6: "done", -1: "aborted"}
+
+    def comm_stage(self) -> str:
+        """How far comm_init got (safe from a watchdog thread while comm_init blocks)."""
+        if not self._s:
+            return "no stepper"
+        return self.COMM_STAGES.get(int(self.lib.gs_stepper_comm_stage(self._s)), "?")
+
+    def abort(self) -> bool:
+        """ncclCommAbort the live communicator once (from a watchdog thread: unblocks
+        collectives that will never complete). True if one was aborted."""
+        return bool(self._s) and bool(self.lib.gs_stepper_abort(self._s))
+
+    def set_step_timeout(self, seconds: float) -> None:
+        """Native progress bound of sync() and of the host running ahead: abort RCCL when no
+        enqueued step completes for this long (0: unbounded)."""
+        self.step_timeout_s = float(seconds)
+        self.lib.gs_stepper_set_timeout(self._s, float(seconds))
+
     # -- state ----------------------------------------------------------------------------
     def init_ics(self, family: str, seed: int) -> None:
         if family in DEVICE_IC_IDS:
@@ -112,11 +142,12 @@ class HipEngine:
             _native.check(self.lib, self.lib.gs_stepper_step(self._s, int(n)), "step")
 
     def sync(self, timeout_s: float = 0.0) -> None:
-        """Wait for the enqueued steps. With a timeout (or P > 1: cfg.step_timeout_s, default
-        600 s) the wait polls RCCL async errors and aborts the communicator when no step
-        completes for that long (it bounds progress, not the length of the run)."""
-        if timeout_s <= 0 and self.nranks > 1:
-            timeout_s = float(self.cfg.step_timeout_s or 0)
+        """Wait for the enqueued steps. With a timeout (or the engine's step timeout: P > 1
+        cfg.step_timeout_s, or set_step_timeout) the wait polls RCCL async errors and aborts the
+        communicator when no step completes for that long (it bounds progress, not the length
+        of the run)."""
+        if timeout_s <= 0:
+            timeout_s = self.step_timeout_s
         if timeout_s > 0:
             _native.check(self.lib, self.lib.gs_stepper_wait(self._s, timeout_s), "wait")
         else:
@@ -135,10 +166,23 @@ class HipEngine:
         out = (ctypes.c_double * 8)()
         _native.check(self.lib, self.lib.gs_stepper_phase_stats(self._s, out), "phase stats")
         v = list(out)
-        return {"steps": int(v[0]), "step_ms": v[1], "gather_ms": v[2], "exchange_ms": v[3],
+        steps, planned = int(v[0]), int(v[7])
+        # how the timed steps ran: from the segmented plan the untimed run replays, eagerly,
+        # or both (a step count that is not a whole number of two-step periods)
+        graph = ("segmented" if planned == steps else "eager" if planned == 0 else
+                 f"segmented ({planned} of {steps} steps)") if steps else None
+        return {"steps": steps, "step_ms": v[1], "gather_ms": v[2], "exchange_ms": v[3],
                 "exposed_gather_ms": v[4], "exposed_exchange_ms": v[5],
                 "deferred_units": int(v[6]), "comm_ms": v[2] + v[3],
-                "exposed_comm_ms": v[4] + v[5]}
+                "exposed_comm_ms": v[4] + v[5], "graph": graph}
+
+    def sym_geometry(self) -> tuple[int, int, int]:
+        """(S shell segments, D diagonal parts, Kr split segments) per chunk row of the sym
+        schedule: a step runs rows x (S + D + Kr) units on a rank (the work audit)."""
+        n_pad = int(self.native_layout["n_pad"])
+        v = [ctypes.c_int32() for _ in range(5)]
+        self.lib.gs_sym_geometry(n_pad, *[ctypes.byref(x) for x in v])
+        return int(v[3].value), int(v[4].value), int(self.lib.gs_sym_split_segments(n_pad))
 
     def unit_trace(self) -> np.ndarray:
         """(entries, 4) uint64 timeline of the last sym force launch (GRAVSIM_UNIT_TRACE set

@@ -84,22 +84,38 @@ def conservation_summary(c0: dict, c1: dict, samples: list = ()) -> dict:
 
 
 class Simulation:
-    def __init__(self, cfg: SimConfig, dist: Optional[comm.DistInfo] = None):
+    def __init__(self, cfg: SimConfig, dist: Optional[comm.DistInfo] = None, guard=None):
         self.cfg = cfg.validate()
         self.dist = dist or comm.env_info()
+        self.overlap_check: Optional[str] = None
         use_gpu = cfg.device == "gpu" or (cfg.device == "auto" and gpu_available())
         if cfg.device == "gpu" and not gpu_available():
             raise RuntimeError("device=gpu requested but no HIP device / native library")
         d = self.dist
+        stage = guard.stage if guard else (lambda *_a, **_k: None)
         if use_gpu:
             import torch
 
+            from ..parallel.guard import INIT_TIMEOUT_S
+
             dev = d.local_rank % max(1, torch.cuda.device_count())
+            stage("engine", INIT_TIMEOUT_S)
             self.engine = HipEngine(cfg, d.rank, d.world, device=dev, dist=d)
+            if guard:
+                guard.on_abort(self.engine.abort)
+                guard.probe(lambda: {"comm_stage": self.engine.comm_stage()})
             if d.world > 1:
+                stage("comm_init", INIT_TIMEOUT_S)
                 uid = HipEngine.unique_id() if d.is_root else None
                 uid = comm.broadcast_bytes(d, uid)
                 self.engine.comm_init(uid)
+                stage("self_check", INIT_TIMEOUT_S)
+                per_step = self._self_check()
+                if cfg.step_timeout_s is None:
+                    from ..parallel.guard import step_timeout
+
+                    self.engine.set_step_timeout(step_timeout(per_step))
+            stage("ics", INIT_TIMEOUT_S)
         else:
             self.engine = CpuEngine(cfg, d.rank, d.world, dist=d)
         self.step0 = 0
@@ -130,6 +146,31 @@ class Simulation:
         elif cfg.integrator == "kd" and self.staggered:
             self._half_kick(+1.0)
             self.staggered = False
+
+    def _self_check(self) -> float:
+        """Multi-rank GPU start-up (collective): the gated launch's bitwise self-check
+        against the ungated schedule (runtime/selfcheck.py; the CLI's default picks overlap 3
+        only if it passes, as bench.py does), or a one-step probe; both from the run's IC
+        family, which the caller then (re)loads. Returns seconds per step."""
+        from ..ops._native import MODE_IDS
+        from .selfcheck import gated_self_check
+
+        eng, cfg = self.engine, self.cfg
+
+        def reload():
+            eng.init_ics(cfg.init, cfg.seed)
+
+        if eng.native_layout["mode"] == MODE_IDS["sym"] and cfg.overlap == -1 and \
+                eng.overlap == 3:
+            _, self.overlap_check, per_step = gated_self_check(eng, self.dist, comm, reload)
+            return per_step
+        reload()
+        eng.sync()
+        comm.barrier(self.dist)
+        t0 = time.perf_counter()
+        eng.step(1)
+        eng.sync()
+        return comm.allreduce_max(self.dist, time.perf_counter() - t0)
 
     @property
     def device(self) -> str:
@@ -258,7 +299,9 @@ class Simulation:
             gi = self.engine.graph_info()
             extra.update(work_audit="ok" if per else "n/a (one-sided schedule)",
                          overlap=self.engine.overlap, graph=gi["mode"],
-                         graph_segments=gi["segments"] or None)
+                         graph_segments=gi["segments"] or None,
+                         overlap_check=self.overlap_check,
+                         step_timeout_s=self.engine.step_timeout_s or None)
         if c0 is not None:
             extra["conservation"] = conservation_summary(c0, self.conserved(), samples)
         lay = getattr(self.engine, "native_layout", {})

@@ -15,6 +15,8 @@
 #   trace[:<rank_shape args>] rocprofv3 kernel trace of bench/rank_shape.py + overlap report
 #   rankprof[:<rank_shape args>] rocprofv3 kernel-trace stats of bench/rank_shape.py
 #   counters                  rocprofv3 -L (the PMC counters this box offers)
+#   hash[:<native dir>]       state hashes after 3 steps (scripts/state_hash.py, HASH_CASES)
+#   accerr                    per-body error of the sym step path at 4K and 64K (accel_err.py)
 #   ipc                       two-process HIP IPC with / without HSA_ENABLE_IPC_MODE_LEGACY=0
 #   abaudit[:<bench args>]    interleaved bench.py A/B of the work-audit counter (GRAVSIM_AUDIT)
 #   abfork[:<bench args>]     reduce-phase span per step: row reduce forked / node split A/B
@@ -79,6 +81,19 @@ for task in "$@"; do
         --output-format csv -- python bench/rank_shape.py $a
       head -8 $out/rankprof/rp_kernel_stats.csv ;;
     counters) step 120 $out/counters.txt rocprofv3 -L ;;
+    hash)
+      cases=${HASH_CASES:-65536:fp32:auto:1,1048576:fp32:auto:1,65536:fp32:exact:1,524288:fp64:auto:1,65536:fp64:exact:1,262144:fp32:auto:3,262144:fp32:auto:8,1048576:fp32:auto:8}
+      tag=$(basename "${a:-in-tree}")
+      if [ -n "$a" ]; then
+        step 600 $out/hash_$tag.jsonl env GRAVSIM_NATIVE_DIR="$a" python -u scripts/state_hash.py --cases $cases
+      else
+        step 600 $out/hash_$tag.jsonl python -u scripts/state_hash.py --cases $cases
+      fi
+      cat $out/hash_$tag.jsonl ;;
+    accerr)
+      step 300 $out/accel_err.txt python -u scripts/accel_err.py --n 4096
+      step 300 $out/accel_err_64k.txt python -u scripts/accel_err.py --n 65536
+      cat $out/accel_err.txt $out/accel_err_64k.txt ;;
     abfork)
       # reduce-phase span per step with the row reduce forked beside the node reduce (1) or
       # after it (0), from kernel traces of the 1M bench (scripts/reduce_span.py)

@@ -74,7 +74,16 @@ def test_bench_gpus_without_devices_refused():
 def test_bench_self_launches_two_ranks():
     """No launcher + --gpus 2: bench.py starts 2 ranks under torch.distributed.run. Both come
     up with WORLD_SIZE=2 (the gloo control group forms) and stop at the GPU check here."""
+    import json
+
     r = _bench(["--gpus", "2", "--n", "4096", "--steps", "1"], {"GRAVSIM_RCCL_RANK_HOSTS": "1"})
     assert r.returncode != 0
-    assert r.stderr.count("bench.py needs a HIP device") == 2, r.stderr[-2000:]
+    # rank 0's guard reports the job in one error line (parallel/guard.py), with both ranks'
+    # records: both reached the device stage and failed there
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, (r.stdout[-2000:], r.stderr[-2000:])
+    e = lines[0]
+    assert e["status"] == "error" and e["stage"] == "device" and e["n_gpus"] == 2, e
+    assert [x["stage"] for x in e["config"]["ranks"]] == ["device", "device"]
+    assert "bench.py needs a HIP device" in e["error"]
     assert "--gpus 2 but" not in r.stderr  # the children saw WORLD_SIZE == --gpus
