@@ -176,10 +176,18 @@ def momentum(dist, comm, vel, mass):
         comm.allreduce_sum(dist, scale)
 
 
-def sampled_error(eng, cfg, samples: int, seed: int = 7) -> float:
-    """Max over sampled own bodies of |a_gpu - a_ref| / |a_ref|, where a_gpu is the step's own
-    force path (sym kernels, configured cutoff mode) and a_ref an fp64 row sum over all N
-    bodies by the native CPU engine (4 blocks of samples/4 contiguous rows). Collective."""
+# Rounding bound of the sampled accuracy gate: |a_gpu - a_ref| <= ACC_BOUND_C * eps_dtype *
+# sum_j |term_ij| per body and component (the small-N kernel tests use the same form,
+# tests/test_gpu_kernels.py assert_close_sum).
+ACC_BOUND_C = 128.0
+
+
+def sampled_error(eng, cfg, samples: int, seed: int = 7) -> tuple[float, float]:
+    """(max relative error, max bound ratio) over sampled own bodies: |a_gpu - a_ref| / |a_ref|
+    and |a_gpu - a_ref| / (eps * sum_j |term_ij|) per component, where a_gpu is the step's own
+    force path (sym kernels, configured cutoff mode) and a_ref, sum |term| an fp64 row sum over
+    all N bodies by the native CPU engine (4 blocks of samples/4 contiguous rows). The bound
+    ratio must stay <= ACC_BOUND_C. Collective."""
     import numpy as np
 
     from gravsim.ops import _native
@@ -189,28 +197,30 @@ def sampled_error(eng, cfg, samples: int, seed: int = 7) -> float:
     L = eng.layout
     real = max(0, min(L.n_local, cfg.n - L.local_begin))
     if samples <= 0 or real == 0:
-        return 0.0
+        return 0.0, 0.0
     rng = np.random.default_rng(seed + eng.rank)
     blk = max(1, min(samples // 4, real))
     starts = sorted(set(int(x) for x in rng.integers(0, real - blk + 1, size=4)))
     mu = cfg.G * st.mass
-    X = np.zeros((L.n_pad, 4))
-    X[:cfg.n, :3] = st.pos
-    X[:cfg.n, 3] = mu
+    X = np.zeros((cfg.n, 4))
+    X[:, :3] = st.pos  # (the device positions, exactly)
+    X[:, 3] = mu.astype(np.float32) if cfg.dtype == "fp32" else mu  # mu as the kernel sees it
     lib = _native.cpu_lib()
-    worst = 0.0
+    eps = 2.0 ** -24 if cfg.dtype == "fp32" else 2.0 ** -53
+    worst, ratio = 0.0, 0.0
     eps2 = cfg.softening ** 2  # the intended physics: hard cutoff, no core
     for s0 in starts:
         g0 = L.local_begin + s0
-        out = np.zeros((blk, 4))
-        _native.check(lib, lib.gs_cpu_accel_f64(_native.dptr(X), cfg.n, g0, g0 + blk, L.chunk,
-                                                cfg.cutoff ** 2, eps2, _native.dptr(out)),
-                      "cpu accel")
-        ref = out[:, :3]
+        out = np.zeros((blk, 8))
+        _native.check(lib, lib.gs_cpu_accel_abs_f64(_native.dptr(X), cfg.n, g0, g0 + blk,
+                                                    cfg.cutoff ** 2, eps2, _native.dptr(out)),
+                      "cpu accel abs")
+        ref, absref = out[:, :3], out[:, 4:7]
         got = a_gpu[s0:s0 + blk, :3]
         err = np.linalg.norm(got - ref, axis=1) / np.maximum(np.linalg.norm(ref, axis=1), 1e-300)
         worst = max(worst, float(err.max()))
-    return worst
+        ratio = max(ratio, float((np.abs(got - ref) / (eps * absref + 1e-300)).max()))
+    return worst, ratio
 
 
 def overlap_self_check(eng, cfg, dist, comm, steps: int = 2):
@@ -364,9 +374,10 @@ def run(a, g) -> int:
 
     # Accuracy of the step's own force path at step 0, and the initial momentum (untimed).
     g.stage("accuracy", budget(2, 180))
-    err = sampled_error(eng, cfg, a.check_samples) if a.check_samples > 0 else None
-    if err is not None:
-        err = comm.allreduce_max(dist, err)
+    err = bound0 = None
+    if a.check_samples > 0:
+        err, bound0 = (comm.allreduce_max(dist, x) for x in sampled_error(eng, cfg,
+                                                                           a.check_samples))
     _, vel0, mass = own_state(eng)
     p0, pscale = momentum(dist, comm, vel0, mass)
     g.stage("energy", budget(4, 180))
@@ -417,9 +428,14 @@ def run(a, g) -> int:
         pos_t, vel_t, _ = own_state(eng)
         p1, _ = momentum(dist, comm, vel_t, mass)
         drift = float(np.linalg.norm(p1 - p0)) / max(pscale, 1e-300)
-        err_end = sampled_error(eng, cfg, a.check_samples) if a.check_samples > 0 else None
-        if err_end is not None:
-            err_end = comm.allreduce_max(dist, err_end)
+        err_end = bound_end = None
+        if a.check_samples > 0:
+            err_end, bound_end = (comm.allreduce_max(dist, x) for x in sampled_error(
+                eng, cfg, a.check_samples))
+            worst_bound = max(bound0, bound_end)
+            if worst_bound > ACC_BOUND_C:
+                failures.append(f"accuracy: a sampled body's error is {worst_bound:.1f} x "
+                                f"eps x sum|terms| (bound {ACC_BOUND_C:.0f})")
         conservation = None
         if cons0 is not None:
             conservation = conservation_summary(cons0, engine_conserved(eng, dist))
@@ -466,7 +482,7 @@ def run(a, g) -> int:
             eng.set_schedule((2 if a.graph_comm else 1) if a.graph else 0, cap)
             eng.set_overlap(overlap)
         return dict(wall=wall, ginfo=ginfo, mem=mem, hbm_max=hbm_max, failures=failures,
-                    units=units, bad=bad, drift=drift, err_end=err_end,
+                    units=units, bad=bad, drift=drift, err_end=err_end, bound_end=bound_end,
                     conservation=conservation, phase=phase, replay=replay)
 
     res = measure(overlap)
@@ -490,6 +506,7 @@ def run(a, g) -> int:
     failures, units, bad, drift = res["failures"], res["units"], res["bad"], res["drift"]
     err_end, conservation, phase, replay = (res["err_end"], res["conservation"], res["phase"],
                                             res["replay"])
+    bound_end = res["bound_end"]
 
     # The reference's exact hard-cutoff select (cuda.cu:39, mpi.c:64), timed on its own.
     lay = eng.native_layout
@@ -571,6 +588,9 @@ def run(a, g) -> int:
                 "pair_evals_per_s": pairs * a.steps / wall,
                 "sampled_rel_err": err,
                 "sampled_rel_err_final": err_end,
+                # max |a - a_ref| / (eps x sum_j |term_ij|) over the sampled bodies and
+                # components, at step 0 and after the run (gate: <= ACC_BOUND_C)
+                "sampled_bound_ratio": [bound0, bound_end],
                 "momentum_rel_drift": drift,
                 # total energy (kinetic + exact-cutoff potential), momentum and angular momentum
                 # before the warmup and after the timed steps (KD is first order: the energy

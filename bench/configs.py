@@ -77,8 +77,7 @@ def main() -> int:
         print(json.dumps(rows[-1]), flush=True)
 
     os.environ["GRAVSIM_EMULATE_RANK"] = "1"
-    os.environ["GRAVSIM_EMU_COMM_GBPS"] = str(a.comm_gbps)
-    os.environ["GRAVSIM_EMU_COMM_US"] = str(a.comm_us)
+    os.environ["GRAVSIM_EMU_COMM"] = f"{a.comm_gbps},{a.comm_us}"  # GB/s, latency us
     how8 = (f"per-rank emulation, modeled comm {a.comm_gbps:g} GB/s + {a.comm_us:g} us"
             if a.comm_gbps > 0 else "per-rank emulation, comm free")
     import torch  # noqa: F401

@@ -49,21 +49,8 @@ def main() -> int:
                     help="emulated rank: an index, -1 the last, 'all' every rank")
     ap.add_argument("--repeat", type=int, default=1, help="run the whole grid this many times "
                     "(alternating configurations, for A/B on a noisy clock)")
-    ap.add_argument("--lf-fill", default="",
-                    help="comma list of GRAVSIM_SYM_LF_FILL values (local units dispatched first "
-                         "by the gated launch; -1 all); empty: built-in default")
-    ap.add_argument("--parity", default="1",
-                    help="comma list of GRAVSIM_SYM_PARITY (1: antipodal pairs split by row "
-                         "parity; 0: round 1's rows-below-NC/2 rule)")
-    ap.add_argument("--diag-last", default="1",
-                    help="comma list of GRAVSIM_SYM_DIAG_LAST (1: diagonal units dispatched last)")
-    ap.add_argument("--gate-probe", default="0",
-                    help="comma list; timing probes of the gated launch: 0 acquire (real), "
-                         "1 no check (order only), 2 relaxed load")
     a = ap.parse_args()
     os.environ["GRAVSIM_EMULATE_RANK"] = "1"
-    os.environ["GRAVSIM_EMU_COMM_US"] = str(a.comm_us)
-    os.environ["GRAVSIM_EMU_COMM_WGS"] = str(a.comm_wgs)
     import torch  # noqa: F401
 
     import gravsim  # noqa: F401
@@ -76,23 +63,15 @@ def main() -> int:
                                   a.strategy.split(","), a.mode.split(","),
                                   [float(x) for x in a.comm_gbps.split(",")],
                                   [int(x) for x in a.overlap.split(",")],
-                                  [int(x) for x in a.gate_probe.split(",")],
-                                  a.lf_fill.split(","), a.diag_last.split(","),
-                                  a.parity.split(","), a.graph.split(",")))
+                                  a.graph.split(",")))
     runs = []
     for P, *rest in grid:
         ranks = range(P) if a.rank == "all" else \
             [((int(a.rank) if int(a.rank) >= 0 else P - 1) if P > 1 else 0)]
         runs += [(P, r, *rest) for r in ranks]
-    for P, r, ipl, kernel, strategy, mode, gbps, ov, gp, fill, dl, par, gmode in runs * a.repeat:
-        os.environ["GRAVSIM_SYM_DIAG_LAST"] = dl
-        os.environ["GRAVSIM_SYM_PARITY"] = par
-        os.environ["GRAVSIM_EMU_COMM_GBPS"] = str(gbps)
-        os.environ["GRAVSIM_GATE_PROBE"] = str(gp)
-        if fill:
-            os.environ["GRAVSIM_SYM_LF_FILL"] = fill
-        else:
-            os.environ.pop("GRAVSIM_SYM_LF_FILL", None)
+    for P, r, ipl, kernel, strategy, mode, gbps, ov, gmode in runs * a.repeat:
+        # modeled collectives: "GB/s,latency us,workgroups" (stepper.hip GRAVSIM_EMU_COMM)
+        os.environ["GRAVSIM_EMU_COMM"] = f"{gbps},{a.comm_us},{a.comm_wgs}"
         cfg = SimConfig(n=a.n, dtype=a.dtype, device="gpu", ipl=ipl, kernel=kernel,
                         strategy=strategy, mode=mode, graph=gmode != "eager",
                         graph_comm=gmode == "full")
@@ -107,8 +86,10 @@ def main() -> int:
         ms = 1e3 * (time.perf_counter() - t0) / a.steps
         phase = None
         if P > 1:
+            if e.graph_info()["mode"] == "segmented":
+                e.step(2 if e.steps_done % 2 == 0 else 1)  # whole plan periods (bench.py)
             e.set_timing(True)
-            e.step(2)
+            e.step(4)
             phase = e.phase_stats()
             e.set_timing(False)
         key = (ipl, kernel, strategy, mode, a.dtype)
@@ -117,9 +98,7 @@ def main() -> int:
         b = base.get(key)
         print(json.dumps(dict(P=P, rank=r, n=a.n, dtype=a.dtype, ipl=ipl, kernel=kernel,
                               strategy=strategy, mode=e.native_layout["mode"], comm_gbps=gbps,
-                              comm_us=a.comm_us, overlap=ov, gate_probe=gp, lf_fill=fill,
-                              diag_last=int(dl), parity=int(par),
-                              graph=gmode, graph_info=e.graph_info(),
+                              comm_us=a.comm_us, overlap=ov, graph=gmode, graph_info=e.graph_info(),
                               ms_per_step=ms,
                               predicted_efficiency=(b / (P * ms)) if b else None,
                               predicted_body_updates_per_s=a.n / (ms * 1e-3), phase=phase,

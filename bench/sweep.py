@@ -1,7 +1,7 @@
 """Kernel/schedule sweep in ONE process (interleaved rounds, §5.4 rule 24 of the HIP guide).
 
     python bench/sweep.py --n 1048576 --steps 3 --rounds 2 --grid "kernel=lds,smem;ipl=1,2,4;mode=fused,split"
-    python bench/sweep.py --n 65536 --grid "mode=sym;env.GRAVSIM_SYM_DIAG_LAST=0,1"
+    python bench/sweep.py --n 65536 --grid "mode=sym;env.GRAVSIM_SYM_BAND_MB=1540,0"
 Axes named env.<VAR> set that environment variable while the engine is created (the native
 stepper reads its A/B knobs at creation). Prints one JSON line per (config, round) and a
 summary sorted by median ms/step.

@@ -14,7 +14,7 @@ emulation of bench/rank_shape.py, collectives free) and reports, per configurati
   xcd_end_ms   per XCD, when its last unit ended (relative to the launch start)
 
     python bench/unit_timeline.py --n 1048576 --ranks 1,8
-    python bench/unit_timeline.py --n 1048576 --ranks 8 --env GRAVSIM_SYM_DIAG_LAST=0,1
+    python bench/unit_timeline.py --n 1048576 --ranks 8 --env GRAVSIM_SYM_OVERLAP=0,3
 """
 from __future__ import annotations
 

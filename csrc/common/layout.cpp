@@ -26,6 +26,16 @@ void gs_set_error(const char* msg) {
 
 extern "C" int32_t gs_auto_chunk(int64_t n) { return gs::auto_chunk(n); }
 
+// Busiest rank's work over the mean when nranks ranks own whole row blocks of the sym
+// schedule: ceil(B / P) * P / B (B row blocks of the n_pad geometry).
+constexpr double kSymMaxImbalance = 1.25;
+extern "C" double gs_sym_imbalance(int64_t n_pad, int32_t nranks) {
+  if (nranks < 1) return 1e30;
+  const int32_t B = gs::sym_blocks((int32_t)(n_pad / 2048));
+  if (nranks > B) return 1e30;
+  return (double)((B + nranks - 1) / nranks) * nranks / B;
+}
+
 extern "C" int gs_layout_compute(const gs_config* cfg, gs_layout* out) {
   if (!cfg || !out) { gs_set_error("layout: null argument"); return -1; }
   if (cfg->n < 1) { gs_set_error("layout: n must be >= 1"); return -1; }
@@ -56,8 +66,13 @@ extern "C" int gs_layout_compute(const gs_config* cfg, gs_layout* out) {
   // 0.283 vs 0.250 (split wins), 50000 1.21 vs 1.75, 300000 37.5 vs 56.5
   // (profiles/r2_sizes_auto_vs_sym.txt). The partial slots are processed in bands of bounded
   // size (stepper.hip ensure_sym), so memory does not limit the choice either.
+  // A rank owns whole row blocks: with few blocks (B = 8 when NC is an odd multiple of 8) some
+  // P leave the busiest rank far above the mean (P = 7: 2 blocks against 1, twice the work),
+  // which cancels the Newton-3 saving; auto then keeps the split schedule's equal slices.
   const int64_t sym_min = cfg->dtype == GS_FP32 ? 16384 : 32768;
-  if (cfg->mode == GS_MODE_AUTO && sym_ok && cfg->n >= sym_min) sym = true;
+  if (cfg->mode == GS_MODE_AUTO && sym_ok && cfg->n >= sym_min &&
+      gs_sym_imbalance(sym_pad, cfg->nranks) <= kSymMaxImbalance)
+    sym = true;
   if (sym) {
     out->n_pad = sym_pad;
     int32_t a0 = 0, rows = 0;
@@ -89,18 +104,18 @@ extern "C" int gs_layout_compute(const gs_config* cfg, gs_layout* out) {
   int32_t ipl = out->kernel == GS_KERNEL_MFMA ? 1 : cfg->ipl;
   if (ipl <= 0) {
     ipl = f32 ? (out->n_local >= 262144 ? 8 : 4) : 2;
-    while (ipl > 1 && out->n_local % (GS_BLOCK * ipl) != 0) ipl /= 2;
+    while (ipl > 1 && out->n_local % (gs::kForceBlock * ipl) != 0) ipl /= 2;
   }
   if (ipl != 1 && ipl != 2 && ipl != 4 && !(ipl == 8 && cfg->dtype == GS_FP32)) {
     gs_set_error("layout: ipl must be 1, 2, 4 (or 8 for fp32)");
     return -1;
   }
-  if ((out->n_local % (GS_BLOCK * ipl)) != 0) {
+  if ((out->n_local % (gs::kForceBlock * ipl)) != 0) {
     gs_set_error("layout: block*ipl must divide the per-rank body count (raise chunk)");
     return -1;
   }
   out->ipl = ipl;
-  const int64_t i_blocks = out->n_local / (GS_BLOCK * ipl);
+  const int64_t i_blocks = out->n_local / (gs::kForceBlock * ipl);
   int32_t mode = sym ? GS_MODE_SYM : cfg->mode;
   if (out->kernel == GS_KERNEL_MFMA) mode = GS_MODE_SPLIT;
   if (mode == GS_MODE_AUTO) {
@@ -142,18 +157,7 @@ extern "C" int gs_sym_geometry(int64_t n_pad, int32_t* NC, int32_t* H, int32_t* 
     l = 1;
     while (l * 2 <= want) l *= 2;
   }
-  // Tuning override (A/B sweeps only; changes the summation order, hence the bits):
-  // a power of two up to 16, or a multiple of 16.
-  if (const char* e = getenv("GRAVSIM_SYM_L")) {
-    const int32_t v = atoi(e);
-    if (v >= 1 && ((v <= 16 && (v & (v - 1)) == 0) || v % 16 == 0)) l = v;
-  }
-  int32_t d = l < 16 ? 16 / l : 1;
-  // Tuning override (A/B only, changes the bits): parts of the diagonal chunk, 1 .. 16.
-  if (const char* e = getenv("GRAVSIM_SYM_D")) {
-    const int32_t v = atoi(e);
-    if (v >= 1 && v <= 16 && (v & (v - 1)) == 0) d = v;
-  }
+  const int32_t d = l < 16 ? 16 / l : 1;
   if (NC) *NC = nc;
   if (H) *H = h;
   if (L) *L = l;
@@ -162,15 +166,13 @@ extern "C" int gs_sym_geometry(int64_t n_pad, int32_t* NC, int32_t* H, int32_t* 
   return 0;
 }
 
+// Split shell segments per row (the launch tail, gs_kernels.h SymArgs::Kr): S / 16 when a
+// segment spans at least 2 quanta (1M / 8 per rank -0.7 %, 65K -0.7 %, 1M one GPU even;
+// Kr 8 / 16 / 32 within noise: profiles/r3s2_split_segments_ab.jsonl, *_kr_sweep.jsonl).
 extern "C" int32_t gs_sym_split_segments(int64_t n_pad) {
   int32_t NC, H, L, S, D;
   if (gs_sym_geometry(n_pad, &NC, &H, &L, &S, &D)) return 0;
-  int32_t kr = L >= 2 ? S / 16 : 0;
-  if (const char* e = getenv("GRAVSIM_SYM_KR")) {
-    const int32_t v = atoi(e);
-    if (v >= 0 && v <= S && (v == 0 || L >= 2)) kr = v;
-  }
-  return kr;
+  return L >= 2 ? S / 16 : 0;
 }
 
 // Rows [a0, a0 + rows) of rank `rank` of `nranks` in the sym schedule: whole row blocks by
@@ -189,19 +191,11 @@ extern "C" int gs_sym_rank_rows(int64_t n_pad, int32_t nranks, int32_t rank, int
   return 0;
 }
 
-// Largest reduction-tree node level in use: maximal nodes (one per rank for P dividing 64).
-// GRAVSIM_SYM_NODE_SPLIT=1 (A/B only) splits one rank's range into 8 nodes, 8x the threads
-// of the node reduce with the same bits; it measured slower: reduce phase at 1M 1373-1381 us
-// per step against 1342-1343 (kernel traces, profiles/r3_reduce_fork_split_ab.txt).
-extern "C" int32_t gs_sym_node_maxl(int32_t B, int32_t nranks) {
-  const char* v = getenv("GRAVSIM_SYM_NODE_SPLIT");
-  if (v && atoi(v) != 0) return gs::sym_node_maxl(B, nranks);
-  return 30;
-}
-
-// Row blocks and reduction-tree nodes: B blocks of RB rows; rank `rank` sends nn dyadic
-// nodes (sub-trees of its block range); nodes of lower ranks come first (nb of them); NN
-// nodes in all.
+// Row blocks and reduction-tree nodes: B blocks of RB rows; rank `rank` sends nn maximal
+// dyadic nodes (sub-trees of its block range; one per rank for P dividing 64); nodes of lower
+// ranks come first (nb of them); NN nodes in all. (Splitting one rank's range into 8 nodes,
+// 8x the threads of the node reduce with the same bits, measured slower: reduce phase at 1M
+// 1373-1381 us per step against 1342-1343, profiles/r3_reduce_fork_split_ab.txt.)
 extern "C" int gs_sym_nodes(int64_t n_pad, int32_t nranks, int32_t rank, int32_t* B, int32_t* RB,
                             int32_t* nn, int32_t* nb, int32_t* NN) {
   if (gs_sym_rank_rows(n_pad, nranks, rank, nullptr, nullptr)) return -1;
@@ -209,8 +203,7 @@ extern "C" int gs_sym_nodes(int64_t n_pad, int32_t nranks, int32_t rank, int32_t
   int32_t before = 0, total = 0, mine = 0;
   for (int32_t q = 0; q < nranks; ++q) {
     const int32_t k = gs::sym_node_count(gs::sym_blk_lo(b, nranks, q),
-                                         gs::sym_blk_lo(b, nranks, q + 1),
-                                         gs_sym_node_maxl(b, nranks));
+                                         gs::sym_blk_lo(b, nranks, q + 1));
     if (q < rank) before += k;
     if (q == rank) mine = k;
     total += k;
@@ -235,10 +228,9 @@ static int32_t sym_row_owner(int32_t A, int32_t NC, int32_t nranks) {
 // 1 .. NC/2 - 1 belong to the row below; each antipodal pair {A, A + NC/2} to one of its two
 // rows, by parity (A < NC/2 takes it iff A is even; NC/2 is a multiple of 4, so A + NC/2 has
 // A's parity and takes it iff A is odd), so any block of rows holds as many long rows as
-// short ones. parity = 0: round 1's rule (rows A < NC/2 take every antipodal pair). Mirrors
-// shell_len() in nbody_sym.hip.
-extern "C" int32_t gs_sym_shell_len(int32_t A, int32_t NC, int32_t parity) {
-  const bool takes = parity ? (A < NC / 2) == ((A & 1) == 0) : A < NC / 2;
+// short ones. Mirrors shell_len() in nbody_sym.hip.
+extern "C" int32_t gs_sym_shell_len(int32_t A, int32_t NC) {
+  const bool takes = (A < NC / 2) == ((A & 1) == 0);
   return takes ? NC / 2 : NC / 2 - 1;
 }
 
@@ -246,8 +238,8 @@ extern "C" int32_t gs_sym_shell_len(int32_t A, int32_t NC, int32_t parity) {
 // 16 quanta per chunk) whose j-chunks A+1 .. all lie in the rank rows [a0, a0 + rows); wrapped
 // chunks count as remote. The force kernel's units 4/5 test in quanta.
 static int32_t sym_local_segs(int32_t A, int32_t NC, int32_t a0, int32_t rows, int32_t L,
-                              int32_t S, int32_t parity) {
-  const int32_t h = gs_sym_shell_len(A, NC, parity);
+                              int32_t S) {
+  const int32_t h = gs_sym_shell_len(A, NC);
   const int32_t segs = (16 * h + L - 1) / L;
   const int32_t own_after = a0 + rows - 1 - A;
   int32_t n;
@@ -264,9 +256,9 @@ static int32_t sym_local_segs(int32_t A, int32_t NC, int32_t a0, int32_t rows, i
 // segments); the rest follow the ungated order: shell segments row by row, then the diagonal
 // parts. Returns the entry count (rows * (S + D)), 0 if the 16-bit fields cannot hold the
 // geometry, -1 on error (cap too small, bad arguments).
-extern "C" int64_t gs_sym_unit_map(int64_t n_pad, int32_t rank, int32_t nranks, int32_t parity,
-                                   int64_t fill, int32_t* out, int64_t cap) {
-  return gs_sym_unit_map_kr(n_pad, rank, nranks, parity, fill, 0, out, cap);
+extern "C" int64_t gs_sym_unit_map(int64_t n_pad, int32_t rank, int32_t nranks, int64_t fill,
+                                   int32_t* out, int64_t cap) {
+  return gs_sym_unit_map_kr(n_pad, rank, nranks, fill, 0, out, cap);
 }
 
 // The same order with the last kr shell segments of every row split (gs_kernels.h SymArgs::Kr):
@@ -274,8 +266,7 @@ extern "C" int64_t gs_sym_unit_map(int64_t n_pad, int32_t rank, int32_t nranks, 
 // half), row by row, so the launch ends with half-length units. Rows < 8192 (13-bit field);
 // rows * (S + D + kr) entries.
 extern "C" int64_t gs_sym_unit_map_kr(int64_t n_pad, int32_t rank, int32_t nranks,
-                                      int32_t parity, int64_t fill, int32_t kr, int32_t* out,
-                                      int64_t cap) {
+                                      int64_t fill, int32_t kr, int32_t* out, int64_t cap) {
   int32_t NC, H, L, S, D, a0, rows;
   if (nranks < 1 || rank < 0 || rank >= nranks || kr < 0 ||
       gs_sym_geometry(n_pad, &NC, &H, &L, &S, &D) ||
@@ -286,18 +277,14 @@ extern "C" int64_t gs_sym_unit_map_kr(int64_t n_pad, int32_t rank, int32_t nrank
   const int64_t total = (int64_t)rows * (per + kr);
   if (rows >= (kr > 0 ? 8192 : 32768) || per >= 65536) return 0;
   if (!out || cap < total) return -1;
-  // GRAVSIM_SYM_DIAG_TAIL=1 (A/B): the diagonal parts (one-sided, the shortest units) all go
-  // last instead of into the local prefix, to fill the launch's final wave.
-  const char* dte = getenv("GRAVSIM_SYM_DIAG_TAIL");
-  const bool diag_tail = dte && atoi(dte) != 0;
   std::vector<int32_t> nl(rows);
   std::vector<char> moved((size_t)rows * per, 0);
   for (int32_t r = 0; r < rows; ++r)  // split segments go to the end
     for (int32_t u = S - kr; u < S; ++u) moved[(size_t)r * per + u] = 1;
   int64_t k = 0;
   for (int32_t r = 0; r < rows; ++r) {
-    nl[r] = sym_local_segs(a0 + r, NC, a0, rows, L, S, parity);
-    for (int32_t q = 0; q < D && !diag_tail && (fill < 0 || k < fill); ++q) {
+    nl[r] = sym_local_segs(a0 + r, NC, a0, rows, L, S);
+    for (int32_t q = 0; q < D && (fill < 0 || k < fill); ++q) {
       out[k++] = (r << 16) | (S + q);
       moved[(size_t)r * per + S + q] = 1;
     }
@@ -330,7 +317,7 @@ extern "C" int64_t gs_sym_unit_map_kr(int64_t n_pad, int32_t rank, int32_t nrank
 // stage (local ones first), row by row within a stage, shell segments before diagonal parts.
 // Returns the entry count, 0 if the fields cannot hold the geometry, -1 on error.
 extern "C" int64_t gs_sym_unit_map_ring(int64_t n_pad, int32_t rank, int32_t nranks,
-                                        int32_t parity, int64_t fill, int32_t* out, int64_t cap) {
+                                        int64_t fill, int32_t* out, int64_t cap) {
   int32_t NC, H, L, S, D, a0, rows;
   if (nranks < 1 || rank < 0 || rank >= nranks || gs_sym_geometry(n_pad, &NC, &H, &L, &S, &D) ||
       gs_sym_rank_rows(n_pad, nranks, rank, &a0, &rows))
@@ -343,7 +330,7 @@ extern "C" int64_t gs_sym_unit_map_ring(int64_t n_pad, int32_t rank, int32_t nra
   std::vector<int8_t> stage((size_t)total, 0);
   for (int32_t r = 0; r < rows; ++r) {
     const int32_t A = a0 + r;
-    const int32_t segs = (16 * gs_sym_shell_len(A, NC, parity) + L - 1) / L;
+    const int32_t segs = (16 * gs_sym_shell_len(A, NC) + L - 1) / L;
     for (int32_t g = 0; g < S && g < segs; ++g) {
       const int32_t q0 = g * L, q1 = (g + 1) * L - 1;  // quanta of the shell, 16 per chunk
       int32_t st = 0;
@@ -359,7 +346,7 @@ extern "C" int64_t gs_sym_unit_map_ring(int64_t n_pad, int32_t rank, int32_t nra
   std::vector<char> moved((size_t)total, 0);
   int64_t k = 0;
   for (int32_t r = 0; r < rows; ++r) {  // the local prefix, exactly as gs_sym_unit_map
-    nl[r] = sym_local_segs(a0 + r, NC, a0, rows, L, S, parity);
+    nl[r] = sym_local_segs(a0 + r, NC, a0, rows, L, S);
     for (int32_t q = 0; q < D && (fill < 0 || k < fill); ++q) {
       out[k++] = (r << 16) | (S + q);
       moved[(size_t)r * per + S + q] = 1;

@@ -33,28 +33,19 @@ template <> struct VecT<float> { using type = float __attribute__((ext_vector_ty
 template <> struct VecT<double> { using type = double __attribute__((ext_vector_type(4))); };
 template <typename T> using V4 = typename VecT<T>::type;
 
-constexpr int kBlock = GS_BLOCK;  // default 256 = 4 waves of 64
+constexpr int kBlock = kForceBlock;  // 256 = 4 waves of 64
 
 __device__ __forceinline__ float rsqrt_dev(float x) { return __builtin_amdgcn_rsqf(x); }
 
 // fp64: v_rsq_f64 seed (max relative error 5.2e-8, measured: profiles/r1_microbench_v3.jsonl)
 // + one Halley step, cubically convergent: e = 1 - x y^2, y <- y + y e (1/2 + 3/8 e).
 // (5.2e-8)^3 is far below 2^-53, so one step reaches double precision in 5 f64 ops where two
-// Newton steps need 7.
+// Newton steps need 7 (512K fp64: profiles/r1_sweep_512k_fp64_halley.log vs _newton.log).
 __device__ __forceinline__ double rsqrt_dev(double x) {
-#ifdef GS_FP64_NEWTON  // A/B reference: two Newton-Raphson steps
-  double y = __builtin_amdgcn_rsq(x);
-  const double hx = 0.5 * x;
-  double e = __builtin_fma(-hx * y, y, 0.5);
-  y = __builtin_fma(y, e, y);
-  e = __builtin_fma(-hx * y, y, 0.5);
-  return __builtin_fma(y, e, y);
-#else
   const double y = __builtin_amdgcn_rsq(x);
   const double e = __builtin_fma(-x * y, y, 1.0);
   const double p = __builtin_fma(e, 0.375, 0.5);
   return __builtin_fma(y * e, p, y);
-#endif
 }
 
 __device__ __forceinline__ float fma_(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
@@ -74,7 +65,6 @@ __device__ __forceinline__ void interact(T xi, T yi, T zi, T xj, T yj, T zj, T m
                                          T eps2, T& ax, T& ay, T& az, T& ph) {
   const T dx = xj - xi, dy = yj - yi, dz = zj - zi;
   const T r2 = fma_(dz, dz, fma_(dy, dy, fma_(dx, dx, eps2)));
-#ifndef GS_FP64_HALLEY_STEP
   if constexpr (sizeof(T) == 8 && FM != FM_PHI) {
     // fp64 step path: refine r^-3 directly instead of r^-1. With y0 = v_rsq_f64(r2) and
     // e = 1 - r2 y0^2 (|e| <= 1.1e-7), r^-3 = y0^3 (1 - e)^(-3/2) = y0^3 (1 + 3/2 e + 15/8 e^2)
@@ -96,7 +86,6 @@ __device__ __forceinline__ void interact(T xi, T yi, T zi, T xj, T yj, T zj, T m
     az = fma_(s, dz, az);
     return;
   }
-#endif
   T inv;
   if constexpr (FM == FM_FAST) {
     inv = rsqrt_dev(r2);
@@ -118,10 +107,10 @@ __device__ __forceinline__ void interact(T xi, T yi, T zi, T xj, T yj, T zj, T m
   if constexpr (FM == FM_PHI) ph += mi;
 }
 
-#ifndef GS_NO_EXPLICIT_PK
 // fp32, pairs of i per lane as 2-vectors: every op but the rsq is one v_pk_* for two
 // interactions, and the j scalar is broadcast by op_sel instead of SGPR-pair copies. Each
-// element sees exactly the scalar interact() arithmetic, so results are bit-identical.
+// element sees exactly the scalar interact() arithmetic, so results are bit-identical
+// (+10 % over the compiler's own SLP packing: profiles/r1_ab_explicit_pk.jsonl).
 using f2 = float __attribute__((ext_vector_type(2)));
 
 template <int FM>
@@ -144,7 +133,6 @@ __device__ __forceinline__ void interact_pk(f2 xi, f2 yi, f2 zi, float xj, float
   ay = __builtin_elementwise_fma(s, dy, ay);
   az = __builtin_elementwise_fma(s, dz, az);
 }
-#endif
 
 template <typename T, int IPL>
 struct IState {
@@ -161,7 +149,6 @@ __device__ __forceinline__ void zero_chunk(IState<T, IPL>& s) {
 
 template <typename T, int IPL, int FM>
 __device__ __forceinline__ void interact_all(IState<T, IPL>& s, const V4<T>& q, T cut2, T eps2) {
-#ifndef GS_NO_EXPLICIT_PK
   if constexpr (sizeof(T) == 4 && IPL % 2 == 0 && FM != FM_PHI) {
 #pragma unroll
     for (int k = 0; k < IPL; k += 2) {
@@ -174,7 +161,6 @@ __device__ __forceinline__ void interact_all(IState<T, IPL>& s, const V4<T>& q, 
     }
     return;
   }
-#endif
 #pragma unroll
   for (int k = 0; k < IPL; ++k)
     interact<T, FM>(s.x[k], s.y[k], s.z[k], q.x, q.y, q.z, q.w, cut2, eps2, s.ax[k], s.ay[k],
@@ -182,19 +168,9 @@ __device__ __forceinline__ void interact_all(IState<T, IPL>& s, const V4<T>& q, 
 }
 
 
-// Optional occupancy floor for the force kernels (A/B knob): waves per SIMD.
-#ifdef GS_WAVES_PER_EU
-#define GS_WPE __attribute__((amdgpu_waves_per_eu(GS_WAVES_PER_EU)))
-#else
-#define GS_WPE
-#endif
-
-// LDS tile geometry: kTileBytes per tile buffer (default 4 KiB = 256 fp32 / 128 fp64 bodies),
+// LDS tile geometry: kTileBytes per tile buffer (4 KiB = 256 fp32 / 128 fp64 bodies),
 // double-buffered. Each wave-instruction of the fill moves one 1-KiB piece.
-#ifndef GS_TILE_BYTES
-#define GS_TILE_BYTES 4096
-#endif
-constexpr int kTileBytes = GS_TILE_BYTES;
+constexpr int kTileBytes = 4096;
 static_assert(kTileBytes % 1024 == 0, "tile must be whole 1 KiB wave pieces");
 template <typename T> struct Tile { static constexpr int kBodies = kTileBytes / sizeof(V4<T>); };
 
@@ -271,23 +247,15 @@ __device__ __forceinline__ void sweep_smem(const V4<T>* __restrict__ X, int64_t 
     // guarantees scalar (s_load) loads even where the compiler cannot prove no-clobber.
     using CV4 = const __attribute__((address_space(4))) V4<T>;
     CV4* p = (CV4*)(X + (int64_t)c * chunk);
-#ifdef GS_SMEM_NO_PREFETCH
-    for (int64_t j = 0; j < chunk; j += 4) {
-#pragma unroll
-      for (int u = 0; u < 4; ++u) interact_all<T, IPL, FM>(st, p[j + u], cut2, eps2);
-    }
-#else
     // Software pipeline: the next 4 j-bodies (one s_load_dwordx16 for fp32) are requested
     // before the current 4 are consumed, so scalar-cache / L2 latency overlaps the VALU work.
     V4<T> q0 = p[0], q1 = p[1], q2 = p[2], q3 = p[3];
     // Scalar loads return out of order, so any wait is lgkmcnt(0). Drain the first batch
     // here; otherwise the wait for it lands inside the loop after the next prefetch is
     // issued and stalls on that prefetch every iteration.
-#ifndef GS_SMEM_NO_DRAIN
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
     __builtin_amdgcn_sched_barrier(0);
-#endif
     for (int64_t j = 4; j < chunk; j += 4) {
       const V4<T> n0 = p[j], n1 = p[j + 1], n2 = p[j + 2], n3 = p[j + 3];
       __builtin_amdgcn_sched_barrier(0);  // keep the loads at the top of the iteration
@@ -301,7 +269,6 @@ __device__ __forceinline__ void sweep_smem(const V4<T>* __restrict__ X, int64_t 
     interact_all<T, IPL, FM>(st, q1, cut2, eps2);
     interact_all<T, IPL, FM>(st, q2, cut2, eps2);
     interact_all<T, IPL, FM>(st, q3, cut2, eps2);
-#endif
     on_chunk(c);
   }
 }
@@ -350,7 +317,7 @@ __device__ __forceinline__ void integrate_store(const KArgs<T>& a, const IState<
 // SPLIT: grid (i_blocks, groups). Workgroup (b, g) sweeps chunks of group g and stores one
 // partial (ax, ay, az, sum mu/r) per chunk: partial[c * n_local + i].
 template <typename T, int IPL, int KV, int FM>
-__global__ __launch_bounds__(kBlock) GS_WPE void force_split_kernel(KArgs<T> a) {
+__global__ __launch_bounds__(kBlock) void force_split_kernel(KArgs<T> a) {
   __shared__ __attribute__((aligned(16))) V4<T> tile[2][Tile<T>::kBodies];
   const int64_t ib = (int64_t)blockIdx.x * (kBlock * IPL);
   const int sb = min(max(a.skip_begin, a.c_begin), a.c_end);
@@ -381,7 +348,7 @@ __global__ __launch_bounds__(kBlock) GS_WPE void force_split_kernel(KArgs<T> a) 
 // FUSED: grid (i_blocks). One workgroup sweeps every chunk in canonical order and integrates
 // in its epilogue (no partial buffer); used when the i-blocks alone fill the GPU.
 template <typename T, int IPL, int KV, int FM>
-__global__ __launch_bounds__(kBlock) GS_WPE void force_fused_kernel(KArgs<T> a) {
+__global__ __launch_bounds__(kBlock) void force_fused_kernel(KArgs<T> a) {
   __shared__ __attribute__((aligned(16))) V4<T> tile[2][Tile<T>::kBodies];
   const int64_t ib = (int64_t)blockIdx.x * (kBlock * IPL);
   IState<T, IPL> st;

@@ -29,55 +29,24 @@ namespace {
 
 // Workgroup shape per precision: W waves, I i-bodies and J j-bodies per lane; one workgroup
 // holds one 2048-body chunk on its i side (W * 64 * I == kSymC).
-//   fp32: (4 waves, I 8, J 2). (8 waves, I 4, J 4) measured 7 % slower: the per-step j
-//         overhead is amortised over fewer i (profiles/r1_sym_ab.jsonl). I 16 (2 waves,
-//         GS_SYM_I32=16) would halve that overhead but needs 256 VGPRs + 94 AGPRs and spills
-//         to scratch (131 VGPRs at I 8).
-//   fp64: (8 waves, I 4, J GS_SYM_J64 = 1): 14 VGPRs per i-body leave no room for I 8.
+//   fp32: (4 waves, I 8, J 2), the j-pair packed tile (gs_sym_tile.h tile_lds_jp).
+//         (8 waves, I 4, J 4) measured 7 % slower: the per-step j overhead is amortised over
+//         fewer i (profiles/r1_sym_ab.jsonl). I 16 (2 waves) would halve that overhead but
+//         needs 256 VGPRs + 94 AGPRs and spills to scratch (131 VGPRs at I 8).
+//   fp64: (8 waves, I 4, J 1): 14 VGPRs per i-body leave no room for I 8. At 4 waves/SIMD
+//         (2 workgroups of 8 waves) with a few spills it beats 2 waves/SIMD at 130 VGPRs:
+//         512K fp64 124.7 -> 119.6 ms (profiles/r1_sym_ab.jsonl); fp32 gains nothing from an
+//         occupancy floor (170.8 vs 170.1 ms).
 template <typename T>
 struct Shape;
-#ifndef GS_SYM_I32
-#define GS_SYM_I32 8
-#endif
 template <>
 struct Shape<float> {
-  static constexpr int I = GS_SYM_I32, W = kSymC / (64 * I), J = 2;
+  static constexpr int I = 8, W = kSymC / (64 * I), J = 2;
 };
-#ifndef GS_SYM_J64
-#define GS_SYM_J64 1
-#endif
 template <>
 struct Shape<double> {
-  static constexpr int W = 8, I = 4, J = GS_SYM_J64;
+  static constexpr int W = 8, I = 4, J = 1;
 };
-
-// Occupancy floor (waves per SIMD), per precision. fp64 at 4 waves/SIMD (2 workgroups of
-// 8 waves) with a few spills beats 2 waves/SIMD at 130 VGPRs: 512K fp64 124.7 -> 119.6 ms
-// with J 1 (profiles/r1_sym_ab.jsonl). fp32 gains nothing from it (170.8 vs 170.1 ms).
-#ifdef GS_SYM_WAVES_PER_EU
-#define GS_SYM_WPE32 __attribute__((amdgpu_waves_per_eu(GS_SYM_WAVES_PER_EU)))
-#else
-#define GS_SYM_WPE32
-#endif
-#ifndef GS_SYM_WAVES_PER_EU64
-#define GS_SYM_WAVES_PER_EU64 4
-#endif
-#define GS_SYM_WPE64 __attribute__((amdgpu_waves_per_eu(GS_SYM_WAVES_PER_EU64)))
-
-#ifndef GS_SYM_JLDS
-#define GS_SYM_JLDS 1
-#endif
-// fp32 j positions: staged in LDS and read per step (1), or held in registers and rotated
-// with DPP (0, gs_sym_tile.h tile). fp64 always stages.
-template <typename T>
-constexpr bool kJlds = sizeof(T) == 8 || GS_SYM_JLDS;  // (the exact-cutoff kernels need 1)
-
-// fp32 tile packing: j-pairs (1, gs_sym_tile.h tile_lds_jp) or i-pairs (0, tile_lds).
-#ifndef GS_SYM_JPACK
-#define GS_SYM_JPACK 1
-#endif
-template <typename T>
-constexpr bool kJpack = sizeof(T) == 4 && GS_SYM_JPACK && GS_SYM_JLDS && Shape<T>::J == 2;
 
 template <typename T>
 struct Geo {
@@ -95,12 +64,11 @@ struct Geo {
 // row below; each antipodal pair {A, A + NC/2} by exactly one of its rows, chosen by parity
 // (A < NC/2 takes it iff A is even; NC/2 is a multiple of 4, so A + NC/2 has A's parity and
 // takes it iff A is odd). Every block of rows thus holds as many long (NC/2) as short rows,
-// so the ranks of a P-rank run carry equal work (before: ranks 0 .. P/2-1 held every long
-// row, one more unit per row, and the max over ranks paid for it).
-// (antipodal = 0 restores round 1's rule, rows A < NC/2 take every antipodal pair: A/B only,
-// GRAVSIM_SYM_PARITY=0.)
-__device__ __forceinline__ int shell_len(int A, int NC, int antipodal = 1) {
-  const bool takes = antipodal ? (A < NC / 2) == ((A & 1) == 0) : A < NC / 2;
+// so the ranks of a P-rank run carry equal work (round 1 gave every antipodal pair to the
+// rows A < NC/2, one more unit per row for ranks 0 .. P/2-1, and the max over ranks paid).
+// Mirrors layout.cpp gs_sym_shell_len.
+__device__ __forceinline__ int shell_len(int A, int NC) {
+  const bool takes = (A < NC / 2) == ((A & 1) == 0);
   return takes ? NC / 2 : NC / 2 - 1;
 }
 
@@ -135,12 +103,16 @@ __device__ __forceinline__ void stage_store(V* dst, int b, const V& q) {
   dst[j * sym::kStagedRows + sym::staged_entry(l, 1)] = q;
 }
 
-// i-set of a lane: i-pair packed accumulators, or j-pair packed ones (kJpack).
+// fp32: the j-pair packed tile (packed i-side accumulators); fp64: plain.
+template <typename T>
+constexpr bool kJpack = sizeof(T) == 4;
+
+// i-set of a lane: j-pair packed accumulators (fp32) or plain fp64 ones.
 template <typename T>
 using ISetK = typename std::conditional<kJpack<T>, sym::ISetP<Geo<T>::I>,
                                         sym::ISetT<T, Geo<T>::I>>::type;
 
-// One staging thread's share of a j-tile: one body (thread b < kTileJ), or with kJpack the
+// One staging thread's share of a j-tile: one body (fp64: thread b < kTileJ), or (fp32) the
 // bodies l and 64 + l (thread l < 64) interleaved into the pair layout of tile_lds_jp.
 template <typename T>
 struct StageQ {
@@ -169,7 +141,7 @@ struct StageQ {
 template <typename T>
 struct Smem {
   T slot[2][Geo<T>::W][3][Geo<T>::kTileJ];  // j-side carriers of each wave, double-buffered
-  sym::Vec4<T> jt[kJlds<T> ? 2 : 1][kJlds<T> ? Geo<T>::J * sym::kStagedRows : 1];
+  sym::Vec4<T> jt[2][Geo<T>::J * sym::kStagedRows];     // staged j-tiles, double-buffered
 };
 
 // Visit the unit's j-tiles. SYM: pairs both ways, j-side partials to Pj (the diagonal chunk
@@ -177,7 +149,6 @@ struct Smem {
 template <typename T, bool SYM, bool EXACT>
 __device__ __forceinline__ void run_tiles(const SymArgs& a, ISetK<T>& is, TileSeq<T> seq,
                                           int br, Smem<T>& sm) {
-  static_assert(kJlds<T> || !EXACT, "the DPP-position tile has no exact-cutoff variant");
   using G = Geo<T>;
   using V4 = sym::Vec4<T>;
   constexpr int J = G::J;
@@ -186,49 +157,30 @@ __device__ __forceinline__ void run_tiles(const SymArgs& a, ISetK<T>& is, TileSe
   const T eps2 = (T)a.eps2, cut2 = (T)a.cut2;
   int buf = 0, cur = 0;
   const bool stager = threadIdx.x < StageQ<T>::kThreads;
-  if constexpr (kJlds<T>) {
-    if (!seq.done() && stager) {
-      StageQ<T> sq;
-      sq.load(X4, seq.row0(), threadIdx.x);
-      sq.store(sm.jt[0], threadIdx.x);
-    }
-    __syncthreads();
+  if (!seq.done() && stager) {
+    StageQ<T> sq;
+    sq.load(X4, seq.row0(), threadIdx.x);
+    sq.store(sm.jt[0], threadIdx.x);
   }
+  __syncthreads();
   while (!seq.done()) {
     TileSeq<T> nx = seq;
     nx.next();
     const int d = seq.d(), t = seq.t();
     StageQ<T> q_next;
-    const bool stage_next = kJlds<T> && !nx.done() && stager;
+    const bool stage_next = !nx.done() && stager;
     if (stage_next) q_next.load(X4, nx.row0(), threadIdx.x);  // lands during the arithmetic
     T cx[J], cy[J], cz[J];
+    sym::CSetT<T, J> cs;
+#pragma unroll
+    for (int j = 0; j < J; ++j) cs.cx[j] = cs.cy[j] = cs.cz[j] = T(0);
     if constexpr (kJpack<T>) {
-      sym::CSetT<T, J> cs;
-#pragma unroll
-      for (int j = 0; j < J; ++j) cs.cx[j] = cs.cy[j] = cs.cz[j] = T(0);
       sym::tile_lds_jp<G::I, SYM, EXACT>(is, cs, sm.jt[cur], eps2, cut2);
-#pragma unroll
-      for (int j = 0; j < J; ++j) { cx[j] = cs.cx[j]; cy[j] = cs.cy[j]; cz[j] = cs.cz[j]; }
-    } else if constexpr (kJlds<T>) {
-      sym::CSetT<T, J> cs;
-#pragma unroll
-      for (int j = 0; j < J; ++j) cs.cx[j] = cs.cy[j] = cs.cz[j] = T(0);
-      sym::tile_lds<T, G::I, J, SYM, EXACT>(is, cs, sm.jt[cur], eps2, cut2);
-#pragma unroll
-      for (int j = 0; j < J; ++j) { cx[j] = cs.cx[j]; cy[j] = cs.cy[j]; cz[j] = cs.cz[j]; }
     } else {
-      sym::JSet<J> js;
-      const int64_t row0 = seq.row0();
-#pragma unroll
-      for (int j = 0; j < J; ++j) {
-        const float4 q = X4[row0 + j * 64 + lane];
-        js.x[j] = q.x; js.y[j] = q.y; js.z[j] = q.z; js.mu[j] = q.w;
-        js.cx[j] = js.cy[j] = js.cz[j] = 0.f;
-      }
-      sym::tile<G::I, J, SYM>(is, js, eps2);
-#pragma unroll
-      for (int j = 0; j < J; ++j) { cx[j] = js.cx[j]; cy[j] = js.cy[j]; cz[j] = js.cz[j]; }
+      sym::tile_lds64<G::I, SYM, EXACT>(is, cs, sm.jt[cur], eps2, cut2);
     }
+#pragma unroll
+    for (int j = 0; j < J; ++j) { cx[j] = cs.cx[j]; cy[j] = cs.cy[j]; cz[j] = cs.cz[j]; }
     if constexpr (SYM) {
 #pragma unroll
       for (int j = 0; j < J; ++j) {
@@ -239,7 +191,7 @@ __device__ __forceinline__ void run_tiles(const SymArgs& a, ISetK<T>& is, TileSe
     }
     // jt[cur ^ 1] was last read in the previous tile, before the previous barrier.
     if (stage_next) q_next.store(sm.jt[cur ^ 1], threadIdx.x);
-    if (kJlds<T> || SYM) __syncthreads();
+    __syncthreads();
     if constexpr (SYM) {
       // Sum the waves' carriers in wave order (fixed) and store the tile's j-side partial.
       T* pj = static_cast<T*>(a.Pj) + ((int64_t)br * a.H + (d - 1)) * 3 * kSymC;
@@ -291,14 +243,8 @@ __device__ __forceinline__ bool local_first_unit(const SymArgs& a, int b, int* b
 __device__ __forceinline__ bool gate_open_or_defer(const SymArgs& a, int b, int stage) {
   __shared__ int open_s;
   if (threadIdx.x == 0) {
-    const unsigned* gate = a.gate + stage;
-    // (gate_probe, timing probes of the per-rank emulation only: 1 skips the check, 2 loads
-    // relaxed, 3 acquires at agent scope)
     const bool open =
-        a.gate_probe == 1   ? true
-        : a.gate_probe == 2 ? __hip_atomic_load(gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u
-        : a.gate_probe == 3 ? __hip_atomic_load(gate, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != 0u
-                            : __hip_atomic_load(gate, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != 0u;
+        __hip_atomic_load(a.gate + stage, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != 0u;
     if (!open) {
       const unsigned k =
           __hip_atomic_fetch_add(a.defer, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -344,7 +290,7 @@ __device__ __forceinline__ void force_sym_body(const SymArgs& a, int b) {
   } else if (a.units == 2 || a.units == 4) {  // shell units: all (2) or the non-local ones (4)
     br = b / a.S;
     s = b % a.S;
-  } else if (a.units == 0 && a.diag_last) {
+  } else if (a.units == 0) {
     // Every unit: the shell segments row by row, then all diagonal parts. A diagonal part is
     // one-sided (about half the issue time of a shell segment), so dispatching them last fills
     // the launch's final, partial wave of workgroups with short jobs. With split segments
@@ -363,7 +309,7 @@ __device__ __forceinline__ void force_sym_body(const SymArgs& a, int b) {
       br = (k >> 1) / a.Kr;
       s = ns + (k >> 1) % a.Kr;
     }
-  } else {  // the diagonal ones + the rank-local shell ones (5), or every unit row by row
+  } else {  // the diagonal ones + the rank-local shell ones (5), row by row
     br = b / (a.S + a.D);
     s = b % (a.S + a.D);
   }
@@ -387,7 +333,7 @@ __device__ __forceinline__ void force_sym_body(const SymArgs& a, int b) {
     seq.u = q * plen;
     seq.u1 = seq.u + plen;
   } else {
-    const int h_tiles = shell_len(A, a.NC, a.parity) * G::kTilesPerChunk;
+    const int h_tiles = shell_len(A, a.NC) * G::kTilesPerChunk;
     const int u0 = s * seg_tiles;
     if (u0 >= h_tiles) {  // past this row's shell: never read
       if (count_empty) audit_unit(a, weight);
@@ -503,17 +449,6 @@ __device__ __forceinline__ void force_sym_entry(SymArgs a) {
       force_sym_body<T, EXACT>(a, (int)u);
       __syncthreads();  // next_s and the LDS tiles are rewritten by the next unit
     }
-    if (a.rearm_lastwg && threadIdx.x == 0) {
-      // Round 2's first re-arm (opt-in for its targeted test, docs/DESIGN.md §8): the last
-      // workgroup out (work[1] counts exits; every workgroup's fetches precede its exit add)
-      // zeroes both counters, so the next launch needs no memset.
-      const unsigned e =
-          __hip_atomic_fetch_add(a.work + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-      if (e == gridDim.x - 1) {
-        __hip_atomic_store(a.work, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(a.work + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
   } else {
     const unsigned n = a.defer[0];
     if (blockIdx.x == 0 && threadIdx.x == 0 && n > 0)
@@ -528,11 +463,12 @@ __device__ __forceinline__ void force_sym_entry(SymArgs a) {
 
 // (separate instantiations: the static kernels keep their own register allocation)
 template <bool EXACT, bool DEFER = false, bool DYN = false>
-__global__ __launch_bounds__(Geo<float>::kThreads) GS_SYM_WPE32 void force_sym_kernel_f32(SymArgs a) {
+__global__ __launch_bounds__(Geo<float>::kThreads) void force_sym_kernel_f32(SymArgs a) {
   force_sym_entry<float, EXACT, DEFER, DYN>(a);
 }
 template <bool EXACT, bool DEFER = false, bool DYN = false>
-__global__ __launch_bounds__(Geo<double>::kThreads) GS_SYM_WPE64 void force_sym_kernel_f64(SymArgs a) {
+__global__ __launch_bounds__(Geo<double>::kThreads) __attribute__((amdgpu_waves_per_eu(4)))
+void force_sym_kernel_f64(SymArgs a) {
   force_sym_entry<double, EXACT, DEFER, DYN>(a);
 }
 
@@ -602,7 +538,7 @@ __device__ __forceinline__ void pj_range_add(const SymArgs& a, int A_lo, int A_h
     for (int u = 0; u < U; ++u) {
       const int A = A0 + u;
       const int d = X - A + wrap;
-      const bool ok = A < A_hi && (d != a.NC / 2 || shell_len(A, a.NC, a.parity) == a.NC / 2);
+      const bool ok = A < A_hi && (d != a.NC / 2 || shell_len(A, a.NC) == a.NC / 2);
       const T* p = p0 + u * step;
 #pragma unroll
       for (int k = 0; k < C; ++k) v[u][k] = ok ? p[k * comp_stride] : T(0);
@@ -672,11 +608,10 @@ __global__ __launch_bounds__(256) void sym_node_reduce_kernel(SymArgs a) {
   if (x >= nb) return;
   const int X = (int)(x / kSymC), c = (int)(x % kSymC);
   const int own_lo = a.blk_lo[a.rank], own_hi = a.blk_lo[a.rank + 1];
-  const int maxl = a.node_maxl;
-  int lo = own_lo, l = sym_dyadic_level(lo, own_hi, maxl);
+  int lo = own_lo, l = sym_dyadic_level(lo, own_hi);
   for (int k = 0; k < (int)blockIdx.y; ++k) {
     lo += 1 << l;
-    l = sym_dyadic_level(lo, own_hi, maxl);
+    l = sym_dyadic_level(lo, own_hi);
   }
   TreeAcc<T, 3> t;
   t.pos = 0;
@@ -713,12 +648,11 @@ __device__ __forceinline__ void sym_tree_all(const SymArgs& a, int64_t li, T* S)
   TreeAcc<T, 3> t;
   t.pos = 0;
   const T* R = static_cast<const T*>(a.Rbuf) + li;
-  const int maxl = a.node_maxl;
   int j = 0;
   for (int q = 0; q < a.P; ++q) {
     const int hi = a.blk_lo[q + 1];
     for (int lo = a.blk_lo[q]; lo < hi; ++j) {
-      const int l = sym_dyadic_level(lo, hi, maxl);
+      const int l = sym_dyadic_level(lo, hi);
       const T* p = R + (int64_t)j * 3 * a.n_local;
       T v[3] = {p[0], p[a.n_local], p[2 * a.n_local]};
       t.push(l, v);
@@ -744,7 +678,7 @@ __global__ __launch_bounds__(256) void sym_row_reduce_kernel(SymArgs a) {
                              k * kSymC + c;
   T acc = pd[0];
   for (int q = 1; q < a.D; ++q) acc += pd[q * 3 * kSymC];
-  const int h = shell_len(A, a.NC, a.parity);
+  const int h = shell_len(A, a.NC);
   const int segs = (16 * h + a.L - 1) / a.L;  // shell length in 128-body quanta / L
   const T* __restrict__ p = static_cast<const T*>(a.Pi) + (int64_t)br * a.S * 3 * kSymC +
                             k * kSymC + c;
@@ -845,7 +779,7 @@ __global__ __launch_bounds__(192) void sym_tail_kernel(SymArgs a) {
     const T* pd = static_cast<const T*>(a.Pd) + (int64_t)br * a.D * 3 * kSymC + k * kSymC + c;
     T ti = pd[0];
     for (int q = 1; q < a.D; ++q) ti += pd[q * 3 * kSymC];
-    const int segs = (16 * shell_len(X, a.NC, a.parity) + a.L - 1) / a.L;
+    const int segs = (16 * shell_len(X, a.NC) + a.L - 1) / a.L;
     const T* pi = static_cast<const T*>(a.Pi) + (int64_t)br * a.S * 3 * kSymC + k * kSymC + c;
     const int ns = min(segs, a.S - a.Kr);
     constexpr int U = 8;
@@ -917,7 +851,7 @@ hipError_t launch_force_sym_t(const SymArgs& a, hipStream_t s) {
                                                                                  : a.S + a.D);
   // units 0 (diagonal parts last) and the all-gather units 6 order list every split segment
   // as two half units at their end
-  if (a.Kr > 0 && ((a.units == 0 && a.diag_last) || (a.units == 6 && a.gate_n <= 1)))
+  if (a.Kr > 0 && (a.units == 0 || (a.units == 6 && a.gate_n <= 1)))
     units += a.band_rows * a.Kr;
   if (a.units >= 6 && (a.band_rows != a.rows || !a.lf)) return hipErrorInvalidValue;
   if (a.units == 7) units = a.defer_grid;  // strided walk over the deferred list

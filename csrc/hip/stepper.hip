@@ -155,7 +155,6 @@ gs::SymArgs sym_args(gs_stepper* s, int cur) {
   a.RB = s->sym_RB;
   a.rank = s->cfg.rank;
   a.nn = s->nn[s->cfg.rank];
-  a.node_maxl = gs_sym_node_maxl(s->sym_B, s->cfg.nranks);
   for (int q = 0; q <= s->cfg.nranks && q < 9; ++q) a.blk_lo[q] = s->blk_lo[q];
   a.Bbuf = s->sym_Bb;
   a.S = s->sym_S_n;
@@ -175,7 +174,6 @@ gs::SymArgs sym_args(gs_stepper* s, int cur) {
   a.lf = s->sym_lf;
   a.defer_grid = 2 * s->cus;  // resident force workgroups: 2 per CU
   a.defer_index = 0;
-  a.gate_probe = s->emulate ? s->gate_probe : 0;
   a.utrace = s->utrace;
   if (s->dyn_cap > 1) {
     a.work = s->gate_buf + 4;
@@ -183,8 +181,6 @@ gs::SymArgs sym_args(gs_stepper* s, int cur) {
     a.first_wave = s->sym_first_wave;
   }
   a.trace_defer0 = (int32_t)s->utrace_main;
-  a.diag_last = s->diag_last;
-  a.parity = s->parity;
   a.audit = s->audit;
   return a;
 }
@@ -295,7 +291,7 @@ int choose_groups(gs_stepper* s, int span, bool phi, bool concurrent = false) {
   if (concurrent) return span;
   const int fm = phi ? 2 : (s->exact ? 1 : 0);
   const int64_t resident = (int64_t)(s->occ[fm] > 0 ? s->occ[fm] : 4) * s->cus;
-  const int64_t ib = s->L.n_local / (GS_BLOCK * s->L.ipl);
+  const int64_t ib = s->L.n_local / (gs::kForceBlock * s->L.ipl);
   int best = 1;
   double best_cost = 1e300;
   for (int g = 1; g <= span; ++g) {
@@ -369,13 +365,12 @@ int ring_finish(gs_stepper* s, const gs::KArgs<T>& a) {
 // row blocks, the row reduce and finalize run as one sym_tail_kernel (same bits). Interleaved A/B
 // (profiles/r2_fused_tail_ab.jsonl): 65K 0.707 vs 0.708 ms, 256K 10.51 vs 10.57 ms, but 1M
 // 166.8 vs 166.1 ms, where the fused kernel's fewer threads for the j-side sums lose.
-// GRAVSIM_SYM_FUSED_TAIL=0 / 1 forces the three-kernel / fused tail at any size.
+// gs_stepper_set_tuning forces the three-kernel / fused tail at any size (bitwise tests).
 // Every sym force launch goes through here: it tells the launcher whether the dynamic unit
 // counter is known to be 0 (re-armed by the fused tail kernel enqueued after the previous
 // launch on this stream), then marks it dirty until the next fused tail.
 hipError_t force_sym_launch(gs_stepper* s, gs::SymArgs a, hipStream_t st) {
-  a.work_zero = s->work_zero || s->rearm_lastwg ? 1 : 0;
-  a.rearm_lastwg = s->rearm_lastwg ? 1 : 0;
+  a.work_zero = s->work_zero ? 1 : 0;
   s->work_zero = false;
   if (s->fault_skip && a.work && (a.units == 0 || a.units == 6)) {
     const hipError_t e = hipMemsetD32Async(a.work, (int)s->fault_skip, 1, st);
@@ -433,24 +428,14 @@ int sym_force(gs_stepper* s, gs::SymArgs a, bool overlap_gather, bool exchange =
     }
     if (fused_tail(s)) continue;  // reductions + integrate in sym_tail_kernel (one band)
     const bool last = b0 + a.band_rows >= a.rows;
-    // Without an exchange the row reduce (Pi, Pd -> Ti) and the block / node reduce (Pj) are
-    // independent: fork_row (A/B knob) runs the row reduce on s_rem beside them (a fork /
-    // join inside a captured step graph). In sequence is faster (see fork_row).
-    const bool fork = !xcomm(s) && s->fork_row;
-    if (fork) {
-      GS_HIP(hipEventRecord(s->ev_fork, s->s_comp));
-      GS_HIP(hipStreamWaitEvent(s->s_rem, s->ev_fork, 0));
-      GS_HIP(gs::launch_sym_row_reduce(a, s->s_rem));
-    }
+    // The row reduce (Pi, Pd -> Ti) runs after the block / node reduce (Pj) on the same
+    // stream: forking it onto a second stream measured slower, the two streaming sums contend
+    // (reduce phase at 1M 1533-1592 us per step against 1342-1381 in sequence;
+    // profiles/r3_reduce_fork_split_ab.txt).
     if (a.Bbuf) GS_HIP(gs::launch_sym_block_reduce(a, s->s_comp));  // the band's leaves
     if (last) GS_HIP(gs::launch_sym_node_reduce(a, s->s_comp));
     if (exchange && last && sym_exchange_rccl(s, false)) return -1;
-    if (fork) {
-      GS_HIP(hipEventRecord(s->ev_remote, s->s_rem));
-      GS_HIP(hipStreamWaitEvent(s->s_comp, s->ev_remote, 0));
-    } else {
-      GS_HIP(gs::launch_sym_row_reduce(a, s->s_comp));
-    }
+    GS_HIP(gs::launch_sym_row_reduce(a, s->s_comp));
     if (exchange && last) {
       if (comp_wait(s, s->ev_sym, kMarkExchange)) return -1;
     }
@@ -741,24 +726,24 @@ int gs_stepper_create(const gs_config* cfg, gs_stepper** out) {
   s->cfg = *cfg;
   if (gs_layout_compute(cfg, &s->L)) { delete s; return -1; }
   s->esz = cfg->dtype == GS_FP64 ? 8 : 4;
-  s->timed = getenv("GRAVSIM_PHASE_TIMING") != nullptr;
+  // Environment knobs (read once, here): the per-rank emulation (GRAVSIM_EMULATE_RANK, its
+  // modeled collectives GRAVSIM_EMU_COMM="GB/s[,latency us[,workgroups]]"), the multi-rank
+  // overlap mode (GRAVSIM_SYM_OVERLAP), fault injection (GRAVSIM_FAULT_SKIP_UNITS). Band
+  // budget, tracing and the 1-rank communicator are read where they act.
   s->emulate = getenv("GRAVSIM_EMULATE_RANK") != nullptr && cfg->nranks > 1;
   // Multi-rank sym steps default to the gated local-first launch (3): remote units start as
   // soon as the gather lands, nothing waits on it (see sym_force).
   s->sym_overlap = cfg->nranks > 1 ? 3 : 0;
   if (const char* ov = getenv("GRAVSIM_SYM_OVERLAP")) s->sym_overlap = atoi(ov);
-  if (const char* v = getenv("GRAVSIM_EMU_COMM_GBPS")) s->emu_gbps = atof(v);
-  if (const char* v = getenv("GRAVSIM_EMU_COMM_US")) s->emu_lat_us = atof(v);
-  if (const char* v = getenv("GRAVSIM_EMU_COMM_WGS")) s->emu_wgs = atoi(v);
-  if (const char* v = getenv("GRAVSIM_GATE_PROBE")) s->gate_probe = atoi(v);
+  if (const char* v = getenv("GRAVSIM_EMU_COMM")) {
+    double us = s->emu_lat_us;
+    int wgs = s->emu_wgs;
+    const int got = sscanf(v, "%lf,%lf,%d", &s->emu_gbps, &us, &wgs);
+    if (got >= 2) s->emu_lat_us = us;
+    if (got >= 3) s->emu_wgs = wgs;
+  }
   if (s->esz == 8) s->dyn_cap = 4;  // fp64: 512K 101.9-102.0 ms at 4 vs 102.0-102.5 at 2
-  if (const char* v = getenv("GRAVSIM_SYM_DYN_CAP")) s->dyn_cap = atoi(v);
-  if (const char* v = getenv("GRAVSIM_SYM_DIAG_LAST")) s->diag_last = atoi(v);
-  if (const char* v = getenv("GRAVSIM_SYM_FUSED_TAIL")) s->fuse_tail = atoi(v) != 0 ? 1 : 0;
-  if (const char* v = getenv("GRAVSIM_SYM_PARITY")) s->parity = atoi(v) != 0 ? 1 : 0;
   if (const char* v = getenv("GRAVSIM_FAULT_SKIP_UNITS")) s->fault_skip = (unsigned)atoi(v);
-  if (const char* v = getenv("GRAVSIM_SYM_REARM")) s->rearm_lastwg = strcmp(v, "lastwg") == 0;
-  if (const char* v = getenv("GRAVSIM_SYM_FORK_ROW")) s->fork_row = atoi(v) != 0;  // (A/B)
   const int64_t own_first = s->L.local_begin / s->L.chunk;
   const int64_t own_last = (s->L.local_begin + s->L.n_local) / s->L.chunk;
   s->own_c0 = (int)(own_first < s->L.n_chunks ? own_first : s->L.n_chunks);
@@ -790,9 +775,7 @@ int gs_stepper_create(const gs_config* cfg, gs_stepper** out) {
   }
   {
     const int occ = gs::sym_occupancy(s->esz == 8);
-    s->sym_first_wave = (occ > 0 ? occ : 2) * s->cus;
-    // (tests shrink it so that small runs take the dynamic path too)
-    if (const char* v = getenv("GRAVSIM_SYM_FIRST_WAVE")) s->sym_first_wave = atoi(v);
+    s->sym_first_wave = (occ > 0 ? occ : 2) * s->cus;  // (gs_stepper_set_tuning: tests)
   }
   for (int fm = 0; fm < 3; ++fm)
     s->occ[fm] = s->esz == 4 ? gs::split_occupancy<float>(s->L.kernel, s->L.ipl, fm)
@@ -840,8 +823,8 @@ int gs_stepper_create(const gs_config* cfg, gs_stepper** out) {
   // [0..1] gather gates, [2..3] deferral stats, [4] dynamic unit-fetch counter
   ALLOC_CLEAN(&s->gate_buf, 8 * sizeof(unsigned), "gate");
   FAIL_CLEAN(hipMemsetAsync(s->gate_buf, 0, 8 * sizeof(unsigned), s->s_comp));
-  if (s->L.mode == GS_MODE_SYM && !(getenv("GRAVSIM_AUDIT") && atoi(getenv("GRAVSIM_AUDIT")) == 0)) {
-    // (GRAVSIM_AUDIT=0: no unit counter, for A/B timing of its cost only)
+  if (s->L.mode == GS_MODE_SYM) {
+    // the work audit's unit counter (its cost is within noise: profiles/r3_abaudit*)
     ALLOC_CLEAN(&s->audit, sizeof(unsigned long long), "audit");
     FAIL_CLEAN(hipMemsetAsync(s->audit, 0, sizeof(unsigned long long), s->s_comp));
   }
@@ -852,15 +835,14 @@ int gs_stepper_create(const gs_config* cfg, gs_stepper** out) {
     ALLOC_CLEAN(&s->defer, units * sizeof(unsigned), "defer");
     FAIL_CLEAN(hipMemsetAsync(s->defer, 0, units * sizeof(unsigned), s->s_comp));
     // unit -> row << 16 | segment (bit 31: remote), local units first (layout.cpp).
-    long fill = 4L * s->cus;  // two dispatch waves of 2 workgroups per CU
-    if (const char* v = getenv("GRAVSIM_SYM_LF_FILL")) fill = atol(v);
+    const long fill = 4L * s->cus;  // two dispatch waves of 2 workgroups per CU
     std::vector<int32_t> lf(units - 1);
     s->sym_ring = cfg->strategy == GS_STRATEGY_RING && cfg->nranks > 1;
     const int64_t got =
-        s->sym_ring ? gs_sym_unit_map_ring(s->L.n_pad, cfg->rank, cfg->nranks, s->parity, fill,
-                                           lf.data(), (int64_t)lf.size())
-                    : gs_sym_unit_map_kr(s->L.n_pad, cfg->rank, cfg->nranks, s->parity, fill,
-                                         s->sym_Kr, lf.data(), (int64_t)lf.size());
+        s->sym_ring ? gs_sym_unit_map_ring(s->L.n_pad, cfg->rank, cfg->nranks, fill, lf.data(),
+                                           (int64_t)lf.size())
+                    : gs_sym_unit_map_kr(s->L.n_pad, cfg->rank, cfg->nranks, fill, s->sym_Kr,
+                                         lf.data(), (int64_t)lf.size());
     lf.resize(got > 0 ? (size_t)got : 0);  // 0: geometry too large for the 16-bit fields
     if (!lf.empty()) {
       ALLOC_CLEAN(&s->sym_lf, lf.size() * sizeof(int32_t), "unit_map");
@@ -1045,6 +1027,14 @@ int gs_stepper_set_schedule(gs_stepper* s, int32_t use_graph, int32_t dyn_cap) {
   if (dyn_cap >= 0) s->dyn_cap = dyn_cap;
   s->graph_failed = false;
   s->work_zero = false;  // (a dynamic launch after a static one re-zeroes its counter)
+  drop_graphs(s);
+  return 0;
+}
+
+int gs_stepper_set_tuning(gs_stepper* s, int32_t first_wave, int32_t fused_tail) {
+  if (first_wave > 0) s->sym_first_wave = first_wave;
+  if (fused_tail >= 0) s->fuse_tail = fused_tail ? 1 : 0;
+  s->work_zero = false;
   drop_graphs(s);
   return 0;
 }

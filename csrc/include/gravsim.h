@@ -99,22 +99,24 @@ int64_t gs_sym_bytes(int64_t n_pad, int32_t nranks, int32_t esz);
 int gs_sym_rank_rows(int64_t n_pad, int32_t nranks, int32_t rank, int32_t* a0, int32_t* rows);
 int gs_sym_nodes(int64_t n_pad, int32_t nranks, int32_t rank, int32_t* B, int32_t* RB,
                  int32_t* nn, int32_t* nb, int32_t* NN);
-int32_t gs_sym_node_maxl(int32_t B, int32_t nranks);
-// Shell length of chunk row A (antipodal pairs split by parity; parity 0: rows A < NC/2).
-int32_t gs_sym_shell_len(int32_t A, int32_t NC, int32_t parity);
+// Busiest rank's work over the mean of the sym schedule's whole-row-block ownership
+// (ceil(B / P) * P / B); mode auto picks sym only up to 1.25.
+double gs_sym_imbalance(int64_t n_pad, int32_t nranks);
+// Shell length of chunk row A (the antipodal pairs split between rows by parity).
+int32_t gs_sym_shell_len(int32_t A, int32_t NC);
 // Unit order of the gated sym launch for one rank (see layout.cpp); returns the entry count.
-int64_t gs_sym_unit_map(int64_t n_pad, int32_t rank, int32_t nranks, int32_t parity,
-                        int64_t fill, int32_t* out, int64_t cap);
+int64_t gs_sym_unit_map(int64_t n_pad, int32_t rank, int32_t nranks, int64_t fill,
+                        int32_t* out, int64_t cap);
 // ... with the last kr shell segments of every row split into two half units at the end.
-int64_t gs_sym_unit_map_kr(int64_t n_pad, int32_t rank, int32_t nranks, int32_t parity,
-                           int64_t fill, int32_t kr, int32_t* out, int64_t cap);
+int64_t gs_sym_unit_map_kr(int64_t n_pad, int32_t rank, int32_t nranks, int64_t fill,
+                           int32_t kr, int32_t* out, int64_t cap);
 // Split shell segments per row (SymArgs::Kr) for a geometry: S / 16 when a segment has at
-// least 2 tiles of 128 bodies (L >= 2), else 0; GRAVSIM_SYM_KR overrides (changes the bits).
+// least 2 tiles of 128 bodies (L >= 2), else 0.
 int32_t gs_sym_split_segments(int64_t n_pad);
 // The same for the ring strategy: entries carry the ring stage (bits 28-30) at which the last
 // slice a unit reads arrives, and units are ordered by stage (rows < 4096, nranks <= 8).
-int64_t gs_sym_unit_map_ring(int64_t n_pad, int32_t rank, int32_t nranks, int32_t parity,
-                             int64_t fill, int32_t* out, int64_t cap);
+int64_t gs_sym_unit_map_ring(int64_t n_pad, int32_t rank, int32_t nranks, int64_t fill,
+                             int32_t* out, int64_t cap);
 
 // ---------------------------------------------------------------- counter-based RNG / ICs (host)
 // Fill bodies [begin, end) of the IC family into fp64 arrays (pos/vel: 3 per body, mass: 1).
@@ -130,6 +132,10 @@ int gs_cpu_accel_f32(const float* X4, int64_t n_real, int64_t i0, int64_t i1, in
                      float cut2, float eps2, float* acc4);
 // One KD step for global bodies [i0, i1): reads X4 (full), vel4 (local, i0-based), writes
 // Xnext4 rows [i0, i1) and vel4. Ghost rows (>= n_real) are zeroed.
+// fp64 accelerations of rows [i0, i1) plus, per component, sum_j |term_ij| (8 doubles per
+// row: a_x, a_y, a_z, 0, |.|_x, |.|_y, |.|_z, 0): the scale of a rounding-error bound.
+int gs_cpu_accel_abs_f64(const double* X4, int64_t n_real, int64_t i0, int64_t i1, double cut2,
+                         double eps2, double* out8);
 int gs_cpu_step_f64(const double* X4, double* Xnext4, double* vel4, int64_t n_real, int64_t i0,
                     int64_t i1, int32_t chunk, double dt, double cut2, double eps2);
 int gs_cpu_step_f32(const float* X4, float* Xnext4, float* vel4, int64_t n_real, int64_t i0,
@@ -185,6 +191,11 @@ int32_t gs_stepper_get_dyn_cap(gs_stepper* s);
 // 1 single-rank graphs, 2 multi-rank capture too; dyn_cap <= 1 static units (one per
 // workgroup), > 1 dynamic fetch with that many units per workgroup, < 0 unchanged.
 int gs_stepper_set_schedule(gs_stepper* s, int32_t use_graph, int32_t dyn_cap);
+// Test / A-B tuning of the sym schedule (< 0 or 0: unchanged): first_wave = workgroups of
+// the dynamic launch that take one unit each (default: the resident slots; tests shrink it so
+// small runs fetch dynamically too); fused_tail 1 / 0 forces the one-rank fused reduction
+// tail / the three-kernel tail (default: fused up to 256K bodies). Same bits either way.
+int gs_stepper_set_tuning(gs_stepper* s, int32_t first_wave, int32_t fused_tail);
 // Re-resolve the force path with a new cutoff mode (0 auto, 1 exact select, 2 fast core).
 int gs_stepper_set_cutoff_mode(gs_stepper* s, int32_t mode);
 // Work audit of the sym schedule: force units completed since the last reset (waits for the

@@ -92,37 +92,25 @@ GS_HD int32_t sym_blk_lo(int32_t B, int32_t P, int32_t r) {
   const int32_t base = B / P, rem = B % P;
   return r * base + (r < rem ? r : rem);
 }
-// Level of the dyadic node that starts at block lo inside [lo, hi): the largest l <= maxl
-// with lo % 2^l == 0 and lo + 2^l <= hi.
-GS_HD int32_t sym_dyadic_level(int32_t lo, int32_t hi, int32_t maxl = 30) {
+// Level of the dyadic node that starts at block lo inside [lo, hi): the largest l with
+// lo % 2^l == 0 and lo + 2^l <= hi (maximal nodes).
+GS_HD int32_t sym_dyadic_level(int32_t lo, int32_t hi) {
   int32_t l = 0;
-  while (l < maxl && ((lo >> l) & 1) == 0 && lo + (2 << l) <= hi) ++l;
+  while (((lo >> l) & 1) == 0 && lo + (2 << l) <= hi) ++l;
   return l;
 }
-// Dyadic nodes covering [lo, hi), none above level maxl.
-GS_HD int32_t sym_node_count(int32_t lo, int32_t hi, int32_t maxl = 30) {
+// Dyadic nodes covering [lo, hi).
+GS_HD int32_t sym_node_count(int32_t lo, int32_t hi) {
   int32_t n = 0;
   while (lo < hi) {
-    lo += 1 << sym_dyadic_level(lo, hi, maxl);
+    lo += 1 << sym_dyadic_level(lo, hi);
     ++n;
   }
   return n;
 }
-// Node level cap of the GRAVSIM_SYM_NODE_SPLIT=1 A/B variant (layout.cpp gs_sym_node_maxl):
-// one rank splits its range into 8 nodes (8x the node-reduce threads; the receiver's merge
-// gives the same bits); with several ranks nodes stay maximal, since every node is sent to
-// every other rank.
-GS_HD int32_t sym_node_maxl(int32_t B, int32_t P) {
-  if (P > 1) return 30;
-  int32_t lb = 0;
-  while ((1 << (lb + 1)) <= B) ++lb;
-  return lb > 3 ? lb - 3 : 0;
-}
 
-// Threads per force-kernel workgroup (i-bodies per workgroup = GS_BLOCK * ipl). 256 = 4
-// waves; other values exist for the block-size sweep (scripts/gpu_block_sweep.sh).
-#ifndef GS_BLOCK
-#define GS_BLOCK 256
-#endif
+// Threads per one-sided force-kernel workgroup (i-bodies per workgroup = kForceBlock * ipl):
+// 4 waves (profiles/r1_block_sweep.jsonl).
+constexpr int kForceBlock = 256;
 
 }  // namespace gs

@@ -78,14 +78,15 @@ struct SymArgs {
   int32_t NC, a0, rows, S, L, H, P, real_chunks;
   int32_t D;           // parts of the diagonal chunk (L < 16 quanta: 16 / L)
   int32_t B, RB;       // row blocks and rows per block
-  int32_t rank, nn;    // this rank and the dyadic nodes it reduces and sends
-  int32_t node_maxl;   // largest node level (gs_sym_node_maxl)
+  int32_t rank, nn;    // this rank and the dyadic nodes it reduces and sends (maximal ones)
   int32_t blk_lo[9];   // rank q owns blocks [blk_lo[q], blk_lo[q + 1]), q < P
   int32_t band0, band_rows;  // rows [band0, band0 + band_rows) of this rank (rank-relative)
                              // are in the Pi/Pj/Pd buffers (row index - band0)
   int32_t fp64;        // element type of every array above
   int32_t exact;       // reference hard cutoff (select at cut2) instead of the fast core
-  int32_t units;       // which units a force launch covers: 0 all, 1 diagonal chunks only
+  int32_t units;       // which units a force launch covers: 0 all (shell segments row by row,
+                       // then the diagonal parts, then the split segments as half units:
+                       // short units fill the launch's last wave), 1 diagonal chunks only
                        // (need only the own rows), 2 shell segments only, 4 the shell
                        // segments with a j-chunk outside the own rows, 5 every other unit
                        // (diagonal + rank-local shell: no gathered positions needed),
@@ -103,9 +104,6 @@ struct SymArgs {
   const int32_t* lf;    // units 6 order: unit -> row << 16 | segment (bit 31: remote unit)
   int32_t defer_grid;   // units 7: workgroups walking the deferred list
   int32_t defer_index;  // (device-side) the deferred entry a units-7 workgroup is running
-  int32_t gate_probe;   // timing probe of the emulation only (GRAVSIM_GATE_PROBE): 0 acquire
-  int32_t diag_last;    // units 0: shell segments first, diagonal parts last (else row by row)
-  int32_t parity;       // antipodal chunk pairs split between rows by parity (else A < NC/2)
   // Unit timeline probe (GRAVSIM_UNIT_TRACE, diagnostics only; nullptr otherwise): per force
   // workgroup 4 words {start, end (s_memrealtime, 100 MHz), HW_ID | XCC_ID << 32,
   // row << 32 | segment}, at [blockIdx.x] (units 0/6) or [trace_defer0 + k] (units 7).
@@ -120,11 +118,9 @@ struct SymArgs {
   // work[0] is already 0 on this stream (the fused tail kernel that ran after the previous
   // dynamic launch re-armed it): the launcher skips its memset.
   int32_t work_zero;
-  // GRAVSIM_SYM_REARM=lastwg (targeted test only): the last workgroup of a dynamic launch
-  // re-arms work[0] and its exit count work[1] in-kernel instead of the launcher's memset.
-  int32_t rearm_lastwg;
-  // Work audit (nullptr: off): +1 per force unit that ran to completion (or was empty), so a
-  // step's count must be rows x (S + D) whatever the launch split, deferral or fetch order.
+  // Work audit: +1 per force unit that ran to completion (or was empty), so a step's count
+  // must be rows x (S + D + Kr) whatever the launch split, deferral or fetch order (a split
+  // segment run whole counts its two halves).
   unsigned long long* audit;
 };
 

@@ -110,13 +110,13 @@ struct gs_stepper {
   std::vector<int32_t> nn, nbase;
   bool uniform = true;  // every rank owns the same body count (P | B: ncclAllGather)
   hipEvent_t ev_sym = nullptr;
-  // Per-rank emulation with modeled collectives (GRAVSIM_EMU_COMM_GBPS > 0): every all-gather
+  // Per-rank emulation with modeled collectives (GRAVSIM_EMU_COMM GB/s > 0): every all-gather
   // and node-sum exchange becomes a comm_model_kernel of the same byte count on s_comm.
   double emu_gbps = 0.0, emu_lat_us = 15.0;
   int emu_wgs = 16;
   void* emu_buf = nullptr;
   unsigned long long* utrace = nullptr;  // GRAVSIM_UNIT_TRACE: per force workgroup timeline
-  // Dynamic unit fetch of the sym force launch (GRAVSIM_SYM_DYN_CAP; <= 1: static units):
+  // Dynamic unit fetch of the sym force launch (gs_stepper_set_schedule; <= 1: static units):
   // units per workgroup after the first wave, and the first wave's size (resident slots).
   // 2 (round 3): the shortest-lived dynamic workgroups shorten the launch tail; against 4:
   // 1M / 8 per rank -1.0 %, P = 4 -0.4 %, 1M one GPU -0.2 %, 65K -1.4 %, same bits
@@ -136,10 +136,7 @@ struct gs_stepper {
   // receive) and its unit map orders the remote units by stage.
   bool sym_ring = false;
   unsigned* ring_gate = nullptr;
-  int gate_probe = 0;         // GRAVSIM_GATE_PROBE (emulation timing probes only)
-  int diag_last = 1;          // GRAVSIM_SYM_DIAG_LAST=0: row-by-row unit order (A/B only)
-  int fuse_tail = -1;         // GRAVSIM_SYM_FUSED_TAIL: -1 by size (<= 256K), 0 off, 1 on
-  int parity = 1;             // GRAVSIM_SYM_PARITY=0: round-1 antipodal rule (A/B only)
+  int fuse_tail = -1;         // -1 by size (<= 256K), 0 off, 1 on (gs_stepper_set_tuning)
   // Phase timing of eager steps (timed): one event set per step, summed by phase_stats.
   struct PhaseEv {
     hipEvent_t t0, end, g0, g1, w0, w1, x0, x1, j0, j1;
@@ -162,11 +159,6 @@ struct gs_stepper {
   // force launch starts its unit counter at k instead of 0, so units 0 .. k-1 never run,
   // exactly the failure class of a stale re-armed counter (a memset node when captured).
   unsigned fault_skip = 0;
-  bool rearm_lastwg = false;  // GRAVSIM_SYM_REARM=lastwg: round 2's in-kernel counter re-arm
-  // GRAVSIM_SYM_FORK_ROW=1 (A/B only): the row reduce on a second stream beside the node
-  // reduce. Measured slower: the two streaming sums contend (reduce phase at 1M 1533-1592 us
-  // per step against 1342-1381 in sequence; profiles/r3_reduce_fork_split_ab.txt).
-  bool fork_row = false;
   // Segmented step graph of multi-rank runs (use_graph 1): the compute stream's work between
   // two cross-stream points is captured as one graph segment; the collectives (RCCL, or the
   // emulation's modeled ones) and the event record/wait that order them against the compute

@@ -13,7 +13,7 @@
 #include <random>
 #include <vector>
 
-#include "gs_sym_tile.h"
+#include "sym_probe_tile.h"
 
 #define CK(x)                                                                      \
   do {                                                                             \
@@ -35,8 +35,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
                                                     int reps, float eps2) {
   const int lane = threadIdx.x & 63;
   const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  gs::sym::ISet<I> a;
-  gs::sym::JSet<J> b;
+  gs::sym::probe::ISet<I> a;
+  gs::sym::probe::JSet<J> b;
 #pragma unroll
   for (int i = 0; i < I; ++i) {
     const f4 q = xi[(size_t)wave * 64 * I + i * 64 + lane];
@@ -49,7 +49,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     b.x[j] = q.x; b.y[j] = q.y; b.z[j] = q.z; b.mu[j] = q.w;
     b.cx[j] = b.cy[j] = b.cz[j] = 0.f;
   }
-  for (int r = 0; r < reps; ++r) gs::sym::tile<I, J, SYM>(a, b, eps2);
+  for (int r = 0; r < reps; ++r) gs::sym::probe::tile<I, J, SYM>(a, b, eps2);
 #pragma unroll
   for (int i = 0; i < I; ++i)
     out_i[(size_t)wave * 64 * I + i * 64 + lane] = f4{a.ax[i], a.ay[i], a.az[i], 0.f};
@@ -69,7 +69,7 @@ __global__ __launch_bounds__(256) void dpp_chain_kernel(float* out, int iters, f
   for (int it = 0; it < iters; ++it) {
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
-      if constexpr (MODE == 1) x[u] = gs::sym::sub_from<1>(x[u], cv);
+      if constexpr (MODE == 1) x[u] = gs::sym::probe::sub_from<1>(x[u], cv);
       else x[u] = x[u] - cv;
     }
   }

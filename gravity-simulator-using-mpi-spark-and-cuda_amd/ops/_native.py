@@ -86,16 +86,17 @@ def _declare_common(lib) -> None:
     _sig(lib, "gs_layout_compute", c_int32, [POINTER(GsConfig), POINTER(GsLayout)])
     _sig(lib, "gs_sym_geometry", c_int32, [c_int64] + [POINTER(c_int32)] * 5)
     _sig(lib, "gs_sym_bytes", c_int64, [c_int64, c_int32, c_int32])
-    _sig(lib, "gs_sym_shell_len", c_int32, [c_int32, c_int32, c_int32])
+    _sig(lib, "gs_sym_shell_len", c_int32, [c_int32, c_int32])
+    _sig(lib, "gs_sym_imbalance", c_double, [c_int64, c_int32])
     _sig(lib, "gs_sym_rank_rows", c_int32, [c_int64, c_int32, c_int32, POINTER(c_int32),
                                             POINTER(c_int32)])
     _sig(lib, "gs_sym_nodes", c_int32, [c_int64, c_int32, c_int32] + [POINTER(c_int32)] * 5)
-    _sig(lib, "gs_sym_unit_map", c_int64, [c_int64, c_int32, c_int32, c_int32, c_int64,
+    _sig(lib, "gs_sym_unit_map", c_int64, [c_int64, c_int32, c_int32, c_int64,
                                            POINTER(c_int32), c_int64])
-    _sig(lib, "gs_sym_unit_map_ring", c_int64, [c_int64, c_int32, c_int32, c_int32, c_int64,
+    _sig(lib, "gs_sym_unit_map_ring", c_int64, [c_int64, c_int32, c_int32, c_int64,
                                                 POINTER(c_int32), c_int64])
-    _sig(lib, "gs_sym_unit_map_kr", c_int64, [c_int64, c_int32, c_int32, c_int32, c_int64,
-                                              c_int32, POINTER(c_int32), c_int64])
+    _sig(lib, "gs_sym_unit_map_kr", c_int64, [c_int64, c_int32, c_int32, c_int64, c_int32,
+                                              POINTER(c_int32), c_int64])
     _sig(lib, "gs_sym_split_segments", c_int32, [c_int64])
     _sig(lib, "gs_auto_chunk", c_int32, [c_int64])
     _sig(lib, "gs_ic_fill_host", None, [c_int32, c_uint64, c_int64, c_int64, c_int64, _PD, _PD,
@@ -118,6 +119,8 @@ def cpu_lib():
             _sig(lib, f"gs_cpu_accel_{t}", c_int32, [P, c_int64, c_int64, c_int64, c_int32, T, T, P])
             _sig(lib, f"gs_cpu_step_{t}", c_int32,
                  [P, P, P, c_int64, c_int64, c_int64, c_int32, T, T, T])
+        _sig(lib, "gs_cpu_accel_abs_f64", c_int32, [_PD, c_int64, c_int64, c_int64, c_double,
+                                                    c_double, _PD])
         _sig(lib, "gs_cpu_num_threads", c_int32, [])
         _sig(lib, "gs_cpu_set_threads", c_int32, [c_int32])
         _cpu = lib
@@ -162,6 +165,7 @@ def hip_lib():
         _sig(lib, "gs_stepper_get_overlap", c_int32, [S])
         _sig(lib, "gs_stepper_get_dyn_cap", c_int32, [S])
         _sig(lib, "gs_stepper_set_cutoff_mode", c_int32, [S, c_int32])
+        _sig(lib, "gs_stepper_set_tuning", c_int32, [S, c_int32, c_int32])
         _sig(lib, "gs_stepper_audit", c_int32, [S, POINTER(c_uint64), POINTER(c_uint64)])
         _sig(lib, "gs_stepper_audit_reset", c_int32, [S])
         _sig(lib, "gs_stepper_graph_info", c_int32, [S, POINTER(c_int32), POINTER(c_int32)])

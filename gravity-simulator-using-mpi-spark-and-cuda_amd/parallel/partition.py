@@ -18,7 +18,6 @@ within one block and the reduction tree over the blocks keeps the bits P-indepen
 """
 from __future__ import annotations
 
-import os
 from dataclasses import dataclass
 
 
@@ -85,9 +84,6 @@ def sym_geometry(n_pad: int) -> dict:
         seg = 1
         while seg * 2 <= want:
             seg *= 2
-    v = int(os.environ.get("GRAVSIM_SYM_L", "0") or 0)  # tuning override (layout.cpp)
-    if v >= 1 and ((v <= 16 and v & (v - 1) == 0) or v % 16 == 0):
-        seg = v
     return {"NC": nc, "H": h, "L": seg, "S": -(-16 * h // seg), "D": 16 // seg if seg < 16 else 1}
 
 
@@ -105,26 +101,16 @@ def sym_blk_lo(B: int, P: int, r: int) -> int:
     return r * base + min(r, rem)
 
 
-def dyadic_nodes(lo: int, hi: int, maxl: int = 30) -> list[tuple[int, int]]:
-    """(first block, level) of the aligned power-of-two pieces covering [lo, hi), none above
-    level maxl."""
+def dyadic_nodes(lo: int, hi: int) -> list[tuple[int, int]]:
+    """(first block, level) of the maximal aligned power-of-two pieces covering [lo, hi)."""
     out = []
     while lo < hi:
         l = 0
-        while l < maxl and (lo >> l) & 1 == 0 and lo + (2 << l) <= hi:
+        while (lo >> l) & 1 == 0 and lo + (2 << l) <= hi:
             l += 1
         out.append((lo, l))
         lo += 1 << l
     return out
-
-
-def sym_node_maxl(B: int, P: int) -> int:
-    """Node level cap (layout.cpp gs_sym_node_maxl): nodes are maximal unless the A/B knob
-    GRAVSIM_SYM_NODE_SPLIT=1 splits one rank's range into 8 (measured slower)."""
-    if P > 1 or os.environ.get("GRAVSIM_SYM_NODE_SPLIT", "0") in ("", "0"):
-        return 30
-    lb = B.bit_length() - 1
-    return lb - 3 if lb > 3 else 0
 
 
 def sym_rank_rows(n_pad: int, nranks: int, rank: int) -> tuple[int, int]:
@@ -141,8 +127,7 @@ def sym_rank_rows(n_pad: int, nranks: int, rank: int) -> tuple[int, int]:
 def sym_nodes(n_pad: int, nranks: int) -> list[list[tuple[int, int]]]:
     """Per rank, the reduction-tree nodes it sends (layout.cpp gs_sym_nodes)."""
     B = sym_blocks(n_pad // SYM_CHUNK)
-    return [dyadic_nodes(sym_blk_lo(B, nranks, q), sym_blk_lo(B, nranks, q + 1),
-                         sym_node_maxl(B, nranks))
+    return [dyadic_nodes(sym_blk_lo(B, nranks, q), sym_blk_lo(B, nranks, q + 1))
             for q in range(nranks)]
 
 
@@ -158,13 +143,27 @@ def sym_bytes(n_pad: int, nranks: int, esz: int = 4) -> int:
         (len(nodes[0]) * n_pad + NN * n_local) * 3 * esz
 
 
+SYM_MAX_IMBALANCE = 1.25  # layout.cpp kSymMaxImbalance
+
+
+def sym_imbalance(n_pad: int, nranks: int) -> float:
+    """Work of the busiest rank over the mean when P ranks own whole row blocks: the
+    busiest holds ceil(B / P) of the B blocks (layout.cpp gs_sym_imbalance)."""
+    B = sym_blocks(n_pad // SYM_CHUNK)
+    return -(-B // nranks) * nranks / B
+
+
 def sym_auto(n: int, nranks: int, chunk: int = 0, dtype: str = "fp32") -> bool:
     """Whether mode=auto picks the sym schedule (mirror of gs_layout_compute)."""
-    del chunk  # (the choice depends on n, the rank count and the dtype only)
     # from 16K (fp32) / 32K (fp64) bodies sym wins, padding included
     # (profiles/r2_sizes_auto_vs_sym.txt); the partial slots are processed in bounded bands,
-    # so memory does not limit the choice; any P up to 8 owns whole row blocks
-    return nranks <= 8 and n >= (16384 if dtype == "fp32" else 32768)
+    # so memory does not limit the choice; a P up to 8 owns whole row blocks, unless that
+    # leaves the busiest rank more than 25 % over the mean (few blocks, e.g. 8 blocks at P = 6
+    # or 7: the split schedule's equal slices win there)
+    if nranks > 8 or n < (16384 if dtype == "fp32" else 32768):
+        return False
+    c = chunk if chunk > 0 else auto_chunk(n)
+    return sym_imbalance(sym_pad(n, c), nranks) <= SYM_MAX_IMBALANCE
 
 
 def layout(n: int, rank: int = 0, nranks: int = 1, chunk: int = 0, sym: bool = False) -> Layout:

@@ -219,6 +219,14 @@ class HipEngine:
         _native.check(self.lib, self.lib.gs_stepper_set_schedule(self._s, int(graph),
                                                                  int(dyn_cap)), "schedule")
 
+    def set_tuning(self, first_wave: int = 0, fused_tail: int = -1) -> None:
+        """Test / A-B tuning of the sym schedule, same bits either way: first_wave > 0 sets
+        how many workgroups of a dynamic launch take one unit each (default: the resident
+        slots); fused_tail 1 / 0 forces the one-rank fused reduction tail / the three-kernel
+        tail (default -1: fused up to 256K bodies)."""
+        _native.check(self.lib, self.lib.gs_stepper_set_tuning(self._s, int(first_wave),
+                                                               int(fused_tail)), "tuning")
+
     def set_cutoff_mode(self, mode: str) -> None:
         """Re-resolve the force path: auto | exact (reference hard-cutoff select) | fast."""
         _native.check(self.lib, self.lib.gs_stepper_set_cutoff_mode(

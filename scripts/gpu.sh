@@ -17,9 +17,9 @@
 #   counters                  rocprofv3 -L (the PMC counters this box offers)
 #   hash[:<native dir>]       state hashes after 3 steps (scripts/state_hash.py, HASH_CASES)
 #   accerr                    per-body error of the sym step path at 4K and 64K (accel_err.py)
+#   perturb                   smoke() and the 1M accuracy test on a deliberately broken build
+#                             (scripts/perturb_build.py -> abv/perturbed): both must FAIL
 #   ipc                       two-process HIP IPC with / without HSA_ENABLE_IPC_MODE_LEGACY=0
-#   abaudit[:<bench args>]    interleaved bench.py A/B of the work-audit counter (GRAVSIM_AUDIT)
-#   abfork[:<bench args>]     reduce-phase span per step: row reduce forked / node split A/B
 #   span[:<bench args>]       reduce-phase span per step of the default schedule
 # Outputs land in gpurun_out/<task>*.log.
 set -o pipefail
@@ -90,23 +90,22 @@ for task in "$@"; do
         step 600 $out/hash_$tag.jsonl python -u scripts/state_hash.py --cases $cases
       fi
       cat $out/hash_$tag.jsonl ;;
+    perturb)
+      : > $out/perturb.txt
+      for t in smoke scale; do
+        if [ $t = smoke ]; then cmd=(python -c "import __graft_entry__ as g; g.smoke()")
+        else cmd=(python -u -m pytest tests/test_gpu_scale.py -x -q -k accel_sampled --timeout 300); fi
+        timeout -k 10 400 env GRAVSIM_NATIVE_DIR=abv/perturbed "${cmd[@]}" > $out/perturb_$t.log 2>&1
+        rc=$?
+        echo "perturbed build, $t: rc=$rc (a gate that bites exits non-zero)" | tee -a $out/perturb.txt
+        grep -E "AssertionError|assert|error" $out/perturb_$t.log | tail -3 | tee -a $out/perturb.txt
+        if [ $rc -eq 124 ] || [ $rc -eq 137 ]; then exit $rc; fi
+        if [ $rc -eq 0 ]; then echo "!! the $t gate passed a broken kernel"; exit 1; fi
+      done ;;
     accerr)
       step 300 $out/accel_err.txt python -u scripts/accel_err.py --n 4096
       step 300 $out/accel_err_64k.txt python -u scripts/accel_err.py --n 65536
       cat $out/accel_err.txt $out/accel_err_64k.txt ;;
-    abfork)
-      # reduce-phase span per step with the row reduce forked beside the node reduce (1) or
-      # after it (0), from kernel traces of the 1M bench (scripts/reduce_span.py)
-      # arms: fork,split (GRAVSIM_SYM_FORK_ROW, GRAVSIM_SYM_NODE_SPLIT)
-      for arm in 1,1 0,1 0,0 1,0 1,1 0,1 0,0 1,0; do
-        f=${arm%,*}; sp=${arm#*,}; d=$out/abfork_${f}_${sp}
-        rm -rf $d
-        step 600 $d.log env GRAVSIM_SYM_FORK_ROW=$f GRAVSIM_SYM_NODE_SPLIT=$sp rocprofv3 \
-          --kernel-trace -d $d -o tr --output-format csv -- python bench.py --steps 6 \
-          --warmup 2 --exact-steps 0 --phase-steps 0 --check-samples 0 --no-replay-audit $a
-        t=$(find $d -name "*kernel_trace.csv" | head -1)
-        echo "fork=$f split=$sp $(python scripts/reduce_span.py $t)" | tee -a $out/abfork.txt
-      done ;;
     span)
       # reduce-phase span per step of the default schedule (two runs), same recipe as abfork
       for i in 1 2; do
@@ -121,15 +120,6 @@ for task in "$@"; do
       # two-process HIP IPC (memory + event) with the launcher's dmabuf setting and without it
       step 300 $out/ipc_dmabuf.log env HSA_ENABLE_IPC_MODE_LEGACY=0 python tests/ipc_peer.py pair
       step 300 $out/ipc_legacy.log env -u HSA_ENABLE_IPC_MODE_LEGACY python tests/ipc_peer.py pair ;;
-    abaudit)
-      # interleaved A/B of the work-audit counter's cost at the headline size (same box)
-      for i in 1 2 3; do
-        for arm in 1 0; do
-          step 600 $out/abaudit_${arm}_$i.log env GRAVSIM_AUDIT=$arm python bench.py --steps 10 \
-            --warmup 2 --exact-steps 0 --phase-steps 0 --check-samples 0 --no-replay-audit $a
-          grep -o '"ms_per_step": [0-9.]*' $out/abaudit_${arm}_$i.log | sed "s/^/audit=$arm /" | tee -a $out/abaudit.txt
-        done
-      done ;;
     *) echo "unknown task $task"; exit 2 ;;
   esac
 done

@@ -30,10 +30,9 @@ def hip():
 # Knobs that change what the native stepper computes (per-rank timing emulation, probes).
 # Tests set them only through monkeypatch; one left in the process environment (e.g. by a
 # module imported at collection) would silently alter every later test.
-_PROCESS_KNOBS = ("GRAVSIM_EMULATE_RANK", "GRAVSIM_UNIT_TRACE", "GRAVSIM_EMU_COMM_GBPS",
-                  "GRAVSIM_SYM_DYN_CAP", "GRAVSIM_SYM_FIRST_WAVE", "GRAVSIM_SYM_BAND_MB",
-                  "GRAVSIM_FAULT_SKIP_UNITS", "GRAVSIM_SYM_REARM",
-                  "GRAVSIM_SYM_FORK_ROW", "GRAVSIM_SYM_NODE_SPLIT")
+_PROCESS_KNOBS = ("GRAVSIM_EMULATE_RANK", "GRAVSIM_UNIT_TRACE", "GRAVSIM_EMU_COMM",
+                  "GRAVSIM_SYM_BAND_MB", "GRAVSIM_FAULT_SKIP_UNITS", "GRAVSIM_SYM_OVERLAP",
+                  "GRAVSIM_FORCE_COMM", "GRAVSIM_TEST_STALL")
 
 
 @pytest.fixture(autouse=True)

@@ -145,39 +145,35 @@ def test_cutoff_paths_below_the_cutoff_pinned(hip, dtype):
 
 
 @pytest.mark.parametrize("n,band_mb,steps", [(65536, "1", 20), (1 << 20, "1540", 2)])
-def test_lastwg_rearm_targeted(hip, monkeypatch, n, band_mb, steps):
-    """Round 2's first re-arm of the dynamic unit counter (the last workgroup out zeroes it
-    in-kernel; opt-in GRAVSIM_SYM_REARM=lastwg), targeted at the failure it was retired for
-    (docs/DESIGN.md §8): many dynamic launches back to back on one stream, band after band
-    (65,536 bodies: one row per band, 32 launches per step, a 16-workgroup first wave so every
-    band launch fetches dynamically; 1M: the original 4-band test), replayed from a hipGraph.
-    Every unit must run exactly once per step (device count) and the bits must equal the
-    stream-ordered memset's. Run once per suite, not in a loop."""
+def test_dynamic_counter_rearm_many_launches(hip, monkeypatch, n, band_mb, steps):
+    """Many dynamic launches back to back on one stream, band after band, replayed from a
+    hipGraph (65,536 bodies: one row per band, 32 launches per step, a 16-workgroup first wave
+    so every band launch fetches dynamically; 1M: 4 bands): the stream-ordered memset re-arms
+    the unit counter before each launch, so every unit runs exactly once per step (device
+    count) and the bits equal one static unit per workgroup. (Round 2's in-kernel
+    last-workgroup re-arm failed exactly this pattern and was retired, docs/DESIGN.md §8.)"""
     from gravsim.runtime.engines import HipEngine
 
-    monkeypatch.setenv("GRAVSIM_SYM_FIRST_WAVE", "16")
     monkeypatch.setenv("GRAVSIM_SYM_BAND_MB", band_mb)
     out = {}
-    for rearm in ("lastwg", "memset"):
-        if rearm == "lastwg":
-            monkeypatch.setenv("GRAVSIM_SYM_REARM", "lastwg")
-        else:
-            monkeypatch.delenv("GRAVSIM_SYM_REARM", raising=False)
+    for cap in (2, 0):
         e = HipEngine(SimConfig(n=n, dtype="fp32", device="gpu", mode="sym"))
         try:
+            e.set_schedule(1, cap)
+            e.set_tuning(first_wave=16)
             e.init_ics("solar+random", 13)
             e.audit_reset()
             e.step(steps)
             e.sync()
             done, per = e.audit()
-            assert done == per * steps, (rearm, done, per)
+            assert done == per * steps, (cap, done, per)
             assert e.graph_info()["mode"] == "graph"
             b = e.state()
-            out[rearm] = (b.pos, b.vel)
+            out[cap] = (b.pos, b.vel)
         finally:
             e.close()
-    assert np.array_equal(out["lastwg"][0], out["memset"][0])
-    assert np.array_equal(out["lastwg"][1], out["memset"][1])
+    assert np.array_equal(out[2][0], out[0][0])
+    assert np.array_equal(out[2][1], out[0][1])
 
 
 def test_device_memory_ledger(hip):

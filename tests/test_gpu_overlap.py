@@ -1,7 +1,7 @@
 """Comm/compute split and overlap of the multi-rank sym step, measured on one GPU.
 
 Per-rank emulation (GRAVSIM_EMULATE_RANK) runs rank r's exact launch shapes of a P-rank run;
-with GRAVSIM_EMU_COMM_GBPS the all-gather and the node-sum exchange become modeled
+with GRAVSIM_EMU_COMM ("GB/s,latency us") the all-gather and the node-sum exchange become modeled
 collectives (comm_model.hip) of their exact byte counts on the comm stream, so the phase
 events see what an xGMI collective would cost. The reference times its whole loop, the
 MPI_Allgatherv included (mpi.c:189,227-247). Overlap modes (gravsim.h, set_overlap):
@@ -20,8 +20,7 @@ def _emu(monkeypatch, n, P, rank, gbps, overlap, strategy="allgather", graph=Tru
     from gravsim.runtime.engines import HipEngine
 
     monkeypatch.setenv("GRAVSIM_EMULATE_RANK", "1")
-    monkeypatch.setenv("GRAVSIM_EMU_COMM_GBPS", str(gbps))
-    monkeypatch.setenv("GRAVSIM_EMU_COMM_US", "15")
+    monkeypatch.setenv("GRAVSIM_EMU_COMM", f"{gbps},15")
     e = HipEngine(SimConfig(n=n, dtype="fp32", device="gpu", mode="sym", strategy=strategy,
                             graph=graph), rank, P)
     e.set_overlap(overlap)

@@ -211,11 +211,11 @@ def test_sym_bands_bitwise(hip, monkeypatch, P, dtype):
 def test_sym_fused_tail_bitwise(hip, monkeypatch, n, dtype):
     """One rank, one band: group reduce + row reduce + finalize fused into sym_tail_kernel
     keeps every sum's order, so steps and step-path accelerations are bitwise those of the
-    three-kernel tail (GRAVSIM_SYM_FUSED_TAIL=0)."""
+    three-kernel tail (set_tuning(fused_tail=0))."""
     out = []
-    for fused in ("0", "1"):
-        monkeypatch.setenv("GRAVSIM_SYM_FUSED_TAIL", fused)
+    for fused in (0, 1):
         e = _engine(n, dtype)
+        e.set_tuning(fused_tail=fused)
         e.init_ics("solar+random", 13)
         a = e.accel(step_path=True)
         e.step(3)
@@ -227,24 +227,24 @@ def test_sym_fused_tail_bitwise(hip, monkeypatch, n, dtype):
 
 
 @pytest.mark.parametrize("n,dtype,P,first_wave", [
-    (262144, "fp32", 1, None),   # default first wave (resident slots), 16,640 units
-    (40000, "fp32", 1, "16"),
-    (40000, "fp32", 2, "16"),    # two virtual ranks
-    (40000, "fp64", 1, "16"),
+    (262144, "fp32", 1, 0),   # default first wave (resident slots), 16,640 units
+    (40000, "fp32", 1, 16),
+    (40000, "fp32", 2, 16),    # two virtual ranks
+    (40000, "fp64", 1, 16),
 ])
-def test_sym_dynamic_unit_fetch_bitwise(hip, monkeypatch, n, dtype, P, first_wave):
-    """Workgroups that fetch their units from a device counter (GRAVSIM_SYM_DYN_CAP > 1, the
-    default) run the same units into the same slots as one unit per workgroup (0): same
-    bits, and the counters re-arm themselves launch after launch (graph replay included)."""
+def test_sym_dynamic_unit_fetch_bitwise(hip, n, dtype, P, first_wave):
+    """Workgroups that fetch their units from a device counter (dyn_cap > 1, the default)
+    run the same units into the same slots as one unit per workgroup (0): same bits, and the
+    counters re-arm themselves launch after launch (graph replay included)."""
     from gravsim.runtime.engines import VirtualGroup
 
-    if first_wave:
-        monkeypatch.setenv("GRAVSIM_SYM_FIRST_WAVE", first_wave)
     cfg = SimConfig(n=n, dtype=dtype, device="gpu", mode="sym")
     out = []
-    for cap in ("0", "4"):
-        monkeypatch.setenv("GRAVSIM_SYM_DYN_CAP", cap)
+    for cap in (0, 4):
         g = VirtualGroup(cfg, P)
+        for sh in g.shards:
+            sh.set_schedule(1, cap)
+            sh.set_tuning(first_wave=first_wave)
         g.init_ics("solar+random", 23)
         g.step(5)
         out.append(g.state())
@@ -260,10 +260,10 @@ def test_sym_graph_replays_rezero_unit_counter(hip, monkeypatch, fused):
     re-zeroed, whether the graph ends in the fused tail (which re-arms it) or not."""
     from gravsim.runtime.engines import HipEngine
 
-    monkeypatch.setenv("GRAVSIM_SYM_FUSED_TAIL", fused)
     out = []
     for graph in (True, False):
         e = HipEngine(SimConfig(n=32768, dtype="fp32", device="gpu", mode="sym", graph=graph))
+        e.set_tuning(fused_tail=int(fused))
         e.init_ics("solar+random", 3)
         e.step(6)
         e.sync()

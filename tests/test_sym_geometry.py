@@ -22,11 +22,17 @@ def _geo(n_pad):
     return lib, dict(zip(("NC", "H", "L", "S", "D"), (x.value for x in v)))
 
 
+def _round1_shell_len(A, NC):
+    """Round 1's rule (rows A < NC/2 take every antipodal pair), for the balance check."""
+    return NC // 2 if A < NC // 2 else NC // 2 - 1
+
+
 @pytest.mark.parametrize("NC", [8, 32, 64, 512, 2048])
-@pytest.mark.parametrize("parity", [0, 1])
-def test_every_chunk_pair_exactly_once(NC, parity):
+@pytest.mark.parametrize("rule", ["parity", "round1"])
+def test_every_chunk_pair_exactly_once(NC, rule):
     lib = _native.cpu_lib()
-    h = np.array([lib.gs_sym_shell_len(A, NC, parity) for A in range(NC)])
+    f = lib.gs_sym_shell_len if rule == "parity" else _round1_shell_len
+    h = np.array([f(A, NC) for A in range(NC)])
     assert set(h.tolist()) <= {NC // 2, NC // 2 - 1}
     A = np.repeat(np.arange(NC), NC // 2)
     d = np.tile(np.arange(1, NC // 2 + 1), NC)
@@ -43,10 +49,10 @@ def test_parity_balances_ranks(P):
     lib = _native.cpu_lib()
     NC = 512
     rows = NC // P
-    work = [sum(lib.gs_sym_shell_len(A, NC, 1) for A in range(r * rows, (r + 1) * rows))
+    work = [sum(lib.gs_sym_shell_len(A, NC) for A in range(r * rows, (r + 1) * rows))
             for r in range(P)]
     assert max(work) - min(work) == 0
-    old = [sum(lib.gs_sym_shell_len(A, NC, 0) for A in range(r * rows, (r + 1) * rows))
+    old = [sum(_round1_shell_len(A, NC) for A in range(r * rows, (r + 1) * rows))
            for r in range(P)]
     assert max(old) - min(old) == rows  # round 1: the first half of the ranks held long rows
 
@@ -60,7 +66,7 @@ def test_unit_map_permutation_and_locality(n_pad, P, fill):
     for rank in (0, P - 1):
         a0, rows = partition.sym_rank_rows(n_pad, P, rank)
         out = (ctypes.c_int32 * (rows * (S + D)))()
-        n = lib.gs_sym_unit_map(n_pad, rank, P, 1, fill, out, len(out))
+        n = lib.gs_sym_unit_map(n_pad, rank, P, fill, out, len(out))
         assert n == rows * (S + D)
         m = np.frombuffer(out, dtype=np.uint32)
         remote = (m >> 31).astype(bool)
@@ -70,7 +76,7 @@ def test_unit_map_permutation_and_locality(n_pad, P, fill):
         assert np.array_equal(np.sort(key), np.arange(rows * (S + D)))  # a permutation
         A = a0 + row.astype(np.int64)
         u = unit.astype(np.int64)
-        h = np.array([lib.gs_sym_shell_len(int(x), NC, 1) for x in range(NC)])[A]
+        h = np.array([lib.gs_sym_shell_len(int(x), NC) for x in range(NC)])[A]
         diag = u >= S
         assert not remote[diag].any()  # diagonal parts read only the own rows
         past = ~diag & (u * L >= 16 * h)  # past the row's shell: reads nothing
@@ -96,7 +102,7 @@ def test_ring_unit_map_stages(n_pad, P, fill):
     for rank in (0, P - 1):
         a0, rows = partition.sym_rank_rows(n_pad, P, rank)
         out = (ctypes.c_int32 * (rows * (S + D)))()
-        n = lib.gs_sym_unit_map_ring(n_pad, rank, P, 1, fill, out, len(out))
+        n = lib.gs_sym_unit_map_ring(n_pad, rank, P, fill, out, len(out))
         assert n == rows * (S + D)
         m = np.frombuffer(out, dtype=np.uint32)
         remote = (m >> 31).astype(bool)
@@ -107,7 +113,7 @@ def test_ring_unit_map_stages(n_pad, P, fill):
         assert np.array_equal(np.sort(key), np.arange(rows * (S + D)))
         assert np.array_equal(remote, stage > 0)
         A = a0 + row
-        h = np.array([lib.gs_sym_shell_len(int(x), NC, 1) for x in range(NC)])[A]
+        h = np.array([lib.gs_sym_shell_len(int(x), NC) for x in range(NC)])[A]
         want = np.zeros(len(m), dtype=np.int64)
         owner_of_row = np.searchsorted(starts, np.arange(NC), side="right") - 1
         seg = np.nonzero((unit < S) & (unit * L < 16 * h))[0]
@@ -124,7 +130,7 @@ def test_ring_unit_map_stages(n_pad, P, fill):
             assert not remote[:min(fill if fill > 0 else n, int((~remote).sum()))].any()
     # too many rows for the 12-bit row field: no gated ring map (the launch stays ungated)
     big = 1 << 25
-    assert lib.gs_sym_unit_map_ring(big, 0, 1, 1, -1, None, 0) == 0
+    assert lib.gs_sym_unit_map_ring(big, 0, 1, -1, None, 0) == 0
 
 
 @pytest.mark.parametrize("n_pad", [16384, 49152, 65536, 1 << 20, 1 << 24])
@@ -212,9 +218,9 @@ def test_split_segment_map(n_pad, P):
     for rank in (0, P - 1):
         a0, rows = partition.sym_rank_rows(n_pad, P, rank)
         plain = (ctypes.c_int32 * (rows * (S + D)))()
-        assert lib.gs_sym_unit_map(n_pad, rank, P, 1, 1024, plain, len(plain)) == rows * (S + D)
+        assert lib.gs_sym_unit_map(n_pad, rank, P, 1024, plain, len(plain)) == rows * (S + D)
         out = (ctypes.c_int32 * (rows * (S + D + kr)))()
-        n = lib.gs_sym_unit_map_kr(n_pad, rank, P, 1, 1024, kr, out, len(out))
+        n = lib.gs_sym_unit_map_kr(n_pad, rank, P, 1024, kr, out, len(out))
         assert n == rows * (S + D + kr)
         m = np.frombuffer(out, dtype=np.uint32)
         half = ((m >> 30) & 1).astype(bool)
