@@ -84,7 +84,7 @@ def parse(argv=None) -> argparse.Namespace:
                     help="capture multi-rank steps, RCCL collectives included, in a hipGraph")
     ap.add_argument("--no-graph-comm", dest="graph_comm", action="store_false",
                     help=argparse.SUPPRESS)
-    ap.add_argument("--overlap", default="auto", choices=["auto", "0", "1", "2", "3"],
+    ap.add_argument("--overlap", default="auto", choices=["auto", "0", "3"],
                     help="sym work beside the all-gather. auto (multi-rank sym): the gated "
                          "local-first launch (3) if a 2-step self-check from the same ICs "
                          "gives the same bits as the ungated schedule (0), else 0")

@@ -40,7 +40,7 @@ def main() -> int:
                     help="comma list of modeled per-rank collective rates in GB/s (0: free)")
     ap.add_argument("--comm-us", type=float, default=15.0, help="modeled latency per collective")
     ap.add_argument("--comm-wgs", type=int, default=16, help="workgroups of a modeled collective")
-    ap.add_argument("--overlap", default="0", help="comma list of sym overlap modes 0..3")
+    ap.add_argument("--overlap", default="3", help="comma list of sym overlap modes (0, 3)")
     ap.add_argument("--graph", default="segmented",
                     help="comma list of multi-rank step modes: eager | segmented (the default: "
                          "compute segments as graphs, collectives eager between them) | full "

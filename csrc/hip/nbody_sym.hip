@@ -284,13 +284,7 @@ __device__ __forceinline__ void force_sym_body(const SymArgs& a, int b) {
     gated = local_first_unit(a, b, &br, &s, &stage, &part) && a.gate != nullptr;
   } else if (a.units == 7) {  // deferred unit a.defer_index of the units-6 launch
     local_first_unit(a, (int)a.defer[1 + a.defer_index], &br, &s, &stage, &part);
-  } else if (a.units == 1) {
-    br = b / a.D;
-    s = a.S + b % a.D;
-  } else if (a.units == 2 || a.units == 4) {  // shell units: all (2) or the non-local ones (4)
-    br = b / a.S;
-    s = b % a.S;
-  } else if (a.units == 0) {
+  } else {  // units 0
     // Every unit: the shell segments row by row, then all diagonal parts. A diagonal part is
     // one-sided (about half the issue time of a shell segment), so dispatching them last fills
     // the launch's final, partial wave of workgroups with short jobs. With split segments
@@ -309,18 +303,14 @@ __device__ __forceinline__ void force_sym_body(const SymArgs& a, int b) {
       br = (k >> 1) / a.Kr;
       s = ns + (k >> 1) % a.Kr;
     }
-  } else {  // the diagonal ones + the rank-local shell ones (5), row by row
-    br = b / (a.S + a.D);
-    s = b % (a.S + a.D);
   }
   const int A = a.a0 + a.band0 + br;
   const bool diag = s >= a.S;
   const bool split = !diag && s >= a.S - a.Kr;  // a split segment (two half sums)
   const unsigned long long weight = split && part < 0 ? 2ull : 1ull;
   // Empty units (all-ghost row, segment past the row's shell) count as done for the work
-  // audit, in exactly one of the launches that list them (units 4 and 5 both list shell
-  // segments: the units-5 launch counts the empty ones).
-  const bool count_empty = a.audit && a.units != 4;
+  // audit (every unit is listed by exactly one launch).
+  const bool count_empty = a.audit != nullptr;
   if ((int64_t)A * kSymC >= a.n_real) {  // all-ghost row: never read
     if (count_empty) audit_unit(a, weight);
     return;
@@ -342,12 +332,6 @@ __device__ __forceinline__ void force_sym_body(const SymArgs& a, int b) {
     seq.u1 = min(u0 + seg_tiles, h_tiles);
     u_lo = u0;
     u_mid = min(u0 + seg_tiles / 2, seq.u1);
-    if (a.units == 4 || a.units == 5) {
-      // Rank-local: every j-chunk of the segment is one of the rank's own rows, so it needs
-      // no gathered positions (chunks A+1 .. < a0 + rows: no wrap below NC).
-      const bool local = A + 1 + (seq.u1 - 1) / G::kTilesPerChunk < a.a0 + a.rows;
-      if (local != (a.units == 5)) return;
-    }
     seq.u = seq.valid(u0);
   }
   if (gated && !gate_open_or_defer(a, b, stage)) return;  // counted when units 7 runs it
@@ -604,8 +588,8 @@ __global__ __launch_bounds__(256) void sym_block_reduce_kernel(SymArgs a) {
 template <typename T>
 __global__ __launch_bounds__(256) void sym_node_reduce_kernel(SymArgs a) {
   const int64_t nb = (int64_t)a.real_chunks * kSymC;
-  const int64_t x = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (x >= nb) return;
+  const int64_t x = a.x_lo + (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (x >= (a.x_hi > 0 && a.x_hi < nb ? a.x_hi : nb)) return;
   const int X = (int)(x / kSymC), c = (int)(x % kSymC);
   const int own_lo = a.blk_lo[a.rank], own_hi = a.blk_lo[a.rank + 1];
   int lo = own_lo, l = sym_dyadic_level(lo, own_hi);
@@ -641,19 +625,23 @@ __global__ __launch_bounds__(256) void sym_node_reduce_kernel(SymArgs a) {
   o[2 * nlq] = r[2];
 }
 
-// S(x) for an own body: every rank's nodes in global order from Rbuf[node][3][n_local],
-// merged into the full tree.
+// S(x) for an own body: every rank's nodes in global order, merged into the full tree; the
+// other ranks' from Rbuf[node][3][n_local] (received), this rank's own nodes straight from
+// its Sbuf block (they never leave the GPU: no copy on the comm stream's critical path).
 template <typename T>
 __device__ __forceinline__ void sym_tree_all(const SymArgs& a, int64_t li, T* S) {
   TreeAcc<T, 3> t;
   t.pos = 0;
   const T* R = static_cast<const T*>(a.Rbuf) + li;
+  const T* own = static_cast<const T*>(a.Sbuf) + (int64_t)a.nn * 3 * a.i_begin + li;
   int j = 0;
   for (int q = 0; q < a.P; ++q) {
     const int hi = a.blk_lo[q + 1];
+    const int j0 = j;
     for (int lo = a.blk_lo[q]; lo < hi; ++j) {
       const int l = sym_dyadic_level(lo, hi);
-      const T* p = R + (int64_t)j * 3 * a.n_local;
+      const T* p = q == a.rank ? own + (int64_t)(j - j0) * 3 * a.n_local
+                               : R + (int64_t)j * 3 * a.n_local;
       T v[3] = {p[0], p[a.n_local], p[2 * a.n_local]};
       t.push(l, v);
       lo += 1 << l;
@@ -847,8 +835,7 @@ __global__ __launch_bounds__(192) void sym_tail_kernel(SymArgs a) {
 
 template <typename T>
 hipError_t launch_force_sym_t(const SymArgs& a, hipStream_t s) {
-  int units = a.band_rows * (a.units == 1 ? a.D : (a.units == 2 || a.units == 4) ? a.S
-                                                                                 : a.S + a.D);
+  int units = a.band_rows * (a.S + a.D);
   // units 0 (diagonal parts last) and the all-gather units 6 order list every split segment
   // as two half units at their end
   if (a.Kr > 0 && (a.units == 0 || (a.units == 6 && a.gate_n <= 1)))
@@ -919,7 +906,9 @@ hipError_t launch_sym_block_reduce(const SymArgs& a, hipStream_t s) {
 hipError_t launch_sym_node_reduce(const SymArgs& a, hipStream_t s) {
   // leaves from Pj need every own row in the slots (one band), else from Bbuf
   if (!a.Bbuf && (a.band0 != 0 || a.band_rows != a.rows)) return hipErrorInvalidValue;
-  const int64_t bodies = (int64_t)a.real_chunks * kSymC;
+  const int64_t nb = (int64_t)a.real_chunks * kSymC;
+  const int64_t bodies = (a.x_hi > 0 && a.x_hi < nb ? a.x_hi : nb) - a.x_lo;
+  if (bodies <= 0) return hipSuccess;
   const dim3 grid((unsigned)((bodies + 255) / 256), (unsigned)a.nn);
   if (a.fp64) hipLaunchKernelGGL(sym_node_reduce_kernel<double>, grid, dim3(256), 0, s, a);
   else hipLaunchKernelGGL(sym_node_reduce_kernel<float>, grid, dim3(256), 0, s, a);

@@ -349,18 +349,13 @@ int ring_finish(gs_stepper* s, const gs::KArgs<T>& a) {
 //     waiting workgroup: per-rank emulation of 1M / 8 with the collectives modeled at
 //     64 GB/s + 15 us, 22.42-22.59 ms against 22.74-22.87 ms for 0 (docs/DESIGN.md §7,
 //     profiles/r2_overlap_fill_ab.jsonl);
-//   0: wait for the gather, then one launch of every unit;
-//   1: the diagonal-chunk units (own rows only) run beside the gather, then the shell units
-//     after it;
-//   2: the diagonal units and the shell segments whose j-chunks are all own rows (1M, P = 8:
-//     2080 of 16448 units) run on s_comp beside the gather and the other shell units on
-//     s_rem after it, concurrently.
-// Modes 1 and 2 pay a launch boundary (a unit is ~0.6 ms of work at 1M) to hide a ~0.1 ms
-// gather and lost to 0 in round 1's emulation with free collectives (0: 21.0-21.2 ms,
-// 1: 21.4-21.6, 2: 22.4-22.6; profiles/r1_sym_overlap_ab.txt); they are kept for A/B runs.
-// With `exchange` the RCCL node-sum exchange starts right
-// after the node reduce and runs beside the last row reduce; the compute stream joins
-// it afterwards.
+//   0: wait for the gather, then one launch of every unit.
+// (Two launches split at the gather, diagonal units or all rank-local units first, paid a
+// launch boundary - a unit is ~0.6 ms of work at 1M - to hide a ~0.1 ms gather and lost to 0:
+// 21.4-21.6 and 22.4-22.6 against 21.0-21.2 ms, profiles/r1_sym_overlap_ab.txt; deleted.)
+// With `exchange` the node reduce is pipelined with the RCCL node-sum exchange (two stages,
+// sym_reduce_exchange), which runs beside the rest of the node reduce and the row reduce;
+// the compute stream joins it before finalize.
 // One rank (no exchange, no virtual shards), one band, up to 256K bodies: the tree over the
 // row blocks, the row reduce and finalize run as one sym_tail_kernel (same bits). Interleaved A/B
 // (profiles/r2_fused_tail_ab.jsonl): 65K 0.707 vs 0.708 ms, 256K 10.51 vs 10.57 ms, but 1M
@@ -391,7 +386,6 @@ int sym_force(gs_stepper* s, gs::SymArgs a, bool overlap_gather, bool exchange =
     a.band_rows = s->sym_band < a.rows - b0 ? s->sym_band : a.rows - b0;
     a.units = 0;
     const bool one_band = a.band_rows == a.rows;
-    const int ov = s->sym_overlap;
     if (overlap_gather && b0 == 0 && one_band && a.gate) {
       // 3: one launch with the local units first; remote units run in it once the gather is
       // published, or are deferred to a second launch queued behind the gather event.
@@ -401,25 +395,6 @@ int sym_force(gs_stepper* s, gs::SymArgs a, bool overlap_gather, bool exchange =
       a.units = 7;
       GS_HIP(force_sym_launch(s, a, s->s_comp));
       a.units = 0;
-    } else if (overlap_gather && b0 == 0 && one_band && ov == 1) {
-      gs::SymArgs d = a;
-      d.units = 1;  // diagonal chunks beside the gather
-      GS_HIP(force_sym_launch(s, d, s->s_comp));
-      if (comp_wait(s, s->ev_gathered, kMarkGather)) return -1;
-      a.units = 2;
-      GS_HIP(force_sym_launch(s, a, s->s_comp));
-    } else if (overlap_gather && b0 == 0 && one_band && ov == 2) {
-      // fork: s_rem starts after everything already on s_comp (X[cur] written) and the gather
-      GS_HIP(hipEventRecord(s->ev_fork, s->s_comp));
-      GS_HIP(hipStreamWaitEvent(s->s_rem, s->ev_fork, 0));
-      GS_HIP(hipStreamWaitEvent(s->s_rem, s->ev_gathered, 0));
-      gs::SymArgs r = a;
-      r.units = 4;  // shell segments that read gathered rows
-      GS_HIP(force_sym_launch(s, r, s->s_rem));
-      GS_HIP(hipEventRecord(s->ev_remote, s->s_rem));
-      a.units = 5;  // diagonal + rank-local shell units, beside the gather
-      GS_HIP(force_sym_launch(s, a, s->s_comp));
-      GS_HIP(hipStreamWaitEvent(s->s_comp, s->ev_remote, 0));  // join
     } else {
       if (overlap_gather && b0 == 0) {
         if (comp_wait(s, s->ev_gathered, kMarkGather)) return -1;
@@ -433,8 +408,13 @@ int sym_force(gs_stepper* s, gs::SymArgs a, bool overlap_gather, bool exchange =
     // (reduce phase at 1M 1533-1592 us per step against 1342-1381 in sequence;
     // profiles/r3_reduce_fork_split_ab.txt).
     if (a.Bbuf) GS_HIP(gs::launch_sym_block_reduce(a, s->s_comp));  // the band's leaves
-    if (last) GS_HIP(gs::launch_sym_node_reduce(a, s->s_comp));
-    if (exchange && last && sym_exchange_rccl(s, false)) return -1;
+    if (last) {
+      if (exchange) {
+        if (sym_reduce_exchange(s, a)) return -1;  // node reduce pipelined with the sends
+      } else {
+        GS_HIP(gs::launch_sym_node_reduce(a, s->s_comp));
+      }
+    }
     GS_HIP(gs::launch_sym_row_reduce(a, s->s_comp));
     if (exchange && last) {
       if (comp_wait(s, s->ev_sym, kMarkExchange)) return -1;
@@ -668,8 +648,7 @@ int accel_impl(gs_stepper* s, double* acc4, bool step_path) {
       }
       gs::SymArgs sa = sym_args(s, cur);
       sa.acc_out = s->acc;
-      if (sym_force(s, sa, false)) return -1;
-      if (xcomm(s) && sym_exchange_rccl(s)) return -1;
+      if (sym_force(s, sa, false, xcomm(s))) return -1;
       if (fused_tail(s)) {
         GS_HIP(gs::launch_sym_tail(sa, s->s_comp));
         s->work_zero = true;
@@ -792,6 +771,7 @@ int gs_stepper_create(const gs_config* cfg, gs_stepper** out) {
   for (auto& e : s->ev_recv) FAIL_CLEAN(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   FAIL_CLEAN(hipEventCreateWithFlags(&s->ev_remote, hipEventDisableTiming));
   FAIL_CLEAN(hipEventCreateWithFlags(&s->ev_sym, hipEventDisableTiming));
+  for (hipEvent_t& e : s->ev_stage) FAIL_CLEAN(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   FAIL_CLEAN(hipEventCreateWithFlags(&s->ev_fork, hipEventDisableTiming));
   FAIL_CLEAN(hipEventCreateWithFlags(&s->ev_ready, hipEventDisableTiming));
   FAIL_CLEAN(hipEventCreateWithFlags(&s->ev_gathered, hipEventDisableTiming));
@@ -887,7 +867,8 @@ int gs_stepper_destroy(gs_stepper* s) {
   for (const auto& m : s->mem) (void)hipFree(m.p);
   s->mem.clear();
   for (hipEvent_t e : {s->ev_ready, s->ev_gathered, s->ev_t0, s->ev_local, s->ev_end,
-                       s->ev_remote, s->ev_fork, s->ev_rem2, s->ev_sym})
+                       s->ev_remote, s->ev_fork, s->ev_rem2, s->ev_sym, s->ev_stage[0],
+                       s->ev_stage[1]})
     if (e) (void)hipEventDestroy(e);
   if (s->s_comp) (void)hipStreamDestroy(s->s_comp);
   if (s->s_comm) (void)hipStreamDestroy(s->s_comm);
@@ -1015,7 +996,7 @@ int gs_stepper_set_timing(gs_stepper* s, int32_t on) {
 }
 
 int gs_stepper_set_overlap(gs_stepper* s, int32_t mode) {
-  if (mode < 0 || mode > 3) { gs_set_error("set_overlap: mode must be 0..3"); return -1; }
+  if (mode != 0 && mode != 3) { gs_set_error("set_overlap: mode must be 0 or 3"); return -1; }
   s->sym_overlap = mode;
   drop_graphs(s);
   return 0;

@@ -136,9 +136,9 @@ int build_graph(gs_stepper* s) {
 }
 
 // Multi-rank steps whose cross-stream points all go through comp_record / comp_wait /
-// comm_do: the sym schedule except overlap 2 (a second compute stream forked per step).
+// comm_do: the sym schedule.
 bool plan_ok(const gs_stepper* s) {
-  return xcomm(s) && use_sym(s) && s->sym_overlap != 2 && s->cfg.use_graph == 1;
+  return xcomm(s) && use_sym(s) && s->cfg.use_graph == 1;
 }
 
 // Record one ping-pong period (two steps, from an even step whose buffer needs its gather)

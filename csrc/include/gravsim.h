@@ -179,10 +179,9 @@ int gs_stepper_set_timing(gs_stepper* s, int32_t on);
 // ms, [3] exchange ms, [4] exposed gather ms, [5] exposed exchange ms (compute-stream stalls),
 // [6] the most force units a step deferred past the gather (overlap 3), [7] reserved.
 int gs_stepper_phase_stats(gs_stepper* s, double* out8);
-// Sym schedule work beside the all-gather: 0 wait then one launch, 1 diagonal units first,
-// 2 local units + remote units on a second stream, 3 one local-first launch whose remote
-// units run once the gather is published or are deferred to a second launch behind it
-// (the default for nranks > 1; GRAVSIM_SYM_OVERLAP sets another initial value).
+// Sym schedule work beside the all-gather: 0 wait then one launch, 3 one local-first launch
+// whose remote units run once the gather is published or are deferred to a second launch
+// behind it (the default for nranks > 1; GRAVSIM_SYM_OVERLAP sets another initial value).
 int gs_stepper_set_overlap(gs_stepper* s, int32_t mode);
 int32_t gs_stepper_get_overlap(gs_stepper* s);
 // Units a dynamic-fetch workgroup may take after the first wave (<= 1: static units).

@@ -70,6 +70,9 @@ struct SymArgs {
   void* Ti;            // [3][n_local] per-body i-side total: sum_q Pd[q] + sum_s Pi[s]
   void* Sbuf;          // [dest rank q][own node k < nn][3][n_local(q)] node sums by destination
   const void* Rbuf;    // [node j, all ranks' nodes in global order][3][n_local] received
+                       // (the own nodes' slots are not used: finalize reads them from Sbuf)
+  int64_t x_lo, x_hi;  // node reduce: bodies [x_lo, x_hi) only (x_hi 0: every real body), so
+                       // one destination's sums can be sent while the next one's are reduced
   void* Bbuf;          // multi-band only: [own block][3][real bodies] per-block leaf sums
   void* X_next;        // [n_pad * 4]
   void* vel;           // [n_local * 4]
@@ -86,12 +89,9 @@ struct SymArgs {
   int32_t exact;       // reference hard cutoff (select at cut2) instead of the fast core
   int32_t units;       // which units a force launch covers: 0 all (shell segments row by row,
                        // then the diagonal parts, then the split segments as half units:
-                       // short units fill the launch's last wave), 1 diagonal chunks only
-                       // (need only the own rows), 2 shell segments only, 4 the shell
-                       // segments with a j-chunk outside the own rows, 5 every other unit
-                       // (diagonal + rank-local shell: no gathered positions needed),
-                       // 6 all, local units first, remote units gated on `gate`,
-                       // 7 the units the units-6 launch deferred (after the gather)
+                       // short units fill the launch's last wave), 6 all, rank-local units
+                       // first, remote units gated on `gate`, 7 the units the units-6 launch
+                       // deferred (after the gather)
   double dt, eps2, cut2;
   // Gather gate (units 6/7): set on the comm stream right after the all-gather; a remote unit
   // that finds it still closed appends itself to defer[1..] (count defer[0]) and exits, and

@@ -78,9 +78,9 @@ struct gs_stepper {
   std::atomic<int> comm_stage{0};
   bool virt = false;  // member of a virtual-rank group (gather = device copies, gs_group_step)
   bool emulate = false;  // GRAVSIM_EMULATE_RANK: run one rank's launch shapes, no exchange
-  // sym work beside a pending gather (GRAVSIM_SYM_OVERLAP): 0 none (wait, then one launch),
-  // 1 the diagonal units first on the compute stream, 2 diagonal + rank-local shell units
-  // concurrently with the rest on a second stream.
+  // sym work beside a pending gather (GRAVSIM_SYM_OVERLAP, gs_stepper_set_overlap): 0 none
+  // (wait, then one launch), 3 one launch with the rank-local units first and the remote ones
+  // gated on the gather in-kernel (the multi-rank default).
   int sym_overlap = 0;
   hipGraphExec_t graph = nullptr;
   bool timed = false;  // eager steps record phase events
@@ -110,6 +110,7 @@ struct gs_stepper {
   std::vector<int32_t> nn, nbase;
   bool uniform = true;  // every rank owns the same body count (P | B: ncclAllGather)
   hipEvent_t ev_sym = nullptr;
+  hipEvent_t ev_stage[2] = {nullptr, nullptr};  // node sums of an exchange stage reduced
   // Per-rank emulation with modeled collectives (GRAVSIM_EMU_COMM GB/s > 0): every all-gather
   // and node-sum exchange becomes a comm_model_kernel of the same byte count on s_comm.
   double emu_gbps = 0.0, emu_lat_us = 15.0;
@@ -260,7 +261,7 @@ int gather(gs_stepper* s, int cur, bool gate = false);
 int ring_src(const gs_stepper* s, int sub);
 void rank_chunks(const gs_stepper* s, int src, int* c0, int* c1);
 int ring_xfer_rccl(gs_stepper* s, int cur, int sub);
-int sym_exchange_rccl(gs_stepper* s, bool join = true);
+int sym_reduce_exchange(gs_stepper* s, const gs::SymArgs& a);
 void maybe_install_crash_trace();
 // ncclCommAbort once (the watchdog thread, a timeout or an async error may all ask for it).
 bool abort_comm(gs_stepper* s);

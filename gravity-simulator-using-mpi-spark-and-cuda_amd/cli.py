@@ -55,7 +55,7 @@ def build_parser() -> argparse.ArgumentParser:
                    help="multi-rank hang detection: abort the RCCL communicator when no step "
                         "completes for this many seconds (default: max(60, 20 x the measured "
                         "step time), at most 240; 0 = wait forever)")
-    p.add_argument("--overlap", type=int, choices=[-1, 0, 1, 2, 3], default=d.overlap,
+    p.add_argument("--overlap", type=int, choices=[-1, 0, 3], default=d.overlap,
                    help="multi-rank sym schedule: work beside the all-gather (3: one launch, "
                         "rank-local units first, remote units once the gather is published, "
                         "the built-in default for P > 1; 0: wait for the gather, one launch; "

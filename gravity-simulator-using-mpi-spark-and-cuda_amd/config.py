@@ -47,10 +47,9 @@ class SimConfig:
                                   # can catch; docs/DESIGN.md "hipGraph and RCCL").
     comm: str = "auto"            # rccl (GPU) | gloo (CPU) | none
     strategy: str = "allgather"   # multi-rank exchange: allgather | ring (pipelined send/recv)
-    overlap: int = -1             # sym work beside the all-gather: 0 none, 1 diagonal units
-                                  # first, 2 two streams, 3 gated local-first launch; -1 native
-                                  # default (3 for P > 1, as bench.py runs; GRAVSIM_SYM_OVERLAP
-                                  # overrides)
+    overlap: int = -1             # sym work beside the all-gather: 0 none, 3 gated local-first
+                                  # launch; -1 native default (3 for P > 1 after a bitwise
+                                  # self-check, as bench.py runs; GRAVSIM_SYM_OVERLAP overrides)
     threads: int = 0              # CPU engine OpenMP threads (0 = default)
     step_timeout_s: Optional[float] = None  # multi-rank hang detection: abort RCCL when no
                                   # step completes for this long; None = derived from the
@@ -108,8 +107,8 @@ class SimConfig:
             raise ValueError("cutoff_mode must be auto, exact or fast")
         if self.strategy not in ("allgather", "ring"):
             raise ValueError("strategy must be allgather or ring")
-        if self.overlap not in (-1, 0, 1, 2, 3):
-            raise ValueError("overlap must be -1 (default) or 0..3")
+        if self.overlap not in (-1, 0, 3):
+            raise ValueError("overlap must be -1 (default), 0 or 3")
         if self.diag_every < 0:
             raise ValueError("diag_every must be >= 0")
         if self.step_timeout_s is not None and self.step_timeout_s < 0:

@@ -141,9 +141,10 @@ class RunGuard:
         with self._lock:
             self._closed = True
             self._deadline = None
-        for p in (self._path(self.rank),):
+        for p in (self._path(self.rank), self.rec.get("rccl_log_path")):
             try:
-                os.remove(p)
+                if p:
+                    os.remove(p)  # (RCCL may still hold its log open: unlinking is fine)
             except OSError:
                 pass
         if self.rank == 0:

@@ -198,8 +198,8 @@ class HipEngine:
         return out
 
     def set_overlap(self, mode: int) -> None:
-        """Sym-schedule work beside the all-gather (0..3, see gravsim.h; 3 is the native
-        default for P > 1)."""
+        """Sym-schedule work beside the all-gather (0 wait, 3 gated local-first launch, the
+        native default for P > 1; see gravsim.h)."""
         _native.check(self.lib, self.lib.gs_stepper_set_overlap(self._s, int(mode)), "overlap")
 
     @property
