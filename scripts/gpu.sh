@@ -17,6 +17,8 @@
 #   counters                  rocprofv3 -L (the PMC counters this box offers)
 #   hash[:<native dir>]       state hashes after 3 steps (scripts/state_hash.py, HASH_CASES)
 #   accerr                    per-body error of the sym step path at 4K and 64K (accel_err.py)
+#   abtree[:<dir>,<rounds>,<bench args>] alternating bench.py runs of another source tree
+#                             (e.g. abv/r3tree: round 3's code) and this one, same box
 #   perturb                   smoke() and the 1M accuracy test on a deliberately broken build
 #                             (scripts/perturb_build.py -> abv/perturbed): both must FAIL
 #   ipc                       two-process HIP IPC with / without HSA_ENABLE_IPC_MODE_LEGACY=0
@@ -84,12 +86,22 @@ for task in "$@"; do
     hash)
       cases=${HASH_CASES:-65536:fp32:auto:1,1048576:fp32:auto:1,65536:fp32:exact:1,524288:fp64:auto:1,65536:fp64:exact:1,262144:fp32:auto:3,262144:fp32:auto:8,1048576:fp32:auto:8}
       tag=$(basename "${a:-in-tree}")
-      if [ -n "$a" ]; then
-        step 600 $out/hash_$tag.jsonl env GRAVSIM_NATIVE_DIR="$a" python -u scripts/state_hash.py --cases $cases
+      if [ -n "$a" ]; then  # <a> = another source tree with its own build (e.g. abv/r3tree)
+        step 600 $out/hash_$tag.jsonl python -u $a/scripts/state_hash.py --cases $cases
       else
         step 600 $out/hash_$tag.jsonl python -u scripts/state_hash.py --cases $cases
       fi
       cat $out/hash_$tag.jsonl ;;
+    abtree)
+      IFS=, read -r tree rounds bargs <<< "$a"
+      for i in $(seq 1 ${rounds:-2}); do
+        for arm in "$tree" .; do
+          lab=$([ "$arm" = . ] && echo head || basename "$arm")
+          step 600 $out/abtree_${i}_$lab.log python $arm/bench.py --exact-steps 0 \
+            --phase-steps 0 --no-replay-audit --no-energy $bargs
+          echo "arm=$lab round=$i $(grep -o '"ms_per_step": [0-9.]*' $out/abtree_${i}_$lab.log)" | tee -a $out/abtree.txt
+        done
+      done ;;
     perturb)
       : > $out/perturb.txt
       for t in smoke scale; do
