@@ -256,11 +256,13 @@ __device__ __forceinline__ bool gate_open_or_defer(const SymArgs& a, int b, int 
   return open_s != 0;
 }
 
-// Work audit (SymArgs::audit): one relaxed device-scope add per unit that completed (or
-// was empty), from one lane, after the unit's partial stores. The host compares the count
-// with rows x (S + D) per step (bench.py work_audit), so a launch that silently skipped
-// units (a stale dynamic-fetch counter, a lost deferred unit) cannot pass as a fast step.
-// A split segment run whole counts its two halves (n = 2), so the count per step is
+// Work audit (SymArgs::audit): a unit that completed (or was empty) reports its weight; a
+// workgroup adds the sum of its units with one relaxed device-scope atomic from one lane when
+// it exits (one per unit in round 3: the batched add also gave the dynamic launch's hot loop
+// back round 3's register assignment, 1.1 % at 1M, profiles/r4_ab_vs_r3.txt). The host
+// compares the count with rows x (S + D + Kr) per step (bench.py work_audit), so a launch that
+// silently skipped units (a stale dynamic-fetch counter, a lost deferred unit) cannot pass as
+// a fast step. A split segment run whole weighs 2 (its two halves), so the count per step is
 // rows x (S + D + Kr) whichever way the segments run.
 __device__ __forceinline__ void audit_unit(const SymArgs& a, unsigned long long n = 1) {
   if (threadIdx.x == 0)
@@ -270,7 +272,7 @@ __device__ __forceinline__ void audit_unit(const SymArgs& a, unsigned long long 
 // One unit b (row a, segment s) per call; s == S is the row's diagonal chunk. b is the
 // workgroup index, or the index the workgroup fetched (SymArgs.work).
 template <typename T, bool EXACT>
-__device__ __forceinline__ void force_sym_body(const SymArgs& a, int b) {
+__device__ __forceinline__ unsigned force_sym_body(const SymArgs& a, int b) {
   using G = Geo<T>;
   using V4 = sym::Vec4<T>;
   __shared__ Smem<T> sm;
@@ -311,10 +313,8 @@ __device__ __forceinline__ void force_sym_body(const SymArgs& a, int b) {
   // Empty units (all-ghost row, segment past the row's shell) count as done for the work
   // audit (every unit is listed by exactly one launch).
   const bool count_empty = a.audit != nullptr;
-  if ((int64_t)A * kSymC >= a.n_real) {  // all-ghost row: never read
-    if (count_empty) audit_unit(a, weight);
-    return;
-  }
+  if ((int64_t)A * kSymC >= a.n_real)  // all-ghost row: never read
+    return count_empty ? (unsigned)weight : 0u;
   const int seg_tiles = a.L * G::kTilesPerQuantum;
   TileSeq<T> seq{A, a.NC, a.real_chunks, 0, 0, diag};
   int u_lo = 0, u_mid = 0;  // shell: the segment's first tile and (split) its half point
@@ -325,16 +325,14 @@ __device__ __forceinline__ void force_sym_body(const SymArgs& a, int b) {
   } else {
     const int h_tiles = shell_len(A, a.NC) * G::kTilesPerChunk;
     const int u0 = s * seg_tiles;
-    if (u0 >= h_tiles) {  // past this row's shell: never read
-      if (count_empty) audit_unit(a, weight);
-      return;
-    }
+    if (u0 >= h_tiles)  // past this row's shell: never read
+      return count_empty ? (unsigned)weight : 0u;
     seq.u1 = min(u0 + seg_tiles, h_tiles);
     u_lo = u0;
     u_mid = min(u0 + seg_tiles / 2, seq.u1);
     seq.u = seq.valid(u0);
   }
-  if (gated && !gate_open_or_defer(a, b, stage)) return;  // counted when units 7 runs it
+  if (gated && !gate_open_or_defer(a, b, stage)) return 0u;  // counted when units 7 runs it
   const unsigned long long t_start = a.utrace ? __builtin_amdgcn_s_memrealtime() : 0ull;
   const V4* X4 = static_cast<const V4*>(a.X);
   ISetK<T> is;
@@ -393,7 +391,6 @@ __device__ __forceinline__ void force_sym_body(const SymArgs& a, int b) {
 
     }
   }
-  if (a.audit) audit_unit(a, weight);
   if (a.utrace && threadIdx.x == 0) {
     // hwreg(HW_ID) whole register, hwreg(XCC_ID) bits 3:0 (ids 4 and 20 on gfx9.4+)
     const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);
@@ -405,6 +402,7 @@ __device__ __forceinline__ void force_sym_body(const SymArgs& a, int b) {
     e[2] = (unsigned long long)hw | ((unsigned long long)xcc << 32);
     e[3] = ((unsigned long long)(unsigned)br << 32) | (unsigned)s;
   }
+  return a.audit ? (unsigned)weight : 0u;
 }
 
 // units 7 runs a separate instantiation (DEFER): a small grid that walks the deferred list
@@ -414,7 +412,8 @@ __device__ __forceinline__ void force_sym_body(const SymArgs& a, int b) {
 template <typename T, bool EXACT, bool DEFER, bool DYN>
 __device__ __forceinline__ void force_sym_entry(SymArgs a) {
   if constexpr (!DEFER && !DYN) {
-    force_sym_body<T, EXACT>(a, blockIdx.x);
+    const unsigned w = force_sym_body<T, EXACT>(a, blockIdx.x);
+    if (w) audit_unit(a, w);
   } else if constexpr (DYN) {
     // Dynamic fetch: unit indices in launch order from a device counter. The hardware hands
     // workgroups to the 8 XCDs in a fixed rotation, so a static unit per workgroup gives every
@@ -424,24 +423,28 @@ __device__ __forceinline__ void force_sym_entry(SymArgs a) {
     // collective), and faster XCDs simply take more. Same units, same slots: same bits.
     __shared__ unsigned next_s;
     const int cap = (int)blockIdx.x < a.first_wave ? 1 : a.unit_cap;
+    unsigned done = 0;  // audit weight of the units this workgroup ran: one add at exit
     for (int k = 0; k < cap; ++k) {
       if (threadIdx.x == 0)
         next_s = __hip_atomic_fetch_add(a.work, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __syncthreads();
       const unsigned u = next_s;
       if (u >= (unsigned)a.n_units) break;
-      force_sym_body<T, EXACT>(a, (int)u);
+      done += force_sym_body<T, EXACT>(a, (int)u);
       __syncthreads();  // next_s and the LDS tiles are rewritten by the next unit
     }
+    if (done) audit_unit(a, done);
   } else {
     const unsigned n = a.defer[0];
     if (blockIdx.x == 0 && threadIdx.x == 0 && n > 0)
       __hip_atomic_fetch_max(a.defer_max, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned done = 0;
     for (unsigned k = blockIdx.x; k < n; k += gridDim.x) {
       a.defer_index = (int32_t)k;
-      force_sym_body<T, EXACT>(a, 0);
+      done += force_sym_body<T, EXACT>(a, 0);
       __syncthreads();  // the next unit reuses the LDS tiles
     }
+    if (done) audit_unit(a, done);
   }
 }
 
