@@ -84,6 +84,11 @@ HIP_FLAGS = ["-O3", "-std=c++17", f"--offload-arch={ARCH}", "-ffp-contract=off",
 # thresholds still hold with it (profiles/r2_s4_sizes_maxilp.txt).
 if os.environ.get("GRAVSIM_SCHED", "max-ilp") != "default":
     HIP_FLAGS += ["-mllvm", f"-amdgpu-sched-strategy={os.environ.get('GRAVSIM_SCHED', 'max-ilp')}"]
+# Loops aligned to 64-byte instruction-fetch lines: the sym force kernel's loops span 20-38 KB;
+# with their heads left where the code happens to fall, the 1M step ran 1.0 % slower after an
+# unrelated code change (164.0-164.2 vs 162.4-162.5 ms alternating on one box; aligned: 162.4-
+# 162.5, profiles/r4_ab_align_loops.jsonl). Aligning pins the layout instead of leaving it to luck.
+HIP_FLAGS += ["-falign-loops=64"]
 if os.environ.get("GRAVSIM_SLP", "1") == "0":
     HIP_FLAGS.append("-fno-slp-vectorize")
 HIP_FLAGS += os.environ.get("GRAVSIM_HIP_EXTRA", "").split()
