@@ -386,8 +386,11 @@ def run(a, g) -> int:
     def measure(overlap: int) -> dict:
         """Warmup + the K timed steps from the ICs already loaded, then the audits of that
         work and the end-of-run physics (all untimed)."""
-        g.stage("warmup", budget(a.warmup))
+        g.stage("warmup", budget(a.warmup + 2))
         eng.step(a.warmup)
+        # (untimed) up to 2 more steps so the timed ones start on a replayable period: graph
+        # replay on one rank, the segmented plan on many
+        extra = eng.align_period() if a.graph else 0
         eng.sync()
         eng.audit_reset()
         torch.cuda.synchronize()
@@ -450,11 +453,10 @@ def run(a, g) -> int:
         phase = None
         if a.phase_steps > 0:
             g.stage("phase", budget(a.phase_steps + 2))
-            if ginfo["mode"] == "segmented":
-                # whole plan periods: from an even step whose buffer still needs its gather
-                # (the state reads above gathered the current one), so the phase events come
-                # from the same segmented plan the timed loop replayed
-                eng.step(2 if eng.steps_done % 2 == 0 else 1)
+            if world > 1 and a.graph:
+                # whole plan periods (the state reads above gathered the current buffer), so
+                # the phase events come from the segmented plan the timed loop replayed
+                eng.align_period()
             eng.set_timing(True)
             eng.step(a.phase_steps)
             phase = eng.phase_stats()
@@ -466,12 +468,12 @@ def run(a, g) -> int:
         # timed run's bits (eager launches, one static unit per workgroup, no gating).
         replay = None
         if a.replay_audit:
-            g.stage("replay", budget(a.warmup + a.steps))
+            g.stage("replay", budget(a.warmup + extra + a.steps))
             cap = eng.dyn_cap
             eng.set_schedule(0, 0)
             eng.set_overlap(0)
             eng.init_ics("solar+random", cfg.seed)
-            eng.step(a.warmup + a.steps)
+            eng.step(a.warmup + extra + a.steps)
             eng.sync()
             pos_r, vel_r, _ = own_state(eng)
             same = np.array_equal(pos_r, pos_t) and np.array_equal(vel_r, vel_t)
@@ -481,7 +483,8 @@ def run(a, g) -> int:
                 failures.append(f"replay: the independent schedule differs on {int(diff)} rank(s)")
             eng.set_schedule((2 if a.graph_comm else 1) if a.graph else 0, cap)
             eng.set_overlap(overlap)
-        return dict(wall=wall, ginfo=ginfo, mem=mem, hbm_max=hbm_max, failures=failures,
+        return dict(extra=extra, wall=wall, ginfo=ginfo, mem=mem, hbm_max=hbm_max,
+                    failures=failures,
                     units=units, bad=bad, drift=drift, err_end=err_end, bound_end=bound_end,
                     conservation=conservation, phase=phase, replay=replay)
 
@@ -581,6 +584,9 @@ def run(a, g) -> int:
                 "overlap_check": overlap_check,
                 "overlap_fallback": fallback,
                 "step_timeout_s": step_to,
+                # untimed steps added after the warmup so the timed ones start on a replayable
+                # two-step period (graph / segmented plan)
+                "warmup_align_steps": res["extra"],
                 "first_step_ms": 1e3 * first_s,
                 # N^2 ordered pair terms per step (what a one-sided sum evaluates) ...
                 "effective_interactions_per_s": float(cfg.n) * cfg.n * a.steps / wall,

@@ -1181,6 +1181,10 @@ int64_t gs_stepper_count_nonfinite(gs_stepper* s) {
 
 int64_t gs_stepper_steps_done(gs_stepper* s) { return s->k; }
 
+int32_t gs_stepper_period_start(gs_stepper* s) {
+  return (s->k & 1) == 0 && (xcomm(s) ? !s->full[0] : true) ? 1 : 0;
+}
+
 int gs_stepper_phase_ms(gs_stepper* s, float* local_ms, float* comm_ms, float* total_ms) {
   if (!s->timed) { gs_set_error("phase timing disabled (set GRAVSIM_PHASE_TIMING=1)"); return -1; }
   GS_HIP(hipEventSynchronize(s->ev_end));

@@ -170,6 +170,9 @@ int gs_stepper_accel_step_path(gs_stepper* s, double* acc4);
 // Non-finite guard: returns number of non-finite position/velocity components on this rank.
 int64_t gs_stepper_count_nonfinite(gs_stepper* s);
 int64_t gs_stepper_steps_done(gs_stepper* s);
+// 1 if the next step starts a replayable two-step period (an even step whose buffer still
+// needs its gather, multi-rank): steps from here run from the graph / segmented plan.
+int32_t gs_stepper_period_start(gs_stepper* s);
 // Per-step phase timing of the last step (ms): up to the local/force phase, the step's
 // collectives (all-gather + node-sum exchange spans on the comm stream), and the whole step.
 int gs_stepper_phase_ms(gs_stepper* s, float* local_ms, float* comm_ms, float* total_ms);

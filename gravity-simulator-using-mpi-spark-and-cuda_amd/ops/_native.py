@@ -157,6 +157,7 @@ def hip_lib():
         _sig(lib, "gs_stepper_accel_step_path", c_int32, [S, _PD])
         _sig(lib, "gs_stepper_count_nonfinite", c_int64, [S])
         _sig(lib, "gs_stepper_steps_done", c_int64, [S])
+        _sig(lib, "gs_stepper_period_start", c_int32, [S])
         _sig(lib, "gs_stepper_phase_ms", c_int32, [S, _PF, _PF, _PF])
         _sig(lib, "gs_stepper_set_timing", c_int32, [S, c_int32])
         _sig(lib, "gs_stepper_phase_stats", c_int32, [S, _PD])

@@ -290,6 +290,17 @@ class HipEngine:
     def steps_done(self) -> int:
         return int(self.lib.gs_stepper_steps_done(self._s))
 
+    def align_period(self) -> int:
+        """Step (0, 1 or 2 steps) until the next step starts a replayable two-step period, so
+        that the following steps run from the step graph / segmented plan, not eagerly (a
+        state read gathers the current buffer; an odd step count ends mid-period). Returns
+        the steps taken."""
+        n = 0
+        while not self.lib.gs_stepper_period_start(self._s) and n < 2:
+            self.step(1)
+            n += 1
+        return n
+
     def force_mode(self) -> dict:
         """Resolved force path: exact hard-cutoff select, or the fast core-softened path."""
         ex, e2 = ctypes.c_int32(), ctypes.c_double()
