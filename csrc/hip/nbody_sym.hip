@@ -591,8 +591,11 @@ __global__ __launch_bounds__(256) void sym_block_reduce_kernel(SymArgs a) {
 template <typename T>
 __global__ __launch_bounds__(256) void sym_node_reduce_kernel(SymArgs a) {
   const int64_t nb = (int64_t)a.real_chunks * kSymC;
-  const int64_t x = a.x_lo + (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (x >= (a.x_hi > 0 && a.x_hi < nb ? a.x_hi : nb)) return;
+  const int64_t tx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (a.x_count > 0 && tx >= a.x_count) return;
+  int64_t x = a.x_lo + tx;
+  if (x >= (int64_t)a.NC * kSymC) x -= (int64_t)a.NC * kSymC;  // (a cyclic range of ranks)
+  if (x >= nb) return;
   const int X = (int)(x / kSymC), c = (int)(x % kSymC);
   const int own_lo = a.blk_lo[a.rank], own_hi = a.blk_lo[a.rank + 1];
   int lo = own_lo, l = sym_dyadic_level(lo, own_hi);
@@ -910,7 +913,7 @@ hipError_t launch_sym_node_reduce(const SymArgs& a, hipStream_t s) {
   // leaves from Pj need every own row in the slots (one band), else from Bbuf
   if (!a.Bbuf && (a.band0 != 0 || a.band_rows != a.rows)) return hipErrorInvalidValue;
   const int64_t nb = (int64_t)a.real_chunks * kSymC;
-  const int64_t bodies = (a.x_hi > 0 && a.x_hi < nb ? a.x_hi : nb) - a.x_lo;
+  const int64_t bodies = a.x_count > 0 ? a.x_count : nb;
   if (bodies <= 0) return hipSuccess;
   const dim3 grid((unsigned)((bodies + 255) / 256), (unsigned)a.nn);
   if (a.fp64) hipLaunchKernelGGL(sym_node_reduce_kernel<double>, grid, dim3(256), 0, s, a);

@@ -132,11 +132,16 @@ int ring_xfer_rccl(gs_stepper* s, int cur, int sub) {
   return 0;
 }
 
-// Node reduce for destination rank q's bodies (its sums land in Sbuf block q).
-static int node_reduce_dest(gs_stepper* s, const gs::SymArgs& a0, int q) {
+// Node reduce for the bodies of destination ranks r + kb .. r + ke - 1 (mod P): consecutive
+// ranks own consecutive rows, so that is one cyclic body range and one launch (their sums
+// land in the Sbuf blocks of those ranks).
+static int node_reduce_dests(gs_stepper* s, const gs::SymArgs& a0, int kb, int ke) {
+  const int P = s->cfg.nranks, r = s->cfg.rank;
   gs::SymArgs a = a0;
-  a.x_lo = s->rbeg[q];
-  a.x_hi = s->rbeg[q] + s->rcnt[q];
+  a.x_lo = s->rbeg[(r + kb) % P];
+  a.x_count = 0;
+  for (int k = kb; k < ke; ++k) a.x_count += s->rcnt[(r + k) % P];
+  if (a.x_count == 0) return 0;
   GS_HIP(gs::launch_sym_node_reduce(a, s->s_comp));
   return 0;
 }
@@ -153,11 +158,14 @@ static int node_reduce_dest(gs_stepper* s, const gs::SymArgs& a0, int q) {
 // The compute stream joins the exchange later (comp_wait on ev_sym before finalize).
 int sym_reduce_exchange(gs_stepper* s, const gs::SymArgs& a0) {
   const int P = s->cfg.nranks, r = s->cfg.rank;
+  // stage g: shifts [k_lo[g], k_lo[g + 1]). Stage 1 is the smaller one (a third of the
+  // shifts): its reduce is short, so the messages start early, and the larger stage 2 reduce
+  // plus the own sums and the row reduce hide behind its transfer.
   const int stages = P - 1 < 2 ? P - 1 : 2;
-  const int k_lo[3] = {1, stages == 2 ? 1 + P / 2 : P, P};  // stage g: shifts [k_lo[g], k_lo[g+1])
+  const int k1 = (P - 1) / 3 > 1 ? (P - 1) / 3 : 1;
+  const int k_lo[3] = {1, stages == 2 ? 1 + k1 : P, P};
   for (int g = 0; g < stages; ++g) {
-    for (int k = k_lo[g]; k < k_lo[g + 1]; ++k)
-      if (node_reduce_dest(s, a0, (r + k) % P)) return -1;
+    if (node_reduce_dests(s, a0, k_lo[g], k_lo[g + 1])) return -1;
     if (comp_record(s, s->ev_stage[g])) return -1;
     const int kb = k_lo[g], ke = k_lo[g + 1];
     const bool first = g == 0, last = g + 1 == stages;
@@ -191,7 +199,7 @@ int sym_reduce_exchange(gs_stepper* s, const gs::SymArgs& a0) {
         }))
       return -1;
   }
-  if (node_reduce_dest(s, a0, r)) return -1;  // the own sums, last
+  if (node_reduce_dests(s, a0, 0, 1)) return -1;  // the own sums, last
   // (a live 1-rank communicator: nothing to exchange; the join below is then immediate)
   if (stages == 0 && comp_record(s, s->ev_sym)) return -1;
   return 0;

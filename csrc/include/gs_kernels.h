@@ -71,8 +71,9 @@ struct SymArgs {
   void* Sbuf;          // [dest rank q][own node k < nn][3][n_local(q)] node sums by destination
   const void* Rbuf;    // [node j, all ranks' nodes in global order][3][n_local] received
                        // (the own nodes' slots are not used: finalize reads them from Sbuf)
-  int64_t x_lo, x_hi;  // node reduce: bodies [x_lo, x_hi) only (x_hi 0: every real body), so
-                       // one destination's sums can be sent while the next one's are reduced
+  int64_t x_lo, x_count;  // node reduce: bodies x_lo .. x_lo + x_count - 1 (cyclic mod n_pad;
+                          // x_count 0: every real body), so the sums of some destination
+                          // ranks can be sent while the next ones' are reduced
   void* Bbuf;          // multi-band only: [own block][3][real bodies] per-block leaf sums
   void* X_next;        // [n_pad * 4]
   void* vel;           // [n_local * 4]
