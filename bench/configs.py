@@ -44,9 +44,10 @@ def gpu_run(n, dtype, steps, warmup, P=1, rank=0, overlap=None, **kw):
     ms = 1e3 * (time.perf_counter() - t0) / steps
     lay = e.native_layout
     phase = None
-    if P > 1:  # comm split of one more (eager, event-timed) step
+    if P > 1:  # comm split of two more event-timed steps, replayed from the segmented plan
+        e.align_period()
         e.set_timing(True)
-        e.step(1)
+        e.step(2)
         phase = e.phase_stats()
         e.set_timing(False)
     e.close()
