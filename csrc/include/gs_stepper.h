@@ -153,8 +153,9 @@ struct gs_stepper {
   double step_timeout_s = 0.0;  // 0: unbounded
   bool graph_failed = false;    // multi-rank capture refused: eager fallback
   bool work_zero = true;        // sym dynamic unit counter (gate_buf[4]) known to be 0
-  // Work audit of the sym force launches: +1 per unit run (nbody_sym.hip audit_unit); a step
-  // runs rows x (S + D) units on this rank whatever the launch split or fetch order.
+  // Work audit of the sym force launches (nbody_sym.hip: one batched add per workgroup of the
+  // units it ran); a step runs rows x (S + D + Kr) units on this rank (each split segment
+  // counts as its two halves) whatever the launch split or fetch order.
   unsigned long long* audit = nullptr;
   // Fault injection for the audit's own test (GRAVSIM_FAULT_SKIP_UNITS=k): every dynamic
   // force launch starts its unit counter at k instead of 0, so units 0 .. k-1 never run,

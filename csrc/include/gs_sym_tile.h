@@ -36,7 +36,10 @@
 // packing instead of j-pair packing (r1_sym_ab_jpack.jsonl); 2 or 8 i-bodies per stage group
 // (+0.7 %); no scheduling regions, or ALU allowed across the step barriers (+1.7 % / +1.0 %,
 // r3s2_sched_barrier_ab.jsonl, r3s2_barrier_mask_ab.jsonl); an fp64 barrier per i-body
-// (+0.5 %, r3s2_sched_barrier_fp64_ab.jsonl).
+// (+0.5 %, r3s2_sched_barrier_fp64_ab.jsonl); the j side accumulated in LDS by no-return
+// ds_add_f32 (6 per step, conflict-free, instead of the 6 v_sub_f32_dpp carrier moves: VALU
+// 150 -> 144 per step) is 6.3x slower, 1030 vs 162.4 ms at 1M: an LDS float atomic costs the
+// CU ~150 cycles per wave-instruction (r4s2_lds_atomic_carriers_ab.jsonl).
 #pragma once
 #include <hip/hip_runtime.h>
 
