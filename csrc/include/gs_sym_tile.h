@@ -39,7 +39,14 @@
 // (+0.5 %, r3s2_sched_barrier_fp64_ab.jsonl); the j side accumulated in LDS by no-return
 // ds_add_f32 (6 per step, conflict-free, instead of the 6 v_sub_f32_dpp carrier moves: VALU
 // 150 -> 144 per step) is 6.3x slower, 1030 vs 162.4 ms at 1M: an LDS float atomic costs the
-// CU ~150 cycles per wave-instruction (r4s2_lds_atomic_carriers_ab.jsonl).
+// CU ~150 cycles per wave-instruction (r4s2_lds_atomic_carriers_ab.jsonl); a software-
+// pipelined rsq (group g's rsq read two regions later, after group g+1's separations; 2
+// i-bodies per group to stay in 256 VGPRs) is 1.3 % slower, 165.1 vs 163.1 ms, same bits
+// (r4s2_rsq_pipeline_u2_ab.jsonl): the rsq latency is not what the tile waits on; i-body
+// splats by op_sel from the (x, y) / (z, mu) pairs as loaded (inline asm: 231 -> 189 VGPRs,
+// the compiler otherwise duplicates each coordinate into a register pair) +0.6 % at 2 waves
+// per SIMD and +1.2 % at 3 (168 VGPRs), same bits (r4s2_opsel_occupancy3_ab.jsonl): more
+// waves per SIMD do not raise this tile's issue rate.
 #pragma once
 #include <hip/hip_runtime.h>
 
