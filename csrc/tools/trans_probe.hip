@@ -9,6 +9,11 @@
 //   mode 3: (1 rsq + 8 pk_fma) x 8               (spaced)
 //   mode 4: (2 rsq + 16 pk_fma) x 4              (pairs spaced)
 //   mode 5: 120 v_fma_f32 (24 chains): the same lane-FMA count unpacked
+//   mode 6: (fma r; rsq r; 7 pk_fma) x 8      (rsq input produced by the op before it)
+//   mode 7: (rsq r; fma r; 7 pk_fma) x 8      (rsq output read by the op after it)
+//   mode 8: (fma r; 7 pk_fma) x 8             (control of 6 / 7 without the rsq)
+//   mode 9: (fma r; rsq r; fma r; 7 pk_fma) x 8 (both, as in the force tile)
+//   mode 10: (fma r; fma r; 7 pk_fma) x 8     (control of 9)
 // Output: one JSON line per (mode, waves/SIMD): ns per wave-iteration per SIMD.
 // Result (profiles/r2_trans_probe.jsonl, 2 waves/SIMD): 64 pk_fma 136 ns, + 8 rsq in any
 // placement 140-143 ns, 120 fma 191 ns. In the sym tile a second transcendental per pair
@@ -29,7 +34,17 @@ typedef float f2 __attribute__((ext_vector_type(2)));
   "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7), "+v"(a8), \
       "+v"(a9), "+v"(a10), "+v"(a11), "+v"(a12), "+v"(a13), "+v"(a14), "+v"(a15), "+v"(r0), \
       "+v"(r1), "+v"(r2), "+v"(r3), "+v"(r4), "+v"(r5), "+v"(r6), "+v"(r7)
-#define INS [m] "v"(m), [c] "v"(c)
+#define INS [m] "v"(m), [c] "v"(c), [ms] "v"(ms), [cs] "v"(cs)
+#define FR(k) "v_fma_f32 %" #k ", %" #k ", %[ms], %[cs]\n"
+#define PK7A PK(0) PK(1) PK(2) PK(3) PK(4) PK(5) PK(6)
+#define PK7B PK(8) PK(9) PK(10) PK(11) PK(12) PK(13) PK(14)
+#define DEP6(k, P7) FR(k) RSQ(k) P7
+#define DEP7(k, P7) RSQ(k) FR(k) P7
+#define DEP8(k, P7) FR(k) P7
+#define DEP9(k, P7) FR(k) RSQ(k) FR(k) P7
+#define DEP10(k, P7) FR(k) FR(k) P7
+#define X8(D) D(16, PK7A) D(17, PK7B) D(18, PK7A) D(19, PK7B) D(20, PK7A) D(21, PK7B) \
+  D(22, PK7A) D(23, PK7B)
 
 template <int MODE>
 __global__ __launch_bounds__(256) void probe(float* out, int iters, float s) {
@@ -39,8 +54,19 @@ __global__ __launch_bounds__(256) void probe(float* out, int iters, float s) {
   float r0 = s + 1, r1 = s + 2, r2 = s + 3, r3 = s + 4, r4 = s + 5, r5 = s + 6, r6 = s + 7,
         r7 = s + 8;
   const f2 m = f2(0.999f), c = f2(1e-3f);
+  const float ms = 0.999f, cs = 1e-3f;
   for (int it = 0; it < iters; ++it) {
-    if constexpr (MODE == 0) {
+    if constexpr (MODE == 6) {
+      asm volatile(X8(DEP6) : OPS : INS);
+    } else if constexpr (MODE == 7) {
+      asm volatile(X8(DEP7) : OPS : INS);
+    } else if constexpr (MODE == 8) {
+      asm volatile(X8(DEP8) : OPS : INS);
+    } else if constexpr (MODE == 9) {
+      asm volatile(X8(DEP9) : OPS : INS);
+    } else if constexpr (MODE == 10) {
+      asm volatile(X8(DEP10) : OPS : INS);
+    } else if constexpr (MODE == 0) {
       asm volatile(PK16 PK16 PK16 PK16 : OPS : INS);
     } else if constexpr (MODE == 1) {
       asm volatile(RSQ(16) RSQ(17) RSQ(18) RSQ(19) RSQ(20) RSQ(21) RSQ(22) RSQ(23) : OPS : INS);
@@ -139,6 +165,11 @@ int main(int argc, char** argv) {
     run<2>("8 rsq burst + 64 pk_fma", out, cus, iters);
     run<3>("(rsq + 8 pk_fma) x8", out, cus, iters);
     run<4>("(2 rsq + 16 pk_fma) x4", out, cus, iters);
+    run<6>("(fma; rsq; 7 pk) x8 [rsq input dependent]", out, cus, iters);
+    run<7>("(rsq; fma; 7 pk) x8 [rsq output dependent]", out, cus, iters);
+    run<8>("(fma; 7 pk) x8 [control]", out, cus, iters);
+    run<9>("(fma; rsq; fma; 7 pk) x8 [both dependent]", out, cus, iters);
+    run<10>("(fma; fma; 7 pk) x8 [control of 9]", out, cus, iters);
   }
   CHECK(hipFree(out));
   return 0;
