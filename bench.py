@@ -26,8 +26,8 @@ N * K / max_rank(wall).
 
 Audits of the timed work (outside the timed region; the run exits non-zero if one fails):
   * unit count: the sym force kernels count every unit they run on device; after the loop
-    each rank must have run exactly rows x (S + D + Kr) units per timed step (a split segment
-    counts as its two halves);
+    each rank must have run exactly rows x (S + D + (Np - 1) Kr) units per timed step (a split
+    segment counts as its Np parts);
   * replay: the same warmup + K steps are re-run from the same ICs on an independent
     schedule (eager launches, one static unit per workgroup, ungated) and must give the
     same bits on every rank.
@@ -419,9 +419,10 @@ def run(a, g) -> int:
             units = {"units_per_step_rank0": per_step,
                      "units_done_rank0": done, "ranks_short": int(short)}
             if short:
-                S, D, Kr = eng.sym_geometry()
+                S, D, Kr, Np = eng.sym_geometry()
                 failures.append(f"unit count: {int(short)} rank(s) did not run rows x (S + D + "
-                                f"Kr) units per timed step (S {S}, D {D}, Kr {Kr}; rank {rank}: "
+                                f"(Np - 1) Kr) units per timed step (S {S}, D {D}, Kr {Kr}, Np "
+                                f"{Np}; rank {rank}: "
                                 f"{done} of {per_step * a.steps})")
         else:
             units = None  # one-sided schedules: no unit counter, the replay audit still runs

@@ -175,6 +175,14 @@ extern "C" int32_t gs_sym_split_segments(int64_t n_pad) {
   return L >= 2 ? S / 16 : 0;
 }
 
+// Parts per split segment (SymArgs::Np): the final units of a launch are 1 / Np of a segment.
+// 4 when a segment spans at least 4 quanta (one fp32 tile each), else 2.
+extern "C" int32_t gs_sym_split_parts(int64_t n_pad) {
+  int32_t NC, H, L, S, D;
+  if (gs_sym_geometry(n_pad, &NC, &H, &L, &S, &D)) return 2;
+  return L >= 4 ? 4 : 2;
+}
+
 // Rows [a0, a0 + rows) of rank `rank` of `nranks` in the sym schedule: whole row blocks by
 // mpi.c's remainder rule (gs_common.h sym_blk_lo). Equal for every P dividing 8.
 extern "C" int gs_sym_rank_rows(int64_t n_pad, int32_t nranks, int32_t rank, int32_t* a0,
@@ -261,21 +269,27 @@ extern "C" int64_t gs_sym_unit_map(int64_t n_pad, int32_t rank, int32_t nranks, 
   return gs_sym_unit_map_kr(n_pad, rank, nranks, fill, 0, out, cap);
 }
 
-// The same order with the last kr shell segments of every row split (gs_kernels.h SymArgs::Kr):
-// they leave the order above and are appended as two half units each (bit 30 set, bit 29 the
-// half), row by row, so the launch ends with half-length units. Rows < 8192 (13-bit field);
-// rows * (S + D + kr) entries.
+// The same order with the last kr shell segments of every row split into np parts
+// (gs_kernels.h SymArgs::Kr, Np): they leave the order above and are appended as np part units
+// each (bit 30 set, bits 28-29 the part), row by row, so the launch ends with 1 / np-length
+// units. Rows < 4096 (12-bit field) with splits; rows * (S + D + (np - 1) kr) entries.
 extern "C" int64_t gs_sym_unit_map_kr(int64_t n_pad, int32_t rank, int32_t nranks,
                                       int64_t fill, int32_t kr, int32_t* out, int64_t cap) {
+  return gs_sym_unit_map_parts(n_pad, rank, nranks, fill, kr, 2, out, cap);
+}
+
+extern "C" int64_t gs_sym_unit_map_parts(int64_t n_pad, int32_t rank, int32_t nranks,
+                                         int64_t fill, int32_t kr, int32_t np, int32_t* out,
+                                         int64_t cap) {
   int32_t NC, H, L, S, D, a0, rows;
-  if (nranks < 1 || rank < 0 || rank >= nranks || kr < 0 ||
+  if (nranks < 1 || rank < 0 || rank >= nranks || kr < 0 || np < 2 || np > 4 ||
       gs_sym_geometry(n_pad, &NC, &H, &L, &S, &D) ||
       gs_sym_rank_rows(n_pad, nranks, rank, &a0, &rows))
     return -1;
   if (kr > S) return -1;
   const int32_t per = S + D;
-  const int64_t total = (int64_t)rows * (per + kr);
-  if (rows >= (kr > 0 ? 8192 : 32768) || per >= 65536) return 0;
+  const int64_t total = (int64_t)rows * (per + (int64_t)(np - 1) * kr);
+  if (rows >= (kr > 0 ? 4096 : 32768) || per >= 65536) return 0;
   if (!out || cap < total) return -1;
   std::vector<int32_t> nl(rows);
   std::vector<char> moved((size_t)rows * per, 0);
@@ -302,9 +316,9 @@ extern "C" int64_t gs_sym_unit_map_kr(int64_t n_pad, int32_t rank, int32_t nrank
       }
   for (int32_t r = 0; r < rows; ++r)
     for (int32_t u = S - kr; u < S; ++u)
-      for (uint32_t h = 0; h < 2; ++h) {
+      for (uint32_t h = 0; h < (uint32_t)np; ++h) {
         const bool remote = u >= nl[r];
-        out[k++] = (int32_t)((remote ? 0x80000000u : 0u) | 0x40000000u | (h << 29) |
+        out[k++] = (int32_t)((remote ? 0x80000000u : 0u) | 0x40000000u | (h << 28) |
                              ((uint32_t)r << 16) | (uint32_t)u);
       }
   return k;

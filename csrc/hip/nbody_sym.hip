@@ -217,16 +217,16 @@ __device__ __forceinline__ void run_tiles(const SymArgs& a, ISetK<T>& is, TileSe
 // a chain of dependent loads in front of every workgroup and cost 2 % of the step.
 // With the ring strategy (gate_n > 1) bits 28-30 hold the ring stage whose slice the unit
 // waits for and rows are < 4096 (layout.cpp gs_sym_unit_map_ring).
-// With split segments (Kr > 0, all-gather order) bit 30 marks a half unit, bit 29 its half,
-// and rows are < 8192 (layout.cpp gs_sym_unit_map_kr).
+// With split segments (Kr > 0, all-gather order) bit 30 marks a part unit, bits 28-29 its
+// part, and rows are < 4096 (layout.cpp gs_sym_unit_map_parts).
 __device__ __forceinline__ bool local_first_unit(const SymArgs& a, int b, int* br, int* s,
                                                  int* stage, int* part) {
   const uint32_t m = (uint32_t)a.lf[b];
   const bool ring = a.gate_n > 1, halves = a.Kr > 0 && !ring;
-  *br = (int)((m >> 16) & (ring ? 0xfffu : halves ? 0x1fffu : 0x7fffu));
+  *br = (int)((m >> 16) & (ring || halves ? 0xfffu : 0x7fffu));
   *s = (int)(m & 0xffffu);
   *stage = ring ? (int)((m >> 28) & 7u) : 0;
-  *part = halves && ((m >> 30) & 1u) ? (int)((m >> 29) & 1u) : -1;
+  *part = halves && ((m >> 30) & 1u) ? (int)((m >> 28) & 3u) : -1;
   return (m >> 31) != 0u;
 }
 
@@ -260,10 +260,10 @@ __device__ __forceinline__ bool gate_open_or_defer(const SymArgs& a, int b, int 
 // workgroup adds the sum of its units with one relaxed device-scope atomic from one lane when
 // it exits (one per unit in round 3: the batched add also gave the dynamic launch's hot loop
 // back round 3's register assignment, 1.1 % at 1M, profiles/r4_ab_vs_r3.txt). The host
-// compares the count with rows x (S + D + Kr) per step (bench.py work_audit), so a launch that
-// silently skipped units (a stale dynamic-fetch counter, a lost deferred unit) cannot pass as
-// a fast step. A split segment run whole weighs 2 (its two halves), so the count per step is
-// rows x (S + D + Kr) whichever way the segments run.
+// compares the count with rows x (S + D + (Np - 1) Kr) per step (bench.py work_audit), so a
+// launch that silently skipped units (a stale dynamic-fetch counter, a lost deferred unit)
+// cannot pass as a fast step. A split segment run whole weighs Np (its parts), so the count
+// per step is the same whichever way the segments run.
 __device__ __forceinline__ void audit_unit(const SymArgs& a, unsigned long long n = 1) {
   if (threadIdx.x == 0)
     __hip_atomic_fetch_add(a.audit, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -279,7 +279,7 @@ __device__ __forceinline__ unsigned force_sym_body(const SymArgs& a, int b) {
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   // Units per row: S shell segments, then D parts of the diagonal chunk.
   // br: row within the band (index into Pi/Pj/Pd); the rank's row is band0 + br.
-  // part: -1 a whole unit, 0 / 1 the first / second half of a split segment (Px).
+  // part: -1 a whole unit, 0 .. Np-1 one part of a split segment (part 0 -> Pi, others -> Px).
   int br, s, stage = 0, part = -1;
   bool gated = false;
   if (a.units == 6) {
@@ -290,7 +290,7 @@ __device__ __forceinline__ unsigned force_sym_body(const SymArgs& a, int b) {
     // Every unit: the shell segments row by row, then all diagonal parts. A diagonal part is
     // one-sided (about half the issue time of a shell segment), so dispatching them last fills
     // the launch's final, partial wave of workgroups with short jobs. With split segments
-    // (Kr) the unsplit segments come first and the split ones last, as two half units each.
+    // (Kr) the unsplit segments come first and the split ones last, as Np part units each.
     const int ns = a.S - a.Kr, shell = a.band_rows * ns, dg = a.band_rows * a.D;
     if (b < shell) {
       br = b / ns;
@@ -301,15 +301,15 @@ __device__ __forceinline__ unsigned force_sym_body(const SymArgs& a, int b) {
       s = a.S + k % a.D;
     } else {
       const int k = b - shell - dg;
-      part = k & 1;
-      br = (k >> 1) / a.Kr;
-      s = ns + (k >> 1) % a.Kr;
+      part = k % a.Np;
+      br = (k / a.Np) / a.Kr;
+      s = ns + (k / a.Np) % a.Kr;
     }
   }
   const int A = a.a0 + a.band0 + br;
   const bool diag = s >= a.S;
-  const bool split = !diag && s >= a.S - a.Kr;  // a split segment (two half sums)
-  const unsigned long long weight = split && part < 0 ? 2ull : 1ull;
+  const bool split = !diag && s >= a.S - a.Kr;  // a split segment (Np part sums)
+  const unsigned long long weight = split && part < 0 ? (unsigned long long)a.Np : 1ull;
   // Empty units (all-ghost row, segment past the row's shell) count as done for the work
   // audit (every unit is listed by exactly one launch).
   const bool count_empty = a.audit != nullptr;
@@ -317,7 +317,7 @@ __device__ __forceinline__ unsigned force_sym_body(const SymArgs& a, int b) {
     return count_empty ? (unsigned)weight : 0u;
   const int seg_tiles = a.L * G::kTilesPerQuantum;
   TileSeq<T> seq{A, a.NC, a.real_chunks, 0, 0, diag};
-  int u_lo = 0, u_mid = 0;  // shell: the segment's first tile and (split) its half point
+  int u_lo = 0;  // shell: the segment's first tile
   if (diag) {
     const int q = s - a.S, plen = G::kTilesPerChunk / a.D;  // D parts of the diagonal chunk
     seq.u = q * plen;
@@ -329,7 +329,6 @@ __device__ __forceinline__ unsigned force_sym_body(const SymArgs& a, int b) {
       return count_empty ? (unsigned)weight : 0u;
     seq.u1 = min(u0 + seg_tiles, h_tiles);
     u_lo = u0;
-    u_mid = min(u0 + seg_tiles / 2, seq.u1);
     seq.u = seq.valid(u0);
   }
   if (gated && !gate_open_or_defer(a, b, stage)) return 0u;  // counted when units 7 runs it
@@ -365,20 +364,23 @@ __device__ __forceinline__ unsigned force_sym_body(const SymArgs& a, int b) {
     run_tiles<T, false, EXACT>(a, is, seq, br, sm);
     store_i(static_cast<T*>(a.Pd) + ((int64_t)br * a.D + (s - a.S)) * 3 * kSymC);
   } else {
-    // One piece (the segment), or for a split segment its halves [u_lo, u_mid) -> Pi and
-    // [u_mid, end) -> Px: both (whole) or the one `part` names. One inlined copy of the tile.
+    // One piece (the segment), or for a split segment its Np parts: part p covers the tiles
+    // [u_lo + p seg / Np, u_lo + (p + 1) seg / Np) (clipped to the shell), part 0 -> Pi,
+    // part p > 0 -> Px slot p - 1; all of them (whole) or the one `part` names. One inlined
+    // copy of the tile.
     T* const pi = static_cast<T*>(a.Pi) + ((int64_t)br * a.S + s) * 3 * kSymC;
     T* const px = split ? static_cast<T*>(a.Px) +
-                              ((int64_t)br * a.Kr + (s - (a.S - a.Kr))) * 3 * kSymC
+                              ((int64_t)br * a.Kr + (s - (a.S - a.Kr))) * (a.Np - 1) * 3 * kSymC
                         : nullptr;
-    const int pc0 = split && part == 1 ? 1 : 0, pc1 = split && part != 0 ? 2 : 1;
+    const int pc0 = split && part > 0 ? part : 0;
+    const int pc1 = !split ? 1 : part >= 0 ? part + 1 : a.Np;
     const int u_end = seq.u1;
 #pragma unroll 1
     for (int pc = pc0; pc < pc1; ++pc) {
       TileSeq<T> sq = seq;
       if (split) {
-        sq.u1 = pc == 0 ? u_mid : u_end;
-        sq.u = sq.valid(pc == 0 ? u_lo : u_mid);
+        sq.u1 = min(u_lo + (pc + 1) * seg_tiles / a.Np, u_end);
+        sq.u = sq.valid(min(u_lo + pc * seg_tiles / a.Np, u_end));
       }
       if (pc > pc0) {
 #pragma unroll
@@ -386,7 +388,7 @@ __device__ __forceinline__ unsigned force_sym_body(const SymArgs& a, int b) {
           is.ax[i] = is.ay[i] = is.az[i] = std::remove_reference_t<decltype(is.ax[i])>(0);
       }
       run_tiles<T, true, EXACT>(a, is, sq, br, sm);
-      store_i(pc == 0 ? pi : px);
+      store_i(pc == 0 ? pi : px + (int64_t)(pc - 1) * 3 * kSymC);
       if (pc + 1 < pc1) __syncthreads();  // the next piece restages the LDS tiles and slots
 
     }
@@ -656,6 +658,23 @@ __device__ __forceinline__ void sym_tree_all(const SymArgs& a, int64_t li, T* S)
   t.result(S);
 }
 
+// The split segments [s, segs) of band row br added to acc in segment order, each as
+// (((part 0 + part 1) + part 2) + ...): part 0 from Pi (p: this body and component's Pi
+// column), parts 1 .. Np-1 from Px (off: the body and component offset within a slot).
+template <typename T>
+__device__ __forceinline__ T split_parts_add(const SymArgs& a, int br, int s, int segs,
+                                             int64_t off, const T* p, T acc) {
+  const T* px =
+      static_cast<const T*>(a.Px) + (int64_t)br * a.Kr * (a.Np - 1) * 3 * kSymC + off;
+  for (; s < segs; ++s) {
+    const int sp = s - (a.S - a.Kr);
+    T t = p[(int64_t)s * 3 * kSymC];
+    for (int q = 0; q + 1 < a.Np; ++q) t += px[((int64_t)sp * (a.Np - 1) + q) * 3 * kSymC];
+    acc += t;
+  }
+  return acc;
+}
+
 // Ti = sum_q Pd[q] + sum_s Pi[s] (each ascending) for the bodies of the band's rows.
 // Grid: (bodies / 256, 3 components). A pure streaming sum with a serial add chain per
 // thread: one component per thread triples the loads in flight, and the loads of 8 segments
@@ -676,7 +695,7 @@ __global__ __launch_bounds__(256) void sym_row_reduce_kernel(SymArgs a) {
   const int segs = (16 * h + a.L - 1) / a.L;  // shell length in 128-body quanta / L
   const T* __restrict__ p = static_cast<const T*>(a.Pi) + (int64_t)br * a.S * 3 * kSymC +
                             k * kSymC + c;
-  const int ns = min(segs, a.S - a.Kr);  // unsplit segments; then split ones: Pi + Px
+  const int ns = min(segs, a.S - a.Kr);  // unsplit segments; then split ones: Pi + Px parts
   constexpr int U = 8;
   int s = 0;
   for (; s + U <= ns; s += U) {
@@ -687,12 +706,7 @@ __global__ __launch_bounds__(256) void sym_row_reduce_kernel(SymArgs a) {
     for (int u = 0; u < U; ++u) acc += v[u];
   }
   for (; s < ns; ++s) acc += __builtin_nontemporal_load(p + (int64_t)s * 3 * kSymC);
-  if (s < segs) {
-    const T* __restrict__ px = static_cast<const T*>(a.Px) + (int64_t)br * a.Kr * 3 * kSymC +
-                               k * kSymC + c - (int64_t)(a.S - a.Kr) * 3 * kSymC;
-    for (; s < segs; ++s)
-      acc += p[(int64_t)s * 3 * kSymC] + px[(int64_t)s * 3 * kSymC];
-  }
+  if (s < segs) acc = split_parts_add(a, br, s, segs, k * kSymC + c, p, acc);
   static_cast<T*>(a.Ti)[(int64_t)k * a.n_local + (int64_t)(a.band0 + br) * kSymC + c] = acc;
 }
 
@@ -786,11 +800,8 @@ __global__ __launch_bounds__(192) void sym_tail_kernel(SymArgs a) {
       for (int u = 0; u < U; ++u) ti += v[u];
     }
     for (; sg < ns; ++sg) ti += __builtin_nontemporal_load(pi + (int64_t)sg * 3 * kSymC);
-    if (sg < segs) {  // split segments: the two half sums (sym_row_reduce_kernel order)
-      const T* px = static_cast<const T*>(a.Px) + (int64_t)br * a.Kr * 3 * kSymC + k * kSymC + c -
-                    (int64_t)(a.S - a.Kr) * 3 * kSymC;
-      for (; sg < segs; ++sg) ti += pi[(int64_t)sg * 3 * kSymC] + px[(int64_t)sg * 3 * kSymC];
-    }
+    if (sg < segs)  // split segments: the part sums (sym_row_reduce_kernel order)
+      ti = split_parts_add(a, br, sg, segs, k * kSymC + c, pi, ti);
     // + S: the tree over the B row blocks (sym_node_reduce_kernel's single node [0, B))
     TreeAcc<T, 1> t;
     t.pos = 0;
@@ -843,9 +854,9 @@ template <typename T>
 hipError_t launch_force_sym_t(const SymArgs& a, hipStream_t s) {
   int units = a.band_rows * (a.S + a.D);
   // units 0 (diagonal parts last) and the all-gather units 6 order list every split segment
-  // as two half units at their end
+  // as Np part units at their end
   if (a.Kr > 0 && (a.units == 0 || (a.units == 6 && a.gate_n <= 1)))
-    units += a.band_rows * a.Kr;
+    units += a.band_rows * a.Kr * (a.Np - 1);
   if (a.units >= 6 && (a.band_rows != a.rows || !a.lf)) return hipErrorInvalidValue;
   if (a.units == 7) units = a.defer_grid;  // strided walk over the deferred list
   if (units <= 0) return hipSuccess;

@@ -141,6 +141,7 @@ gs::SymArgs sym_args(gs_stepper* s, int cur) {
   a.Pd = s->sym_Pd;
   a.Px = s->sym_Px;
   a.Kr = s->sym_Kr;
+  a.Np = s->sym_Np;
   a.Sbuf = s->sym_S;
   a.Rbuf = s->sym_R;
   a.Ti = s->sym_Ti;
@@ -191,6 +192,7 @@ int ensure_sym(gs_stepper* s) {
   if (gs_sym_geometry(s->L.n_pad, &s->sym_NC, &s->sym_H, &s->sym_L, &s->sym_S_n, &s->sym_D))
     return -1;
   s->sym_Kr = gs_sym_split_segments(s->L.n_pad);
+  s->sym_Np = gs_sym_split_parts(s->L.n_pad);
   const int P = s->cfg.nranks;
   s->rbeg.assign(P, 0);
   s->rcnt.assign(P, 0);
@@ -215,7 +217,7 @@ int ensure_sym(gs_stepper* s) {
   // (tests use a tiny budget to force many bands). 1M bodies need 6.4 GB for all rows; 16M
   // on 8 ranks needs 109 GB per rank, one band on an otherwise empty MI355X.
   const size_t per_row =
-      (size_t)(s->sym_S_n + s->sym_Kr + s->sym_H + s->sym_D) * 3 * gs::kSymC * e;
+      (size_t)(s->sym_S_n + s->sym_kx() + s->sym_H + s->sym_D) * 3 * gs::kSymC * e;
   size_t budget = (size_t)32 << 30;
   size_t free_b = 0, total_b = 0;
   if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b / 2 > budget) budget = free_b / 2;
@@ -230,7 +232,7 @@ int ensure_sym(gs_stepper* s) {
   if (dev_alloc(s, &s->sym_Pj, band * s->sym_H * 3 * gs::kSymC * e, "sym_Pj")) return -1;
   if (dev_alloc(s, &s->sym_Pd, band * s->sym_D * 3 * gs::kSymC * e, "sym_Pd")) return -1;
   if (s->sym_Kr > 0 &&
-      dev_alloc(s, &s->sym_Px, band * s->sym_Kr * 3 * gs::kSymC * e, "sym_Px"))
+      dev_alloc(s, &s->sym_Px, band * s->sym_kx() * 3 * gs::kSymC * e, "sym_Px"))
     return -1;
   if (dev_alloc(s, &s->sym_Ti, 3 * nl * e, "sym_Ti")) return -1;
   const size_t nb = (size_t)((s->L.n + gs::kSymC - 1) / gs::kSymC) * gs::kSymC;  // real chunks
@@ -811,7 +813,7 @@ int gs_stepper_create(const gs_config* cfg, gs_stepper** out) {
   if (s->L.mode == GS_MODE_SYM) {
     // Deferred-unit list of the gated launch (one band's units) and the local-first order.
     const int rows = (int)(s->L.n_local / gs::kSymC);
-    const size_t units = (size_t)rows * (s->sym_S_n + s->sym_D + s->sym_Kr) + 1;
+    const size_t units = (size_t)rows * (s->sym_S_n + s->sym_D + s->sym_kx()) + 1;
     ALLOC_CLEAN(&s->defer, units * sizeof(unsigned), "defer");
     FAIL_CLEAN(hipMemsetAsync(s->defer, 0, units * sizeof(unsigned), s->s_comp));
     // unit -> row << 16 | segment (bit 31: remote), local units first (layout.cpp).
@@ -821,8 +823,8 @@ int gs_stepper_create(const gs_config* cfg, gs_stepper** out) {
     const int64_t got =
         s->sym_ring ? gs_sym_unit_map_ring(s->L.n_pad, cfg->rank, cfg->nranks, fill, lf.data(),
                                            (int64_t)lf.size())
-                    : gs_sym_unit_map_kr(s->L.n_pad, cfg->rank, cfg->nranks, fill, s->sym_Kr,
-                                         lf.data(), (int64_t)lf.size());
+                    : gs_sym_unit_map_parts(s->L.n_pad, cfg->rank, cfg->nranks, fill, s->sym_Kr,
+                                            s->sym_Np, lf.data(), (int64_t)lf.size());
     lf.resize(got > 0 ? (size_t)got : 0);  // 0: geometry too large for the 16-bit fields
     if (!lf.empty()) {
       ALLOC_CLEAN(&s->sym_lf, lf.size() * sizeof(int32_t), "unit_map");
@@ -832,7 +834,7 @@ int gs_stepper_create(const gs_config* cfg, gs_stepper** out) {
   }
   if (s->L.mode == GS_MODE_SYM && getenv("GRAVSIM_UNIT_TRACE")) {
     // One entry per unit of a band-wide launch plus as many deferred ones (units 7).
-    s->utrace_main = (int64_t)s->sym_band * (s->sym_S_n + s->sym_D + s->sym_Kr);
+    s->utrace_main = (int64_t)s->sym_band * (s->sym_S_n + s->sym_D + s->sym_kx());
     ALLOC_CLEAN(&s->utrace, (size_t)(2 * s->utrace_main) * 4 * sizeof(unsigned long long), "unit_trace");
     FAIL_CLEAN(hipMemsetAsync(s->utrace, 0, (size_t)(2 * s->utrace_main) * 4 * 8, s->s_comp));
   }
@@ -1052,8 +1054,8 @@ int gs_stepper_audit(gs_stepper* s, uint64_t* units_done, uint64_t* units_per_st
   if (!s->audit) return 0;  // one-sided schedules: no unit audit
   GS_HIP(hipSetDevice(s->cfg.device));
   const uint64_t rows = (uint64_t)(s->L.n_local / gs::kSymC);
-  // (a split segment counts as its two halves, whichever way it ran)
-  if (units_per_step) *units_per_step = rows * (uint64_t)(s->sym_S_n + s->sym_D + s->sym_Kr);
+  // (a split segment counts as its Np parts, whichever way it ran)
+  if (units_per_step) *units_per_step = rows * (uint64_t)(s->sym_S_n + s->sym_D + s->sym_kx());
   if (units_done) {
     GS_HIP(hipStreamSynchronize(s->s_comp));
     unsigned long long h = 0;

@@ -107,12 +107,17 @@ int32_t gs_sym_shell_len(int32_t A, int32_t NC);
 // Unit order of the gated sym launch for one rank (see layout.cpp); returns the entry count.
 int64_t gs_sym_unit_map(int64_t n_pad, int32_t rank, int32_t nranks, int64_t fill,
                         int32_t* out, int64_t cap);
-// ... with the last kr shell segments of every row split into two half units at the end.
+// ... with the last kr shell segments of every row split into np part units at the end (bit
+// 30, part in bits 28-29; rows < 4096); the _kr form is np = 2.
 int64_t gs_sym_unit_map_kr(int64_t n_pad, int32_t rank, int32_t nranks, int64_t fill,
                            int32_t kr, int32_t* out, int64_t cap);
+int64_t gs_sym_unit_map_parts(int64_t n_pad, int32_t rank, int32_t nranks, int64_t fill,
+                              int32_t kr, int32_t np, int32_t* out, int64_t cap);
 // Split shell segments per row (SymArgs::Kr) for a geometry: S / 16 when a segment has at
-// least 2 tiles of 128 bodies (L >= 2), else 0.
+// least 2 tiles of 128 bodies (L >= 2), else 0; and the parts each is split into (SymArgs::Np:
+// 4 when L >= 4, else 2).
 int32_t gs_sym_split_segments(int64_t n_pad);
+int32_t gs_sym_split_parts(int64_t n_pad);
 // The same for the ring strategy: entries carry the ring stage (bits 28-30) at which the last
 // slice a unit reads arrives, and units are ordered by stage (rows < 4096, nranks <= 8).
 int64_t gs_sym_unit_map_ring(int64_t n_pad, int32_t rank, int32_t nranks, int64_t fill,
@@ -201,8 +206,8 @@ int gs_stepper_set_tuning(gs_stepper* s, int32_t first_wave, int32_t fused_tail)
 // Re-resolve the force path with a new cutoff mode (0 auto, 1 exact select, 2 fast core).
 int gs_stepper_set_cutoff_mode(gs_stepper* s, int32_t mode);
 // Work audit of the sym schedule: force units completed since the last reset (waits for the
-// compute stream) and the units one step must run on this rank (rows x (S + D + Kr): a split
-// segment counts as its two halves, whichever way it runs); both 0 for the one-sided
+// compute stream) and the units one step must run on this rank (rows x (S + D + (Np - 1) Kr):
+// a split segment counts as its Np parts, whichever way it runs); both 0 for the one-sided
 // schedules.
 int gs_stepper_audit(gs_stepper* s, uint64_t* units_done, uint64_t* units_per_step);
 int gs_stepper_audit_reset(gs_stepper* s);

@@ -61,12 +61,14 @@ struct SymArgs {
   void* Pj;            // [rows][H][3][kSymC] j-side partials, H = NC / 2
   void* Pd;            // [rows][D][3][kSymC] diagonal-chunk partials
   // Split segments (the launch tail): the last Kr shell segments of every row are summed as
-  // two halves of their tiles, h1 in Pi and h2 in Px[rows][Kr][3][kSymC]; the row reduce adds
-  // Pi + Px for them. A designated segment runs whole (both halves, one workgroup) or as two
-  // half units (entries at the end of the units 0 / units 6 orders, so the launch's last
-  // units are half as long); either way the same two sums, so the same bits.
+  // Np parts of their tiles (gs_sym_split_parts: 4 when a segment has >= 4 quanta, else 2),
+  // part 0 in Pi and part p > 0 in Px[rows][Kr][Np - 1][3][kSymC]; the row reduce adds
+  // (((part 0 + part 1) + part 2) + ...) for them. A designated segment runs whole (all parts,
+  // one workgroup) or as Np part units (entries at the end of the units 0 / units 6 orders, so
+  // the launch's last units are 1 / Np as long); either way the same Np sums, so the same
+  // bits. A step then runs rows x (S + D + (Np - 1) Kr) units.
   void* Px;
-  int32_t Kr;
+  int32_t Kr, Np;
   void* Ti;            // [3][n_local] per-body i-side total: sum_q Pd[q] + sum_s Pi[s]
   void* Sbuf;          // [dest rank q][own node k < nn][3][n_local(q)] node sums by destination
   const void* Rbuf;    // [node j, all ranks' nodes in global order][3][n_local] received
@@ -89,7 +91,7 @@ struct SymArgs {
   int32_t fp64;        // element type of every array above
   int32_t exact;       // reference hard cutoff (select at cut2) instead of the fast core
   int32_t units;       // which units a force launch covers: 0 all (shell segments row by row,
-                       // then the diagonal parts, then the split segments as half units:
+                       // then the diagonal parts, then the split segments as part units:
                        // short units fill the launch's last wave), 6 all, rank-local units
                        // first, remote units gated on `gate`, 7 the units the units-6 launch
                        // deferred (after the gather)
@@ -120,8 +122,8 @@ struct SymArgs {
   // dynamic launch re-armed it): the launcher skips its memset.
   int32_t work_zero;
   // Work audit: +1 per force unit that ran to completion (or was empty), so a step's count
-  // must be rows x (S + D + Kr) whatever the launch split, deferral or fetch order (a split
-  // segment run whole counts its two halves).
+  // must be rows x (S + D + (Np - 1) Kr) whatever the launch split, deferral or fetch order (a
+  // split segment run whole counts its Np parts).
   unsigned long long* audit;
 };
 

@@ -93,13 +93,16 @@ struct gs_stepper {
   char* sym_Pi = nullptr;  // element type: float or double (esz)
   char* sym_Pj = nullptr;
   char* sym_Pd = nullptr;
-  char* sym_Px = nullptr;  // second halves of the split segments [band][Kr][3][kSymC]
+  char* sym_Px = nullptr;  // parts 1 .. Np-1 of the split segments [band][Kr][Np-1][3][kSymC]
   char* sym_S = nullptr;  // node sums by destination rank
   char* sym_R = nullptr;  // node sums of every rank, global node order (== sym_S, one rank)
   char* sym_Ti = nullptr;  // per-body i-side totals [3][n_local]
   char* sym_Bb = nullptr;  // multi-band runs: per-block leaf sums [own blocks][3][bodies]
   int32_t sym_NC = 0, sym_H = 0, sym_L = 0, sym_S_n = 0, sym_D = 1;
   int32_t sym_Kr = 0;    // split shell segments per row (gs_sym_split_segments)
+  int32_t sym_Np = 2;    // parts per split segment (gs_sym_split_parts)
+  // extra units per row from the split segments: a step runs rows x (S + D + kx) units
+  int32_t sym_kx() const { return sym_Kr * (sym_Np - 1); }
   int32_t sym_band = 0;  // rows per band (Pi/Pj/Pd hold one band; a multiple of sym_RB)
   // Row blocks and reduction-tree nodes (gs_sym_nodes): rank q owns blocks
   // [blk_lo[q], blk_lo[q + 1]) = bodies [rbeg[q], rbeg[q] + rcnt[q]); it sends nn(q) nodes,
@@ -154,8 +157,8 @@ struct gs_stepper {
   bool graph_failed = false;    // multi-rank capture refused: eager fallback
   bool work_zero = true;        // sym dynamic unit counter (gate_buf[4]) known to be 0
   // Work audit of the sym force launches (nbody_sym.hip: one batched add per workgroup of the
-  // units it ran); a step runs rows x (S + D + Kr) units on this rank (each split segment
-  // counts as its two halves) whatever the launch split or fetch order.
+  // units it ran); a step runs rows x (S + D + (Np - 1) Kr) units on this rank (each split
+  // segment counts as its Np parts) whatever the launch split or fetch order.
   unsigned long long* audit = nullptr;
   // Fault injection for the audit's own test (GRAVSIM_FAULT_SKIP_UNITS=k): every dynamic
   // force launch starts its unit counter at k instead of 0, so units 0 .. k-1 never run,

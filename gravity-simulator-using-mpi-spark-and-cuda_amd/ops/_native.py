@@ -74,7 +74,9 @@ def _build(which: str) -> None:
         raise NativeUnavailable(f"building libgravsim_{which}.so failed:\n{r.stdout}\n{r.stderr}")
 
 
-def _sig(lib, name, res, args):
+def _sig(lib, name, res, args, optional=False):
+    if optional and not hasattr(lib, name):
+        return None
     f = getattr(lib, name)
     f.restype = res
     f.argtypes = args
@@ -98,6 +100,11 @@ def _declare_common(lib) -> None:
     _sig(lib, "gs_sym_unit_map_kr", c_int64, [c_int64, c_int32, c_int32, c_int64, c_int32,
                                               POINTER(c_int32), c_int64])
     _sig(lib, "gs_sym_split_segments", c_int32, [c_int64])
+    # Np-part split segments (round 4); optional only so that A/B runs can load an older
+    # library (scripts/build_variant.py of an earlier tree), whose split segments have 2 parts
+    _sig(lib, "gs_sym_unit_map_parts", c_int64, [c_int64, c_int32, c_int32, c_int64, c_int32,
+                                                 c_int32, POINTER(c_int32), c_int64], optional=True)
+    _sig(lib, "gs_sym_split_parts", c_int32, [c_int64], optional=True)
     _sig(lib, "gs_auto_chunk", c_int32, [c_int64])
     _sig(lib, "gs_ic_fill_host", None, [c_int32, c_uint64, c_int64, c_int64, c_int64, _PD, _PD,
                                         _PD])

@@ -176,13 +176,17 @@ class HipEngine:
                 "deferred_units": int(v[6]), "comm_ms": v[2] + v[3],
                 "exposed_comm_ms": v[4] + v[5], "graph": graph}
 
-    def sym_geometry(self) -> tuple[int, int, int]:
-        """(S shell segments, D diagonal parts, Kr split segments) per chunk row of the sym
-        schedule: a step runs rows x (S + D + Kr) units on a rank (the work audit)."""
+    def sym_geometry(self) -> tuple[int, int, int, int]:
+        """(S shell segments, D diagonal parts, Kr split segments, Np parts per split segment)
+        per chunk row of the sym schedule: a step runs rows x (S + D + (Np - 1) Kr) units on a
+        rank (the work audit)."""
         n_pad = int(self.native_layout["n_pad"])
         v = [ctypes.c_int32() for _ in range(5)]
         self.lib.gs_sym_geometry(n_pad, *[ctypes.byref(x) for x in v])
-        return int(v[3].value), int(v[4].value), int(self.lib.gs_sym_split_segments(n_pad))
+        parts = (int(self.lib.gs_sym_split_parts(n_pad))
+                 if hasattr(self.lib, "gs_sym_split_parts") else 2)  # (pre-round-4 builds: 2)
+        return (int(v[3].value), int(v[4].value), int(self.lib.gs_sym_split_segments(n_pad)),
+                parts)
 
     def unit_trace(self) -> np.ndarray:
         """(entries, 4) uint64 timeline of the last sym force launch (GRAVSIM_UNIT_TRACE set

@@ -2,8 +2,9 @@
 
 bench.py must not be able to print a fast headline for steps that skipped work (round 2:
 graph replays after the first ran no units until commit 8fdec84). The force kernels count
-every unit they run (nbody_sym.hip audit_unit); a step must run rows x (S + D) units per
-rank whatever the launch split, band count, fetch order or graph replay. A skipped-unit fault
+every unit they run (nbody_sym.hip audit_unit); a step must run rows x (S + D + (Np - 1) Kr)
+units per rank (Kr split segments of Np parts per row) whatever the launch split, band count,
+fetch order or graph replay. A skipped-unit fault
 (GRAVSIM_FAULT_SKIP_UNITS: the dynamic counter starts past 0, the failure class of a stale
 re-armed counter) must be caught by bench.py's unit count and by its independent replay.
 
@@ -49,12 +50,13 @@ def test_unit_audit_counts_every_unit(hip, monkeypatch, n, dtype, P, band_mb, gr
         per = []
         for s in g.shards:
             done, per_step = s.audit()
-            assert per_step > 0
+            S, D, Kr, Np = s.sym_geometry()
+            assert per_step == s.layout.n_local // 2048 * (S + D + (Np - 1) * Kr)
             assert done == per_step * steps, (done, per_step)
             per.append(per_step)
-        # every rank's rows together: all NC rows x (S + D)
+        # every rank's rows together: all NC rows x (S + D + (Np - 1) Kr)
         NC = g.shards[0].layout.n_pad // 2048
-        assert sum(per) % NC == 0
+        assert sum(per) == NC * (S + D + (Np - 1) * Kr)
         # the step-path acceleration query runs every unit once more
         if P == 1:
             s = g.shards[0]

@@ -207,39 +207,48 @@ def test_node_merge_equals_full_tree_bitwise_for_every_P(B):
 
 @pytest.mark.parametrize("n_pad,P", [(65536, 1), (65536, 8), (1 << 20, 1), (1 << 20, 8),
                                      (1 << 20, 3), (262144, 6)])
-def test_split_segment_map(n_pad, P):
+@pytest.mark.parametrize("np_", [None, 2])
+def test_split_segment_map(n_pad, P, np_):
     """The last Kr shell segments of every row (Kr = S / 16 when a segment has >= 2 tiles) are
-    split: the gated order lists every other unit once and each split segment as two half
-    units (bit 30, half in bit 29) at the very end, with the segment's locality flag."""
+    split into Np parts (gs_sym_split_parts: 4 when a segment spans >= 4 quanta, else 2): the
+    gated order lists every other unit once and each split segment as Np part units (bit 30,
+    part in bits 28-29, rows in bits 16-27) at the very end, with the segment's locality."""
     lib, g = _geo(n_pad)
     S, D = g["S"], g["D"]
     kr = lib.gs_sym_split_segments(n_pad)
     assert kr == (S // 16 if g["L"] >= 2 else 0)
+    npart = lib.gs_sym_split_parts(n_pad) if np_ is None else np_
+    assert npart == (4 if g["L"] >= 4 else 2) or np_ is not None
     for rank in (0, P - 1):
         a0, rows = partition.sym_rank_rows(n_pad, P, rank)
         plain = (ctypes.c_int32 * (rows * (S + D)))()
         assert lib.gs_sym_unit_map(n_pad, rank, P, 1024, plain, len(plain)) == rows * (S + D)
-        out = (ctypes.c_int32 * (rows * (S + D + kr)))()
-        n = lib.gs_sym_unit_map_kr(n_pad, rank, P, 1024, kr, out, len(out))
-        assert n == rows * (S + D + kr)
+        total = rows * (S + D + (npart - 1) * kr)
+        out = (ctypes.c_int32 * total)()
+        n = lib.gs_sym_unit_map_parts(n_pad, rank, P, 1024, kr, npart, out, len(out))
+        assert n == total
+        if npart == 2:  # the _kr entry point is the two-part map
+            out2 = (ctypes.c_int32 * total)()
+            assert lib.gs_sym_unit_map_kr(n_pad, rank, P, 1024, kr, out2, len(out2)) == total
+            assert bytes(out2) == bytes(out)
         m = np.frombuffer(out, dtype=np.uint32)
-        half = ((m >> 30) & 1).astype(bool)
-        part = (m >> 29) & 1
-        row = (m >> 16) & 0x1FFF
+        split = ((m >> 30) & 1).astype(bool)
+        part = (m >> 28) & 3
+        row = (m >> 16) & 0xFFF
         unit = m & 0xFFFF
-        n_half = rows * kr * 2
-        assert half[len(m) - n_half:].all() and not half[:len(m) - n_half].any()  # at the end
-        whole = unit[~half].astype(np.int64) + row[~half].astype(np.int64) * (S + D)
+        n_part = rows * kr * npart
+        assert split[len(m) - n_part:].all() and not split[:len(m) - n_part].any()  # at the end
+        whole = unit[~split].astype(np.int64) + ((m[~split] >> 16) & 0x7FFF).astype(np.int64) * (S + D)
         expect = [r * (S + D) + u for r in range(rows) for u in range(S + D)
                   if not (S - kr <= u < S)]
         assert np.array_equal(np.sort(whole), np.array(expect, dtype=np.int64))
-        hk = (row[half].astype(np.int64) * S + unit[half]) * 2 + part[half]
-        want = sorted((r * S + u) * 2 + h for r in range(rows) for u in range(S - kr, S)
-                      for h in (0, 1))
+        hk = (row[split].astype(np.int64) * S + unit[split]) * npart + part[split]
+        want = sorted((r * S + u) * npart + h for r in range(rows) for u in range(S - kr, S)
+                      for h in range(npart))
         assert np.array_equal(np.sort(hk), np.array(want, dtype=np.int64))
-        # a split segment's halves carry its locality (remote = reads gathered rows)
+        # a split segment's parts carry its locality (remote = reads gathered rows)
         pm = np.frombuffer(plain, dtype=np.uint32)
         rem_plain = {(int((x >> 16) & 0x7FFF), int(x & 0xFFFF)): bool(x >> 31) for x in pm}
-        for x in m[half]:
-            key = (int((x >> 16) & 0x1FFF), int(x & 0xFFFF))
+        for x in m[split]:
+            key = (int((x >> 16) & 0xFFF), int(x & 0xFFFF))
             assert bool(x >> 31) == rem_plain[key]
