@@ -12,7 +12,7 @@ ms(P=1) / (P * ms(P)). Not physics: remote slices hold stale positions.
     python bench/rank_shape.py --n 1048576 --ranks 1,2,4,8 --comm-gbps 0,64 --overlap 0,3
 
 Since round 3 the sym schedule runs every P up to 8 (uneven row blocks for P not dividing
-the 64 blocks): --rank all measures every rank of such a run (rank 0 holds the most blocks).
+the 256 blocks): --rank all measures every rank of such a run (rank 0 holds the most blocks).
 """
 from __future__ import annotations
 

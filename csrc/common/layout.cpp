@@ -383,8 +383,9 @@ extern "C" int64_t gs_sym_unit_map_ring(int64_t n_pad, int32_t rank, int32_t nra
 }
 
 // Partial-slot bytes of rank 0 (the largest share) if all of its rows were held at once (one
-// band): Pi + Pj + Pd (3 elements per body per slot), the node sums it sends (nn x 3 per
-// body of the run) and the ones it receives (NN x 3 per own body).
+// band): Pi + Px (the split segments' extra parts) + Pj + Pd (3 elements per body per slot),
+// the node sums it sends (nn x 3 per body of the run) and the ones it receives (NN x 3 per own
+// body).
 extern "C" int64_t gs_sym_bytes(int64_t n_pad, int32_t nranks, int32_t esz) {
   int32_t nc, h, l, sg, dp, a0, rows, nn, NN;
   if (gs_sym_geometry(n_pad, &nc, &h, &l, &sg, &dp) ||
@@ -392,7 +393,8 @@ extern "C" int64_t gs_sym_bytes(int64_t n_pad, int32_t nranks, int32_t esz) {
       gs_sym_nodes(n_pad, nranks, 0, nullptr, nullptr, &nn, nullptr, &NN))
     return -1;
   const int64_t n_local = (int64_t)rows * 2048;
-  return n_local * 3 * esz * ((int64_t)sg + h + dp) +
+  const int64_t kx = (int64_t)gs_sym_split_segments(n_pad) * (gs_sym_split_parts(n_pad) - 1);
+  return n_local * 3 * esz * ((int64_t)sg + kx + h + dp) +
          ((int64_t)nn * n_pad + (int64_t)NN * n_local) * 3 * esz;
 }
 

@@ -13,7 +13,7 @@
 //     every chunk row carries the same amount of work and rank ownership is a plain block
 //     partition of rows;
 //   * both sides land in pre-assigned partial slots and are summed in a fixed order by the
-//     node-reduce and finalize kernels (a binary tree over 64 row blocks): deterministic, and
+//     node-reduce and finalize kernels (a binary tree over up to 256 row blocks): deterministic, and
 //     the same bits for every rank count P from 1 to 8 (the tree nodes are what crosses
 //     ranks; a rank owns whole row blocks by mpi.c:184-187's remainder rule).
 #include <hip/hip_runtime.h>
@@ -478,7 +478,7 @@ void force_sym_kernel_f64(SymArgs a) {
 // scratch); callers push in a wave-uniform order, so the carry branches do not diverge.
 template <typename T, int C>
 struct TreeAcc {
-  static constexpr int kDepth = 7;  // B <= 64 blocks
+  static constexpr int kDepth = 9;  // B <= 256 blocks (gs_common.h kSymMaxBlocks)
   T st[kDepth][C];
   unsigned pos;
   __device__ __forceinline__ void push(int level, T* v) {
@@ -508,6 +508,31 @@ struct TreeAcc {
     for (int c = 0; c < C; ++c) v[c] = st[0][c];
   }
 };
+
+// Leaves b in [lo, lo + n) of an aligned sub-tree (n a power of two, lo a multiple of n) into
+// t. Four aligned leaves are summed as ((l0 + l1) + (l2 + l3)) and pushed as one level-2
+// sub-tree: exactly what four level-0 pushes merge to (binary-counter order), with a quarter of
+// the stack shifts. (Loading the four leaves' rows as one batch for 1- and 2-row blocks, same
+// bits, doubled the node reduce at 1M: 1.12 vs ~0.6 ms, profiles/r4s2_b256_leaf_batch_ab.jsonl.)
+template <typename T, int C, typename Leaf>
+__device__ __forceinline__ void push_leaves(TreeAcc<T, C>& t, int lo, int n, Leaf&& leaf) {
+  if (n >= 4) {
+    for (int b = lo; b < lo + n; b += 4) {
+      T v[4][C];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) leaf(b + j, v[j]);
+#pragma unroll
+      for (int c = 0; c < C; ++c) v[0][c] = (v[0][c] + v[1][c]) + (v[2][c] + v[3][c]);
+      t.push(2, v[0]);
+    }
+  } else {
+    for (int b = lo; b < lo + n; ++b) {
+      T v[C];
+      leaf(b, v);
+      t.push(0, v);
+    }
+  }
+}
 
 // Adds, in ascending row order, Pj of the rows in [A_lo, A_hi) whose shell holds chunk X
 // (body (X, c), one component per C). The caller passes a range where the distance
@@ -608,8 +633,8 @@ __global__ __launch_bounds__(256) void sym_node_reduce_kernel(SymArgs a) {
   TreeAcc<T, 3> t;
   t.pos = 0;
   const T* Bb = static_cast<const T*>(a.Bbuf);
-  for (int b = lo; b < lo + (1 << l); ++b) {
-    T v[3];
+  const T* pjc = static_cast<const T*>(a.Pj) + c;
+  auto leaf = [&](int b, T* v) {
     if (Bb) {
       const T* p = Bb + (int64_t)(b - own_lo) * 3 * nb + x;
       v[0] = p[0];
@@ -617,10 +642,10 @@ __global__ __launch_bounds__(256) void sym_node_reduce_kernel(SymArgs a) {
       v[2] = p[2 * nb];
     } else {
       const int A_lo = b * a.RB, A_hi = min((b + 1) * a.RB, a.real_chunks);
-      pj_row_sum<T, 3>(a, A_lo, max(A_lo, A_hi), X, static_cast<const T*>(a.Pj) + c, kSymC, v);
+      pj_row_sum<T, 3>(a, A_lo, max(A_lo, A_hi), X, pjc, kSymC, v);
     }
-    t.push(0, v);
-  }
+  };
+  push_leaves(t, lo, 1 << l, leaf);
   T r[3];
   t.result(r);
   const int q = sym_row_owner(a, X);
@@ -806,12 +831,10 @@ __global__ __launch_bounds__(192) void sym_tail_kernel(SymArgs a) {
     TreeAcc<T, 1> t;
     t.pos = 0;
     const T* pjc = static_cast<const T*>(a.Pj) + k * kSymC + c;
-    for (int b = 0; b < a.B; ++b) {
+    push_leaves(t, 0, a.B, [&](int b, T* v) {
       const int A_lo = b * a.RB, A_hi = min((b + 1) * a.RB, a.real_chunks);
-      T v[1];
       pj_row_sum<T, 1>(a, A_lo, max(A_lo, A_hi), X, pjc, kSymC, v);
-      t.push(0, v);
-    }
+    });
     T S[1];
     t.result(S);
     ti = ti + S[0];

@@ -38,7 +38,7 @@ inline int split_span(const KArgs<T>& a) {
 // ---- Newton-3 symmetric schedule (fp32/fp64, fast cutoff; nbody_sym.hip) -------------
 // Canonical decomposition, a function of the padded body count only (so every rank count
 // P from 1 to 8 produces the same bits): chunks of kSymC = 2048 bodies, NC = n_pad / 2048 of
-// them, B row blocks of RB = NC / B rows (gs_common.h sym_blocks: B <= 64). Chunk A pairs
+// them, B row blocks of RB = NC / B rows (gs_common.h sym_blocks: B <= 256). Chunk A pairs
 // with the next h(A) chunks cyclically (h = NC/2 - 1, plus the antipodal chunk A + NC/2 for
 // half of the rows, alternating by parity: every unordered chunk pair exactly once, equal
 // work per block of rows) and with itself (one-sided). Row A's shell is cut into segments of

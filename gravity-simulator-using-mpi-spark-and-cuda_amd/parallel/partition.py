@@ -12,7 +12,7 @@ order fixed, so instead:
   so partials computed on any rank, in any launch shape, add up to the same bits.
 
 The Newton-3 (sym) schedule pads as an 8-rank run would and cuts its NC chunk rows into B
-row blocks (B <= 64, a power of two dividing NC); rank r owns whole blocks by mpi.c's own
+row blocks (B <= 256, a power of two dividing NC); rank r owns whole blocks by mpi.c's own
 remainder rule (the first B mod P ranks hold one more), so every P from 1 to 8 is balanced to
 within one block and the reduction tree over the blocks keeps the bits P-independent.
 """
@@ -87,9 +87,12 @@ def sym_geometry(n_pad: int) -> dict:
     return {"NC": nc, "H": h, "L": seg, "S": -(-16 * h // seg), "D": 16 // seg if seg < 16 else 1}
 
 
+SYM_MAX_BLOCKS = 256  # gs_common.h kSymMaxBlocks
+
+
 def sym_blocks(nc: int) -> int:
-    """Row blocks of the sym schedule: the largest power of two <= 64 dividing NC."""
-    b = 64
+    """Row blocks of the sym schedule: the largest power of two <= 256 dividing NC."""
+    b = SYM_MAX_BLOCKS
     while b > 1 and nc % b:
         b >>= 1
     return b
@@ -131,15 +134,24 @@ def sym_nodes(n_pad: int, nranks: int) -> list[list[tuple[int, int]]]:
             for q in range(nranks)]
 
 
+def sym_split(n_pad: int) -> tuple[int, int]:
+    """(Kr, Np): the split shell segments per row and their parts (layout.cpp
+    gs_sym_split_segments / gs_sym_split_parts): S / 16 segments when a segment spans >= 2
+    quanta, in 4 parts when it spans >= 4, else 2."""
+    g = sym_geometry(n_pad)
+    return (g["S"] // 16 if g["L"] >= 2 else 0), (4 if g["L"] >= 4 else 2)
+
+
 def sym_bytes(n_pad: int, nranks: int, esz: int = 4) -> int:
     """Partial-slot bytes of rank 0 (the largest share) if all its rows were held at once
     (one band), plus the node sums it sends and receives (layout.cpp gs_sym_bytes)."""
     g = sym_geometry(n_pad)
+    kr, np_ = sym_split(n_pad)
     _, rows = sym_rank_rows(n_pad, nranks, 0)
     n_local = rows * SYM_CHUNK
     nodes = sym_nodes(n_pad, nranks)
     NN = sum(len(x) for x in nodes)
-    return n_local * 3 * esz * (g["S"] + g["H"] + g["D"]) + \
+    return n_local * 3 * esz * (g["S"] + kr * (np_ - 1) + g["H"] + g["D"]) + \
         (len(nodes[0]) * n_pad + NN * n_local) * 3 * esz
 
 

@@ -57,7 +57,7 @@ def test_segmented_plan_matches_eager(hip, monkeypatch, strategy, overlap):
 
 @pytest.mark.parametrize("P,rank", [(3, 0), (3, 2), (5, 4), (6, 5), (7, 0), (7, 6)])
 def test_uneven_rank_emulation_runs(hip, monkeypatch, P, rank):
-    """Per-rank emulation of P not dividing the 64 row blocks (1M bodies): rank 0 holds the
+    """Per-rank emulation of P not dividing the 256 row blocks (1M bodies): rank 0 holds the
     most blocks, the last ranks the fewest and receive the most tree nodes; the modeled
     collectives (gather, node exchange) stay inside their buffers and every unit runs."""
     e = _emu(monkeypatch, 1 << 20, P, rank, 64, 3)

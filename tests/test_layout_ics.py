@@ -156,12 +156,13 @@ def test_sym_layout_rejects_unsupported():
 
 def test_sym_auto_at_headline_size():
     """N = 1M fp32 picks the Newton-3 schedule for every P from 1 to 8 with unchanged
-    padding; ranks own whole row blocks of 8 rows (64 blocks), mpi.c's remainder rule."""
+    padding; ranks own whole row blocks of 2 rows (256 blocks), mpi.c's remainder rule."""
     for P in range(1, 9):
         assert partition.sym_auto(1 << 20, P)
         lays = [partition.layout(1 << 20, r, P, sym=True) for r in range(P)]
         assert all(L.n_pad == 1 << 20 for L in lays)
-        counts = [L.n_local // (8 * 2048) for L in lays]  # blocks per rank
-        assert sum(counts) == 64 and max(counts) - min(counts) <= 1
-        assert counts == sorted(counts, reverse=True)  # the first 64 mod P ranks hold one more
-        assert [L.local_begin for L in lays] == [sum(counts[:r]) * 8 * 2048 for r in range(P)]
+        counts = [L.n_local // (2 * 2048) for L in lays]  # blocks per rank
+        assert sum(counts) == 256 and max(counts) - min(counts) <= 1
+        assert counts == sorted(counts, reverse=True)  # the first 256 mod P ranks hold one more
+        assert max(counts) * P / 256 <= 1.02  # at most 2 % over the mean for every P <= 8
+        assert [L.local_begin for L in lays] == [sum(counts[:r]) * 2 * 2048 for r in range(P)]

@@ -187,7 +187,7 @@ def _counter_merge(nodes_vals):
     return acc[k]
 
 
-@pytest.mark.parametrize("B", [8, 16, 32, 64])
+@pytest.mark.parametrize("B", [8, 16, 32, 64, 128, 256])
 def test_node_merge_equals_full_tree_bitwise_for_every_P(B):
     """fp32 leaves: every rank reduces its dyadic nodes (a sub-tree each) and the receiver
     merges them in global order. The result is the full tree's, bit for bit, for every P:
@@ -196,7 +196,7 @@ def test_node_merge_equals_full_tree_bitwise_for_every_P(B):
     leaves = (rng.standard_normal((B, 1000)) * np.exp(rng.uniform(-20, 20, (B, 1)))).astype(
         np.float32)
     full = _tree(list(leaves))
-    n_pad = B * (3 if B < 64 else 1) * 2048  # NC with sym_blocks(NC) == B
+    n_pad = B * (3 if B < 256 else 1) * 2048  # NC with sym_blocks(NC) == B
     assert partition.sym_blocks(n_pad // 2048) == B
     for P in range(1, min(8, B) + 1):
         vals = [(l, _tree(list(leaves[lo:lo + (1 << l)])))
@@ -252,3 +252,26 @@ def test_split_segment_map(n_pad, P, np_):
         for x in m[split]:
             key = (int((x >> 16) & 0xFFF), int(x & 0xFFFF))
             assert bool(x >> 31) == rem_plain[key]
+
+
+@pytest.mark.parametrize("B", [4, 8, 64, 256])
+def test_grouped_leaf_pushes_equal_single_pushes(B):
+    """nbody_sym.hip push_leaves: four aligned leaves summed as ((l0 + l1) + (l2 + l3)) and
+    pushed as one level-2 sub-tree give the bits of four level-0 pushes (and of the full
+    tree), so grouping the node reduce's leaves by four changes only the work."""
+    rng = np.random.default_rng(100 + B)
+    leaves = (rng.standard_normal((B, 500)) * np.exp(rng.uniform(-15, 15, (B, 1)))).astype(
+        np.float32)
+    single = _counter_merge([(0, l) for l in leaves])
+    grouped = _counter_merge([(2, (leaves[i] + leaves[i + 1]) + (leaves[i + 2] + leaves[i + 3]))
+                              for i in range(0, B, 4)])
+    assert np.array_equal(single.view(np.uint32), grouped.view(np.uint32))
+    assert np.array_equal(single.view(np.uint32), _tree(list(leaves)).view(np.uint32))
+
+
+@pytest.mark.parametrize("n_pad", [16384, 65536, 262144, 1 << 20, 1 << 24])
+def test_split_geometry_matches_native(n_pad):
+    """Split segments per row and their parts: native == the Python mirror."""
+    lib = _native.cpu_lib()
+    assert (lib.gs_sym_split_segments(n_pad), lib.gs_sym_split_parts(n_pad)) == \
+        partition.sym_split(n_pad)
