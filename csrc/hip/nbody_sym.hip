@@ -33,10 +33,12 @@ namespace {
 //         (8 waves, I 4, J 4) measured 7 % slower: the per-step j overhead is amortised over
 //         fewer i (profiles/r1_sym_ab.jsonl). I 16 (2 waves) would halve that overhead but
 //         needs 256 VGPRs + 94 AGPRs and spills to scratch (131 VGPRs at I 8).
-//   fp64: (8 waves, I 4, J 1): 14 VGPRs per i-body leave no room for I 8. At 4 waves/SIMD
-//         (2 workgroups of 8 waves) with a few spills it beats 2 waves/SIMD at 130 VGPRs:
-//         512K fp64 124.7 -> 119.6 ms (profiles/r1_sym_ab.jsonl); fp32 gains nothing from an
-//         occupancy floor (170.8 vs 170.1 ms).
+//   fp64: (4 waves, I 8, J 1): 197 VGPRs, 2 waves/SIMD. The carriers' per-step cost (3 x
+//         (2 v_mov_b32_dpp + v_add_f64)) and the LDS reads are shared by 8 i-bodies instead
+//         of 4: 22.1 instead of 23.25 f64-pipe instructions per pair, 512K 96.8 vs 100.6 ms,
+//         4M / 8 per rank 765.7 vs 796-798 ms against round 1-3's (8 waves, I 4) at 4 waves/SIMD
+//         (profiles/r4s2_fp64_i8_ab.jsonl); that shape had beaten I 4 at 2 waves/SIMD (512K
+//         124.7 -> 119.6 ms, profiles/r1_sym_ab.jsonl).
 template <typename T>
 struct Shape;
 template <>
@@ -45,7 +47,7 @@ struct Shape<float> {
 };
 template <>
 struct Shape<double> {
-  static constexpr int W = 8, I = 4, J = 1;
+  static constexpr int W = 4, I = 8, J = 1;
 };
 
 template <typename T>
@@ -456,7 +458,7 @@ __global__ __launch_bounds__(Geo<float>::kThreads) void force_sym_kernel_f32(Sym
   force_sym_entry<float, EXACT, DEFER, DYN>(a);
 }
 template <bool EXACT, bool DEFER = false, bool DYN = false>
-__global__ __launch_bounds__(Geo<double>::kThreads) __attribute__((amdgpu_waves_per_eu(4)))
+__global__ __launch_bounds__(Geo<double>::kThreads)
 void force_sym_kernel_f64(SymArgs a) {
   force_sym_entry<double, EXACT, DEFER, DYN>(a);
 }

@@ -124,7 +124,8 @@ struct gs_stepper {
   // units per workgroup after the first wave, and the first wave's size (resident slots).
   // 2 (round 3): the shortest-lived dynamic workgroups shorten the launch tail; against 4:
   // 1M / 8 per rank -1.0 %, P = 4 -0.4 %, 1M one GPU -0.2 %, 65K -1.4 %, same bits
-  // (profiles/r3s2_dyn_cap_ab.jsonl). fp64 keeps 4 (its 8-wave workgroups measured no gain).
+  // (profiles/r3s2_dyn_cap_ab.jsonl). fp64 keeps 4 (no gain from 2 with its round-3 8-wave
+  // workgroups, nor with the 4-wave I 8 tile: profiles/r4s2_fp64_i8_dyncap_ab.jsonl).
   int dyn_cap = 2;
   int sym_first_wave = 0;
   int64_t utrace_main = 0;               // entries of the main launch (deferred ones follow)
