@@ -195,6 +195,8 @@ def test_device_memory_ledger(hip):
         slots = n_pad * 3 * 4
         assert m["sym_Pi"] == slots * g["S"] and m["sym_Pj"] == slots * g["H"]
         assert m["sym_Pd"] == slots * g["D"]
+        kr, np_ = partition.sym_split(n_pad)  # split segments: parts 1 .. Np-1 in Px
+        assert m.get("sym_Px", 0) == slots * kr * (np_ - 1)
         assert m["sym_S"] == len(partition.sym_nodes(n_pad, 1)[0]) * 3 * n_pad * 4
         assert "sym_R" not in m and "partial" not in m  # one rank: R is S; no split slots
         assert all(v > 0 for v in m.values())
