@@ -1,0 +1,136 @@
+// Probe: can a hipGraph carry an *external* event record node that another stream waits on
+// while the rest of the graph is still running? (HIP: hipEventRecordWithFlags(...,
+// hipEventRecordExternal) during stream capture.) If yes, the segmented multi-rank plan
+// (stepper_plan.hip) could keep its event records inside graph segments instead of cutting a
+// segment at every record.
+//
+// Per iteration: graph on s1 = [A: counter += 1, stamp] -> record E (external) -> [B: spin
+// ~spin_us, stamp]; then, issued after the graph launch, s2 waits E and runs C (reads the
+// counter, stamps). Checks: C saw this iteration's increment (the wait did not refer to an older
+// record), and C started before B ended (the wait released at the record, not at the graph's
+// end). Output: one JSON line per iteration and a verdict line.
+//
+// Result on MI355X / ROCm 7: "correct and early" here, with the host running ahead too (async
+// pass). Inside the stepper's plan, however (records after memset / kernel nodes, several
+// events per segment), HIP logged "hipEventRecord add external event node failed" and the next
+// launch returned hipErrorInvalidValue, so the plan still cuts a segment at every record
+// (docs/DESIGN.md §11). Build: hipcc -O2 --offload-arch=gfx950 graph_event_probe.hip.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+
+#define CHECK(x)                                                              \
+  do {                                                                        \
+    hipError_t e_ = (x);                                                      \
+    if (e_ != hipSuccess) {                                                   \
+      fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e_));                 \
+      exit(1);                                                                \
+    }                                                                         \
+  } while (0)
+
+__global__ void kern_a(unsigned* counter, unsigned long long* stamp) {
+  if (threadIdx.x == 0) {
+    counter[0] += 1u;
+    stamp[0] = __builtin_amdgcn_s_memrealtime();
+    __threadfence_system();
+  }
+}
+
+// Spins for `ticks` of the 100 MHz realtime clock (one workgroup: the GPU stays free for C).
+__global__ void kern_b(unsigned long long ticks, unsigned long long* stamp) {
+  if (threadIdx.x == 0) {
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
+    stamp[1] = __builtin_amdgcn_s_memrealtime();
+  }
+}
+
+__global__ void kern_c(const unsigned* counter, unsigned* seen, unsigned long long* stamp, int it) {
+  if (threadIdx.x == 0) {
+    stamp[2 + it] = __builtin_amdgcn_s_memrealtime();
+    seen[it] = counter[0];
+  }
+}
+
+int main(int argc, char** argv) {
+  const int iters = argc > 1 ? atoi(argv[1]) : 6;
+  const unsigned long long spin_ticks = 100ull * (argc > 2 ? atoi(argv[2]) : 20000);  // us
+  hipStream_t s1, s2;
+  CHECK(hipStreamCreateWithFlags(&s1, hipStreamNonBlocking));
+  CHECK(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
+  hipEvent_t e;
+  CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  unsigned *counter, *seen;
+  unsigned long long *stamp_a, *stamp_c;
+  CHECK(hipMalloc(&counter, sizeof(unsigned)));
+  CHECK(hipMalloc(&seen, 64 * sizeof(unsigned)));
+  CHECK(hipMalloc(&stamp_a, 2 * 64 * sizeof(unsigned long long)));
+  CHECK(hipMalloc(&stamp_c, 80 * sizeof(unsigned long long)));
+  CHECK(hipMemset(counter, 0, sizeof(unsigned)));
+  CHECK(hipMemset(seen, 0, 64 * sizeof(unsigned)));
+  CHECK(hipDeviceSynchronize());
+
+  hipGraph_t g;
+  hipGraphExec_t x;
+  CHECK(hipStreamBeginCapture(s1, hipStreamCaptureModeThreadLocal));
+  hipLaunchKernelGGL(kern_a, dim3(1), dim3(64), 0, s1, counter, stamp_a);
+  CHECK(hipEventRecordWithFlags(e, s1, hipEventRecordExternal));
+  {
+    // does the capture-time record leave a sticky error behind for hipGetLastError?
+    const hipError_t le = hipGetLastError();
+    printf("{\"last_error_after_external_record\": \"%s\"}\n", hipGetErrorName(le));
+  }
+  hipLaunchKernelGGL(kern_b, dim3(1), dim3(64), 0, s1, spin_ticks, stamp_a);
+  CHECK(hipStreamEndCapture(s1, &g));
+  CHECK(hipGraphInstantiate(&x, g, nullptr, nullptr, 0));
+
+  // async pass first: every launch, wait and C issued back to back, one sync at the end (the
+  // way the plan runs ahead of the GPU): each C must still see its own iteration's increment
+  const int n_async = iters < 32 ? iters : 32;
+  for (int it = 0; it < n_async; ++it) {
+    CHECK(hipGraphLaunch(x, s1));
+    CHECK(hipStreamWaitEvent(s2, e, 0));
+    hipLaunchKernelGGL(kern_c, dim3(1), dim3(64), 0, s2, counter, seen, stamp_c, it);
+  }
+  CHECK(hipDeviceSynchronize());
+  int bad_async = 0;
+  {
+    unsigned v[32];
+    CHECK(hipMemcpy(v, seen, n_async * sizeof(unsigned), hipMemcpyDeviceToHost));
+    for (int it = 0; it < n_async; ++it) bad_async += v[it] != (unsigned)(it + 1);
+    printf("{\"async_iters\": %d, \"async_wrong\": %d, \"first\": %u, \"last\": %u}\n",
+           n_async, bad_async, v[0], v[n_async - 1]);
+  }
+  CHECK(hipMemset(counter, 0, sizeof(unsigned)));
+  CHECK(hipMemset(seen, 0, 64 * sizeof(unsigned)));
+  CHECK(hipDeviceSynchronize());
+
+  int bad_value = bad_async, waited_for_end = 0;
+  for (int it = 0; it < iters && it < 64; ++it) {
+    CHECK(hipGraphLaunch(x, s1));
+    CHECK(hipStreamWaitEvent(s2, e, 0));
+    hipLaunchKernelGGL(kern_c, dim3(1), dim3(64), 0, s2, counter, seen, stamp_c, it);
+    CHECK(hipStreamSynchronize(s2));
+    CHECK(hipStreamSynchronize(s1));
+    unsigned v = 0;
+    unsigned long long sa[2], sc = 0;
+    CHECK(hipMemcpy(&v, seen + it, sizeof(v), hipMemcpyDeviceToHost));
+    CHECK(hipMemcpy(sa, stamp_a, sizeof(sa), hipMemcpyDeviceToHost));
+    CHECK(hipMemcpy(&sc, stamp_c + 2 + it, sizeof(sc), hipMemcpyDeviceToHost));
+    const bool ok_value = v == (unsigned)(it + 1);
+    const bool before_end = sc < sa[1];
+    bad_value += !ok_value;
+    waited_for_end += !before_end;
+    printf("{\"iter\": %d, \"seen\": %u, \"expect\": %d, \"c_after_a_us\": %.1f, "
+           "\"b_end_after_c_us\": %.1f}\n",
+           it, v, it + 1, (double)((long long)(sc - sa[0])) / 100.0,
+           (double)((long long)(sa[1] - sc)) / 100.0);
+  }
+  printf("{\"verdict\": \"%s\", \"stale_waits\": %d, \"waits_released_at_graph_end\": %d}\n",
+         bad_value ? "stale" : waited_for_end ? "correct but serial" : "correct and early",
+         bad_value, waited_for_end);
+  CHECK(hipGraphExecDestroy(x));
+  CHECK(hipGraphDestroy(g));
+  return bad_value ? 2 : 0;
+}

@@ -214,6 +214,7 @@ def test_bench_two_ranks_gated_audit_failure_is_reported(hip):
                      "--exact-steps", "0", "--phase-steps", "0", "--check-samples", "0",
                      "--no-energy"],
                     {"GRAVSIM_RCCL_RANK_HOSTS": "1", "GRAVSIM_TEST_FAIL_GATED_AUDIT": "1"})
+    assert out.get("status") != "error", (out.get("error"), out.get("stage"))
     c = out["config"]
     if c["overlap_check"] and "overlap 0" in c["overlap_check"] and c["overlap_fallback"] is None:
         assert r.returncode == 0, r.stderr[-3000:]
