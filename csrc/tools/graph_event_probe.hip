@@ -14,7 +14,10 @@
 // pass). Inside the stepper's plan, however (records after memset / kernel nodes, several
 // events per segment), HIP logged "hipEventRecord add external event node failed" and the next
 // launch returned hipErrorInvalidValue, so the plan still cuts a segment at every record
-// (docs/DESIGN.md §11). Build: hipcc -O2 --offload-arch=gfx950 graph_event_probe.hip.
+// (docs/DESIGN.md §11). The last block checks the obvious suspects (the same event recorded twice
+// in one capture, in a second live graph, right after a memset node, after an eager record):
+// all succeed here, so the stepper's failing pattern is not one of them.
+// Build: hipcc -O2 --offload-arch=gfx950 graph_event_probe.hip.
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -130,6 +133,45 @@ int main(int argc, char** argv) {
   printf("{\"verdict\": \"%s\", \"stale_waits\": %d, \"waits_released_at_graph_end\": %d}\n",
          bad_value ? "stale" : waited_for_end ? "correct but serial" : "correct and early",
          bad_value, waited_for_end);
+  // Two external records of the SAME event: a second node in one capture, and a second graph.
+  {
+    hipGraph_t g2;
+    (void)hipGetLastError();
+    CHECK(hipStreamBeginCapture(s1, hipStreamCaptureModeThreadLocal));
+    hipLaunchKernelGGL(kern_a, dim3(1), dim3(64), 0, s1, counter, stamp_a);
+    hipError_t r1 = hipEventRecordWithFlags(e, s1, hipEventRecordExternal);
+    hipError_t l1 = hipGetLastError();
+    hipLaunchKernelGGL(kern_a, dim3(1), dim3(64), 0, s1, counter, stamp_a);
+    hipError_t r2 = hipEventRecordWithFlags(e, s1, hipEventRecordExternal);
+    hipError_t l2 = hipGetLastError();
+    CHECK(hipStreamEndCapture(s1, &g2));
+    printf("{\"same_event_twice_in_one_capture\": [\"%s\", \"%s\", \"%s\", \"%s\"]}\n",
+           hipGetErrorName(r1), hipGetErrorName(l1), hipGetErrorName(r2), hipGetErrorName(l2));
+    (void)hipGraphDestroy(g2);
+    // the first graph g (with its record of e) is still alive: record e in a new capture
+    hipGraph_t g3;
+    CHECK(hipStreamBeginCapture(s1, hipStreamCaptureModeThreadLocal));
+    hipLaunchKernelGGL(kern_a, dim3(1), dim3(64), 0, s1, counter, stamp_a);
+    hipError_t r3 = hipEventRecordWithFlags(e, s1, hipEventRecordExternal);
+    hipError_t l3 = hipGetLastError();
+    CHECK(hipStreamEndCapture(s1, &g3));
+    printf("{\"same_event_in_a_second_graph\": [\"%s\", \"%s\"]}\n", hipGetErrorName(r3),
+           hipGetErrorName(l3));
+    (void)hipGraphDestroy(g3);
+    // a record right after a memset node, and with the event also recorded eagerly before
+    hipEvent_t e2;
+    CHECK(hipEventCreateWithFlags(&e2, hipEventDisableTiming));
+    CHECK(hipEventRecord(e2, s2));
+    hipGraph_t g4;
+    CHECK(hipStreamBeginCapture(s1, hipStreamCaptureModeThreadLocal));
+    CHECK(hipMemsetAsync(counter, 0, 4, s1));
+    hipError_t r4 = hipEventRecordWithFlags(e2, s1, hipEventRecordExternal);
+    hipError_t l4 = hipGetLastError();
+    CHECK(hipStreamEndCapture(s1, &g4));
+    printf("{\"after_memset_node_eagerly_recorded_event\": [\"%s\", \"%s\"]}\n",
+           hipGetErrorName(r4), hipGetErrorName(l4));
+    (void)hipGraphDestroy(g4);
+  }
   CHECK(hipGraphExecDestroy(x));
   CHECK(hipGraphDestroy(g));
   return bad_value ? 2 : 0;
