@@ -64,15 +64,16 @@ def test_sym_1m_step_path_accel_sampled(hip):
 
 
 def test_sym_1m_bands_bitwise(hip, monkeypatch):
-    """N = 1M (NC = 512 rows, 12.02 MiB of partial slots per row) in 4 bands of 128 rows (the
-    multi-band path the 16M / 8-rank config runs with 4 bands of 256 rows) and in 6 uneven
-    bands (5 x 100 + 12) gives the same bits as one band, over 2 steps; so does a
-    2-virtual-rank run with 2 bands per rank."""
+    """N = 1M (NC = 512 rows, 13.15 MiB of partial slots per row: S + (Np - 1) Kr + H + D =
+    256 + 48 + 256 + 1 slots) in bands of 116 and of 92 rows (multi-band, the last band short)
+    gives the same bits as one band, over 2 steps; so do a 2-virtual-rank run with 2 bands per
+    rank and an 8-virtual-rank run (the headline decomposition: 32 of the 256 row blocks per
+    rank, the quarter split parts at the end of every rank's launch)."""
     from gravsim.runtime.engines import VirtualGroup
 
     cfg = SimConfig(n=N1M, dtype="fp32", device="gpu", mode="sym")
     out = []
-    for P, band_mb in ((1, None), (1, "1540"), (1, "1210"), (2, "1540")):
+    for P, band_mb in ((1, None), (1, "1540"), (1, "1210"), (2, "1540"), (8, None)):
         if band_mb:
             monkeypatch.setenv("GRAVSIM_SYM_BAND_MB", band_mb)
         else:
