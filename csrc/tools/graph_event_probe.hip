@@ -14,9 +14,12 @@
 // pass). Inside the stepper's plan, however (records after memset / kernel nodes, several
 // events per segment), HIP logged "hipEventRecord add external event node failed" and the next
 // launch returned hipErrorInvalidValue, so the plan still cuts a segment at every record
-// (docs/DESIGN.md §11). The last block checks the obvious suspects (the same event recorded twice
-// in one capture, in a second live graph, right after a memset node, after an eager record):
-// all succeed here, so the stepper's failing pattern is not one of them.
+// (docs/DESIGN.md §11). In the stepper the first external record of a plan (ev_stage[0], right
+// after the node-reduce kernel node, one dependency) returns hipErrorInvalidValue. The last
+// block checks the obvious suspects (the same event recorded twice in one capture or in a
+// second live graph, after a memset node, after an eager record on the same stream, while that
+// record is still pending and waited on, a 2-D grid kernel node, a priority stream, a timing
+// event): all succeed here, so the stepper's failing pattern is none of them.
 // Build: hipcc -O2 --offload-arch=gfx950 graph_event_probe.hip.
 #include <hip/hip_runtime.h>
 
@@ -171,6 +174,72 @@ int main(int argc, char** argv) {
     printf("{\"after_memset_node_eagerly_recorded_event\": [\"%s\", \"%s\"]}\n",
            hipGetErrorName(r4), hipGetErrorName(l4));
     (void)hipGraphDestroy(g4);
+    // an event recorded eagerly on the capturing stream itself and waited on by s2 first
+    hipEvent_t e3;
+    CHECK(hipEventCreateWithFlags(&e3, hipEventDisableTiming));
+    hipLaunchKernelGGL(kern_a, dim3(1), dim3(64), 0, s1, counter, stamp_a);
+    CHECK(hipEventRecord(e3, s1));
+    CHECK(hipStreamWaitEvent(s2, e3, 0));
+    CHECK(hipDeviceSynchronize());
+    hipGraph_t g5;
+    CHECK(hipStreamBeginCapture(s1, hipStreamCaptureModeThreadLocal));
+    hipLaunchKernelGGL(kern_a, dim3(1), dim3(64), 0, s1, counter, stamp_a);
+    hipError_t r5 = hipEventRecordWithFlags(e3, s1, hipEventRecordExternal);
+    hipError_t l5 = hipGetLastError();
+    CHECK(hipStreamEndCapture(s1, &g5));
+    printf("{\"after_eager_record_on_same_stream\": [\"%s\", \"%s\"]}\n", hipGetErrorName(r5),
+           hipGetErrorName(l5));
+    (void)hipGraphDestroy(g5);
+    // a 2-D grid kernel node before the record
+    hipGraph_t g6;
+    CHECK(hipStreamBeginCapture(s1, hipStreamCaptureModeThreadLocal));
+    hipLaunchKernelGGL(kern_a, dim3(4, 3), dim3(256), 0, s1, counter, stamp_a);
+    hipError_t r6 = hipEventRecordWithFlags(e2, s1, hipEventRecordExternal);
+    hipError_t l6 = hipGetLastError();
+    CHECK(hipStreamEndCapture(s1, &g6));
+    printf("{\"after_2d_grid_kernel\": [\"%s\", \"%s\"]}\n", hipGetErrorName(r6),
+           hipGetErrorName(l6));
+    (void)hipGraphDestroy(g6);
+    // non-blocking stream created with a priority (as the stepper's compute stream)
+    hipStream_t sp;
+    int lo = 0, hi = 0;
+    CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+    CHECK(hipStreamCreateWithPriority(&sp, hipStreamNonBlocking, hi));
+    hipGraph_t g7;
+    CHECK(hipStreamBeginCapture(sp, hipStreamCaptureModeThreadLocal));
+    hipLaunchKernelGGL(kern_a, dim3(1), dim3(64), 0, sp, counter, stamp_a);
+    hipError_t r7 = hipEventRecordWithFlags(e2, sp, hipEventRecordExternal);
+    hipError_t l7 = hipGetLastError();
+    CHECK(hipStreamEndCapture(sp, &g7));
+    printf("{\"priority_stream\": [\"%s\", \"%s\"]}\n", hipGetErrorName(r7), hipGetErrorName(l7));
+    (void)hipGraphDestroy(g7);
+    // the event's eager record is still pending (behind a 20 ms spin on s1) and s2 waits on it
+    hipEvent_t e4;
+    CHECK(hipEventCreateWithFlags(&e4, hipEventDisableTiming));
+    hipLaunchKernelGGL(kern_b, dim3(1), dim3(64), 0, s1, 2000000ull, stamp_a);
+    CHECK(hipEventRecord(e4, s1));
+    CHECK(hipStreamWaitEvent(s2, e4, 0));
+    hipGraph_t g8;
+    CHECK(hipStreamBeginCapture(s1, hipStreamCaptureModeThreadLocal));
+    hipLaunchKernelGGL(kern_a, dim3(1), dim3(64), 0, s1, counter, stamp_a);
+    hipError_t r8 = hipEventRecordWithFlags(e4, s1, hipEventRecordExternal);
+    hipError_t l8 = hipGetLastError();
+    CHECK(hipStreamEndCapture(s1, &g8));
+    printf("{\"while_eager_record_pending\": [\"%s\", \"%s\"]}\n", hipGetErrorName(r8),
+           hipGetErrorName(l8));
+    (void)hipGraphDestroy(g8);
+    CHECK(hipDeviceSynchronize());
+    // event created with default flags (timing enabled)
+    hipEvent_t e5;
+    CHECK(hipEventCreate(&e5));
+    hipGraph_t g9;
+    CHECK(hipStreamBeginCapture(s1, hipStreamCaptureModeThreadLocal));
+    hipLaunchKernelGGL(kern_a, dim3(1), dim3(64), 0, s1, counter, stamp_a);
+    hipError_t r9 = hipEventRecordWithFlags(e5, s1, hipEventRecordExternal);
+    hipError_t l9 = hipGetLastError();
+    CHECK(hipStreamEndCapture(s1, &g9));
+    printf("{\"timing_event\": [\"%s\", \"%s\"]}\n", hipGetErrorName(r9), hipGetErrorName(l9));
+    (void)hipGraphDestroy(g9);
   }
   CHECK(hipGraphExecDestroy(x));
   CHECK(hipGraphDestroy(g));
