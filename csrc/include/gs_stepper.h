@@ -122,11 +122,13 @@ struct gs_stepper {
   unsigned long long* utrace = nullptr;  // GRAVSIM_UNIT_TRACE: per force workgroup timeline
   // Dynamic unit fetch of the sym force launch (gs_stepper_set_schedule; <= 1: static units):
   // units per workgroup after the first wave, and the first wave's size (resident slots).
-  // 2 (round 3): the shortest-lived dynamic workgroups shorten the launch tail; against 4:
-  // 1M / 8 per rank -1.0 %, P = 4 -0.4 %, 1M one GPU -0.2 %, 65K -1.4 %, same bits
-  // (profiles/r3s2_dyn_cap_ab.jsonl). fp64 keeps 4 (no gain from 2 with its round-3 8-wave
-  // workgroups, nor with the 4-wave I 8 tile: profiles/r4s2_fp64_i8_dyncap_ab.jsonl).
-  int dyn_cap = 2;
+  // Round 3 took 2 (shorter-lived workgroups shorten the launch tail; against 4: 1M / 8 per
+  // rank -1.0 %, 1M one GPU -0.2 %, 65K -1.4 %, profiles/r3s2_dyn_cap_ab.jsonl). With the
+  // final units in quarter parts (round 4) the tail no longer needs that: 3 against 2, paired
+  // per round, 1M one GPU -0.14 % (4 of 4 rounds), 65K -0.5 %, 1M / 8 per rank even
+  // (profiles/r4s2_dyn_cap_quarter_parts_ab.jsonl). Same units and slots: same bits. fp64
+  // keeps 4 (no gain from 2: profiles/r4s2_fp64_i8_dyncap_ab.jsonl).
+  int dyn_cap = 3;
   int sym_first_wave = 0;
   int64_t utrace_main = 0;               // entries of the main launch (deferred ones follow)
   size_t emu_cap = 0;
