@@ -454,9 +454,10 @@ def run(a, g) -> int:
         phase = None
         if a.phase_steps > 0:
             g.stage("phase", budget(a.phase_steps + 2))
-            if world > 1 and a.graph:
-                # whole plan periods (the state reads above gathered the current buffer), so
-                # the phase events come from the segmented plan the timed loop replayed
+            if a.graph:
+                # whole periods (the state reads above gathered the current buffer), so the
+                # phase events come from the schedule the timed loop replayed: the step graph
+                # (one rank) or the segmented plan
                 eng.align_period()
             eng.set_timing(True)
             eng.step(a.phase_steps)

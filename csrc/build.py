@@ -4,9 +4,14 @@
   libgravsim_hip.so : hipcc --offload-arch=gfx950, kernels + Stepper runtime, links RCCL.
   gravsim_bench     : standalone C++ driver (csrc/tools/gravsim_main.cpp), no Python needed.
 
+  probes (--tools)  : microbench, sym_probe, trans_probe, graph_event_probe (csrc/tools/*.hip);
+                      measurement instruments, never part of the production build: a broken
+                      probe cannot fail build_all() (the driver's build check).
+
 Outputs land in <package>/_native/ so they travel with the repo snapshot to the GPU box.
 Rebuilds only when a source or header is newer than the target. Usage:
-    python csrc/build.py [--force] [--only cpu|hip|tool]
+    python csrc/build.py [--force] [--only cpu|hip|tool|microbench|sym_probe|trans_probe|
+                          graph_event_probe] [--tools]
 """
 from __future__ import annotations
 
@@ -43,6 +48,8 @@ PROBE_SRC = CSRC / "tools" / "sym_probe.hip"
 PROBE_BIN = OUT / "sym_probe"
 TRANS_SRC = CSRC / "tools" / "trans_probe.hip"
 TRANS_BIN = OUT / "trans_probe"
+GEV_SRC = CSRC / "tools" / "graph_event_probe.hip"
+GEV_BIN = OUT / "graph_event_probe"
 
 
 def _stale(target: Path, deps: list[Path]) -> bool:
@@ -94,12 +101,43 @@ if os.environ.get("GRAVSIM_SLP", "1") == "0":
 HIP_FLAGS += os.environ.get("GRAVSIM_HIP_EXTRA", "").split()
 
 
+OBJ = OUT / "obj"
+
+
+def _objects(force: bool) -> list[Path]:
+    """One object per HIP source (the same PIC objects go into the library and the tool),
+    compiled in parallel: each translation unit is independent (no device code crosses them),
+    and nbody_sym.hip alone takes most of a serial build."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    OBJ.mkdir(parents=True, exist_ok=True)
+    objs = [OBJ / (src.stem + ("_c" if src.suffix == ".cpp" else "") + ".o") for src in HIP_SRC]
+    todo = [(src, o) for src, o in zip(HIP_SRC, objs) if force or _stale(o, [src, *HEADERS])]
+
+    def one(job):
+        src, o = job
+        tmp = o.with_suffix(".o.tmp")
+        cmd = [hipcc(), *HIP_FLAGS, "-c", f"-I{CSRC / 'include'}", str(src), "-o", str(tmp)]
+        print("+", " ".join(cmd), flush=True)
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode:
+            sys.stderr.write(r.stdout + r.stderr)
+            raise subprocess.CalledProcessError(r.returncode, cmd)
+        os.replace(tmp, o)
+
+    jobs = int(os.environ.get("GRAVSIM_BUILD_JOBS", "0") or 0) or min(8, os.cpu_count() or 1)
+    with ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
+        list(ex.map(one, todo))
+    return objs
+
+
 def build_hip(force: bool = False) -> Path:
     OUT.mkdir(parents=True, exist_ok=True)
     if force or _stale(HIP_LIB, HIP_SRC + HEADERS):
+        objs = _objects(force)
         tmp = HIP_LIB.with_suffix(".so.tmp")
-        _run([hipcc(), *HIP_FLAGS, "-shared", f"-I{CSRC / 'include'}", *map(str, HIP_SRC),
-              f"-L{ROCM / 'lib'}", "-lrccl", "-o", str(tmp)])
+        _run([hipcc(), *HIP_FLAGS, "-shared", *map(str, objs), f"-L{ROCM / 'lib'}", "-lrccl",
+              "-o", str(tmp)])
         os.replace(tmp, HIP_LIB)
     return HIP_LIB
 
@@ -108,9 +146,12 @@ def build_tool(force: bool = False) -> Path:
     OUT.mkdir(parents=True, exist_ok=True)
     deps = TOOL_SRC + HIP_SRC + HEADERS
     if all(p.exists() for p in TOOL_SRC) and (force or _stale(TOOL_BIN, deps)):
+        objs = _objects(force)
+        main_o = OBJ / "gravsim_main.o"  # (compiled apart: hipcc's -x hip would take the
+        _run([hipcc(), *HIP_FLAGS, "-c", f"-I{CSRC / 'include'}", *map(str, TOOL_SRC),  # .o
+              "-o", str(main_o)])                                            # as sources)
         tmp = TOOL_BIN.with_suffix(".tmp")
-        _run([hipcc(), *HIP_FLAGS, f"-I{CSRC / 'include'}", *map(str, TOOL_SRC),
-              *map(str, HIP_SRC), f"-L{ROCM / 'lib'}", "-lrccl",
+        _run([hipcc(), *HIP_FLAGS, str(main_o), *map(str, objs), f"-L{ROCM / 'lib'}", "-lrccl",
               f"-Wl,-rpath,{ROCM / 'lib'}", "-o", str(tmp)])
         os.replace(tmp, TOOL_BIN)
     return TOOL_BIN
@@ -149,20 +190,38 @@ def build_trans_probe(force: bool = False) -> Path:
     return TRANS_BIN
 
 
+def build_graph_event_probe(force: bool = False) -> Path:
+    """External event-record / wait graph-node probe (csrc/tools/graph_event_probe.hip)."""
+    OUT.mkdir(parents=True, exist_ok=True)
+    if GEV_SRC.exists() and (force or _stale(GEV_BIN, [GEV_SRC])):
+        tmp = GEV_BIN.with_suffix(".tmp")
+        _run([hipcc(), "-O2", "-std=c++17", f"--offload-arch={ARCH}", str(GEV_SRC), "-o",
+              str(tmp)])
+        os.replace(tmp, GEV_BIN)
+    return GEV_BIN
+
+
 def build_all(force: bool = False) -> None:
+    """The production artefacts only: the CPU engine, the HIP library and gravsim_bench."""
     build_cpu(force)
     build_hip(force)
     build_tool(force)
+
+
+def build_tools(force: bool = False) -> None:
+    """The measurement probes (opt-in: --tools or --only <probe>)."""
     build_microbench(force)
     build_sym_probe(force)
     build_trans_probe(force)
+    build_graph_event_probe(force)
 
 
 def main(argv: list[str] | None = None) -> int:
     ap = argparse.ArgumentParser(description=__doc__)
     ap.add_argument("--force", action="store_true")
     ap.add_argument("--only", choices=["cpu", "hip", "tool", "microbench", "sym_probe",
-                                          "trans_probe"])
+                                          "trans_probe", "graph_event_probe"])
+    ap.add_argument("--tools", action="store_true", help="also build the measurement probes")
     a = ap.parse_args(argv)
     if a.only == "cpu":
         build_cpu(a.force)
@@ -176,8 +235,12 @@ def main(argv: list[str] | None = None) -> int:
         build_sym_probe(a.force)
     elif a.only == "trans_probe":
         build_trans_probe(a.force)
+    elif a.only == "graph_event_probe":
+        build_graph_event_probe(a.force)
     else:
         build_all(a.force)
+        if a.tools:
+            build_tools(a.force)
     return 0
 
 

@@ -257,12 +257,21 @@ static int32_t sym_local_segs(int32_t A, int32_t NC, int32_t a0, int32_t rows, i
   return n < S ? n : S;
 }
 
+// Unit-map entry (gs_common.h sym_unit_entry): row in bits 12-27 (rows < 65536), unit in bits
+// 0-11 (S + D < 4096; S is ~128-256 at every size), bit 31 remote, bit 30 a part unit with its
+// part in bits 28-29 (all-gather order) or the ring stage in bits 28-30 (ring order). (Round 4
+// kept the row in bits 16-27 next to a 16-bit unit field: rows < 4096, so a 16M run on 2 ranks,
+// 4096 rows each, got no map and silently ran ungated.)
+static inline int32_t unit_entry(uint32_t flags, int32_t row, int32_t unit) {
+  return (int32_t)(flags | ((uint32_t)row << gs::kUnitRowShift) | (uint32_t)unit);
+}
+
 // The gated sym launch's unit order (units 6, gs_kernels.h) for rank `rank` of `nranks`, one
-// band: entry = row << 16 | unit (unit < S: shell segment, >= S: diagonal part), bit 31 set
+// band: entry = row, unit (unit < S: shell segment, >= S: diagonal part), bit 31 set
 // for a remote unit (a j-chunk outside the rank's rows). The first `fill` entries (all local
 // units when fill < 0) are rank-local ones, row by row (diagonal parts, then local
 // segments); the rest follow the ungated order: shell segments row by row, then the diagonal
-// parts. Returns the entry count (rows * (S + D)), 0 if the 16-bit fields cannot hold the
+// parts. Returns the entry count (rows * (S + D)), 0 if the entry fields cannot hold the
 // geometry, -1 on error (cap too small, bad arguments).
 extern "C" int64_t gs_sym_unit_map(int64_t n_pad, int32_t rank, int32_t nranks, int64_t fill,
                                    int32_t* out, int64_t cap) {
@@ -272,7 +281,7 @@ extern "C" int64_t gs_sym_unit_map(int64_t n_pad, int32_t rank, int32_t nranks, 
 // The same order with the last kr shell segments of every row split into np parts
 // (gs_kernels.h SymArgs::Kr, Np): they leave the order above and are appended as np part units
 // each (bit 30 set, bits 28-29 the part), row by row, so the launch ends with 1 / np-length
-// units. Rows < 4096 (12-bit field) with splits; rows * (S + D + (np - 1) kr) entries.
+// units. rows * (S + D + (np - 1) kr) entries.
 extern "C" int64_t gs_sym_unit_map_kr(int64_t n_pad, int32_t rank, int32_t nranks,
                                       int64_t fill, int32_t kr, int32_t* out, int64_t cap) {
   return gs_sym_unit_map_parts(n_pad, rank, nranks, fill, kr, 2, out, cap);
@@ -289,7 +298,7 @@ extern "C" int64_t gs_sym_unit_map_parts(int64_t n_pad, int32_t rank, int32_t nr
   if (kr > S) return -1;
   const int32_t per = S + D;
   const int64_t total = (int64_t)rows * (per + (int64_t)(np - 1) * kr);
-  if (rows >= (kr > 0 ? 4096 : 32768) || per >= 65536) return 0;
+  if (rows > gs::kUnitRowMax || per > gs::kUnitMax) return 0;
   if (!out || cap < total) return -1;
   std::vector<int32_t> nl(rows);
   std::vector<char> moved((size_t)rows * per, 0);
@@ -299,11 +308,11 @@ extern "C" int64_t gs_sym_unit_map_parts(int64_t n_pad, int32_t rank, int32_t nr
   for (int32_t r = 0; r < rows; ++r) {
     nl[r] = sym_local_segs(a0 + r, NC, a0, rows, L, S);
     for (int32_t q = 0; q < D && (fill < 0 || k < fill); ++q) {
-      out[k++] = (r << 16) | (S + q);
+      out[k++] = unit_entry(0u, r, S + q);
       moved[(size_t)r * per + S + q] = 1;
     }
     for (int32_t g = 0; g < nl[r] && g < S - kr && (fill < 0 || k < fill); ++g) {
-      out[k++] = (r << 16) | g;
+      out[k++] = unit_entry(0u, r, g);
       moved[(size_t)r * per + g] = 1;
     }
   }
@@ -312,22 +321,20 @@ extern "C" int64_t gs_sym_unit_map_parts(int64_t n_pad, int32_t rank, int32_t nr
       for (int32_t u = pass ? S : 0; u < (pass ? per : S); ++u) {
         if (moved[(size_t)r * per + u]) continue;
         const bool remote = u < S && u >= nl[r];
-        out[k++] = (int32_t)((remote ? 0x80000000u : 0u) | ((uint32_t)r << 16) | (uint32_t)u);
+        out[k++] = unit_entry(remote ? 0x80000000u : 0u, r, u);
       }
   for (int32_t r = 0; r < rows; ++r)
     for (int32_t u = S - kr; u < S; ++u)
       for (uint32_t h = 0; h < (uint32_t)np; ++h) {
         const bool remote = u >= nl[r];
-        out[k++] = (int32_t)((remote ? 0x80000000u : 0u) | 0x40000000u | (h << 28) |
-                             ((uint32_t)r << 16) | (uint32_t)u);
+        out[k++] = unit_entry((remote ? 0x80000000u : 0u) | 0x40000000u | (h << 28), r, u);
       }
   return k;
 }
 
 // The gated sym launch's unit order for the ring strategy: the slice of rank (rank - k) mod P
 // arrives at ring stage k (1 .. P-1), so a remote unit can start once the stage of the latest
-// slice it reads has landed. Entry = bit 31 remote | stage << 28 | row << 16 | unit (rows <
-// 4096). Order: the first `fill` local units as in gs_sym_unit_map, then every other unit by
+// slice it reads has landed. Entry = bit 31 remote | stage << 28 | row | unit. Order: the first `fill` local units as in gs_sym_unit_map, then every other unit by
 // stage (local ones first), row by row within a stage, shell segments before diagonal parts.
 // Returns the entry count, 0 if the fields cannot hold the geometry, -1 on error.
 extern "C" int64_t gs_sym_unit_map_ring(int64_t n_pad, int32_t rank, int32_t nranks,
@@ -338,7 +345,7 @@ extern "C" int64_t gs_sym_unit_map_ring(int64_t n_pad, int32_t rank, int32_t nra
     return -1;
   const int32_t per = S + D;
   const int64_t total = (int64_t)rows * per;
-  if (rows >= 4096 || per >= 65536 || nranks > 8) return 0;
+  if (rows > gs::kUnitRowMax || per > gs::kUnitMax || nranks > 8) return 0;
   if (!out || cap < total) return -1;
   // ring stage of every unit (0: reads only the rank's own rows)
   std::vector<int8_t> stage((size_t)total, 0);
@@ -362,11 +369,11 @@ extern "C" int64_t gs_sym_unit_map_ring(int64_t n_pad, int32_t rank, int32_t nra
   for (int32_t r = 0; r < rows; ++r) {  // the local prefix, exactly as gs_sym_unit_map
     nl[r] = sym_local_segs(a0 + r, NC, a0, rows, L, S);
     for (int32_t q = 0; q < D && (fill < 0 || k < fill); ++q) {
-      out[k++] = (r << 16) | (S + q);
+      out[k++] = unit_entry(0u, r, S + q);
       moved[(size_t)r * per + S + q] = 1;
     }
     for (int32_t g = 0; g < nl[r] && (fill < 0 || k < fill); ++g) {
-      out[k++] = (r << 16) | g;
+      out[k++] = unit_entry(0u, r, g);
       moved[(size_t)r * per + g] = 1;
     }
   }
@@ -377,7 +384,7 @@ extern "C" int64_t gs_sym_unit_map_ring(int64_t n_pad, int32_t rank, int32_t nra
           const size_t i = (size_t)r * per + u;
           if (moved[i] || stage[i] != st) continue;
           const uint32_t remote = st > 0 ? 0x80000000u : 0u;
-          out[k++] = (int32_t)(remote | ((uint32_t)st << 28) | ((uint32_t)r << 16) | (uint32_t)u);
+          out[k++] = unit_entry(remote | ((uint32_t)st << 28), r, u);
         }
   return k;
 }

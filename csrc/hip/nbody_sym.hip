@@ -215,18 +215,19 @@ __device__ __forceinline__ void run_tiles(const SymArgs& a, ISetK<T>& is, TileSe
 // rank-local shell segments, row by row) before the remote ones (row by row). Workgroups are
 // dispatched in grid order, so the gathered rows are needed only after ~the local share of
 // the step has been handed out. The order is a host-built map (one uniform load per
-// workgroup: unit -> row << 16 | segment, bit 31 = remote); a search through prefix sums put
-// a chain of dependent loads in front of every workgroup and cost 2 % of the step.
+// workgroup: unit -> row, segment, bit 31 = remote; gs_common.h kUnitRowShift); a search
+// through prefix sums put a chain of dependent loads in front of every workgroup and cost 2 %
+// of the step.
 // With the ring strategy (gate_n > 1) bits 28-30 hold the ring stage whose slice the unit
-// waits for and rows are < 4096 (layout.cpp gs_sym_unit_map_ring).
+// waits for (layout.cpp gs_sym_unit_map_ring).
 // With split segments (Kr > 0, all-gather order) bit 30 marks a part unit, bits 28-29 its
-// part, and rows are < 4096 (layout.cpp gs_sym_unit_map_parts).
+// part (layout.cpp gs_sym_unit_map_parts).
 __device__ __forceinline__ bool local_first_unit(const SymArgs& a, int b, int* br, int* s,
                                                  int* stage, int* part) {
   const uint32_t m = (uint32_t)a.lf[b];
   const bool ring = a.gate_n > 1, halves = a.Kr > 0 && !ring;
-  *br = (int)((m >> 16) & (ring || halves ? 0xfffu : 0x7fffu));
-  *s = (int)(m & 0xffffu);
+  *br = (int)((m >> kUnitRowShift) & (uint32_t)kUnitRowMax);
+  *s = (int)(m & (uint32_t)kUnitMax);
   *stage = ring ? (int)((m >> 28) & 7u) : 0;
   *part = halves && ((m >> 30) & 1u) ? (int)((m >> 28) & 3u) : -1;
   return (m >> 31) != 0u;

@@ -101,6 +101,7 @@ gs_stepper::PhaseEv* phase_begin(gs_stepper* s) {
   }
   gs_stepper::PhaseEv* p = &s->pev[s->pev_used++];
   p->g = p->w = p->x = p->j = false;
+  p->nsteps = 1;
   return p;
 }
 
@@ -816,7 +817,7 @@ int gs_stepper_create(const gs_config* cfg, gs_stepper** out) {
     const size_t units = (size_t)rows * (s->sym_S_n + s->sym_D + s->sym_kx()) + 1;
     ALLOC_CLEAN(&s->defer, units * sizeof(unsigned), "defer");
     FAIL_CLEAN(hipMemsetAsync(s->defer, 0, units * sizeof(unsigned), s->s_comp));
-    // unit -> row << 16 | segment (bit 31: remote), local units first (layout.cpp).
+    // unit -> row, segment (bit 31: remote), local units first (layout.cpp).
     const long fill = 4L * s->cus;  // two dispatch waves of 2 workgroups per CU
     std::vector<int32_t> lf(units - 1);
     s->sym_ring = cfg->strategy == GS_STRATEGY_RING && cfg->nranks > 1;
@@ -825,7 +826,7 @@ int gs_stepper_create(const gs_config* cfg, gs_stepper** out) {
                                            (int64_t)lf.size())
                     : gs_sym_unit_map_parts(s->L.n_pad, cfg->rank, cfg->nranks, fill, s->sym_Kr,
                                             s->sym_Np, lf.data(), (int64_t)lf.size());
-    lf.resize(got > 0 ? (size_t)got : 0);  // 0: geometry too large for the 16-bit fields
+    lf.resize(got > 0 ? (size_t)got : 0);  // 0: geometry too large for the entry fields
     if (!lf.empty()) {
       ALLOC_CLEAN(&s->sym_lf, lf.size() * sizeof(int32_t), "unit_map");
       FAIL_CLEAN(hipMemcpy(s->sym_lf, lf.data(), lf.size() * sizeof(int32_t),
@@ -955,8 +956,10 @@ int gs_stepper_step(gs_stepper* s, int32_t nsteps) {
   // Multi-rank runs with use_graph 1 (the default) replay a segmented plan instead: compute
   // segments as graphs, collectives eager between them (plan_ok, build_plan).
   const bool seg = plan_ok(s);
-  const bool graph_ok = seg || (s->cfg.use_graph >= (xcomm(s) ? 2 : 1) && !s->timed &&
-                                !(xcomm(s) && s->graph_failed));
+  // (timed steps replay the graph too: a one-rank period is timed as a whole, so the phase
+  // pass measures the schedule the timed loop ran; captured multi-rank steps stay eager)
+  const bool graph_ok = seg || (s->cfg.use_graph >= (xcomm(s) ? 2 : 1) &&
+                                !(xcomm(s) && (s->graph_failed || s->timed)));
   int32_t left = nsteps;
   while (left > 0) {
     const bool period_start = (s->k & 1) == 0 && (xcomm(s) ? !s->full[0] : true);
@@ -973,7 +976,16 @@ int gs_stepper_step(gs_stepper* s, int32_t nsteps) {
           s->graph_failed = true;  // eager from here on (the error text is kept for inspection)
           continue;
         }
+        gs_stepper::PhaseEv* pe = s->timed ? phase_begin(s) : nullptr;
+        if (pe) {
+          pe->nsteps = 2;
+          GS_HIP(hipEventRecord(pe->t0, s->s_comp));
+        }
         GS_HIP(hipGraphLaunch(s->graph, s->s_comp));
+        if (pe) {
+          GS_HIP(hipEventRecord(pe->end, s->s_comp));
+          s->pev_plan += 2;
+        }
       }
       s->k += 2;
       // After one period: X[1] was gathered in the second step, X[0] holds only the own slice.
@@ -1109,19 +1121,22 @@ int gs_stepper_wait(gs_stepper* s, double timeout_s) {
   return wait_until(s, s->prog_rec, timeout_s);
 }
 
-// Phase timing of the eager steps enqueued since gs_stepper_set_timing(s, 1) / the previous
-// call (at most 256), averaged per step. out[0] steps, [1] total ms, [2] all-gather ms and
-// [3] node-sum exchange ms (spans on the comm stream), [4] exposed gather ms and [5]
+// Phase timing of the steps enqueued since gs_stepper_set_timing(s, 1) / the previous call
+// (at most 256 event sets), averaged per step. out[0] steps, [1] total ms, [2] all-gather ms
+// and [3] node-sum exchange ms (spans on the comm stream), [4] exposed gather ms and [5]
 // exposed exchange ms (compute-stream stalls on them: exposed comm = [4] + [5]), [6] the
-// most force units one step deferred past the gather (overlap 3), [7] reserved (0).
+// most force units one step deferred past the gather (overlap 3), [7] how many of the steps
+// were replayed (one-rank step graph, or the multi-rank segmented plan) instead of eager.
 int gs_stepper_phase_stats(gs_stepper* s, double* out8) {
   for (int i = 0; i < 8; ++i) out8[i] = 0.0;
   for (hipStream_t st : {s->s_comm, s->s_rem, s->s_rem2, s->s_comp})
     GS_HIP(hipStreamSynchronize(st));
   s->prog_done = s->prog_rec;
-  const int n = s->pev_used;
-  for (int i = 0; i < n; ++i) {
+  const int n_ev = s->pev_used;
+  int n = 0;  // steps (a one-rank graph period's event set spans two)
+  for (int i = 0; i < n_ev; ++i) {
     const gs_stepper::PhaseEv& p = s->pev[i];
+    n += p.nsteps;
     float v = 0.f;
     GS_HIP(hipEventElapsedTime(&v, p.t0, p.end));
     out8[1] += v;
@@ -1136,7 +1151,7 @@ int gs_stepper_phase_stats(gs_stepper* s, double* out8) {
   unsigned d[2] = {0, 0};
   GS_HIP(hipMemcpy(d, s->gate_buf + 2, sizeof(d), hipMemcpyDeviceToHost));
   out8[6] = d[1];
-  out8[7] = s->pev_plan;  // of them replayed from the segmented plan (the rest eager)
+  out8[7] = s->pev_plan;  // of them replayed (graph or segmented plan; the rest eager)
   s->pev_plan = 0;
   // (on s_comp: a legacy-stream memset is not ordered against the non-blocking compute
   // stream, so the next gated launch could race it)

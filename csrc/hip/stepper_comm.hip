@@ -48,6 +48,7 @@ int gather(gs_stepper* s, int cur, bool gate) {
   if (comp_record(s, s->ev_ready)) return -1;
   s->full[cur] = true;
   return comm_do(s, [s, cur, gate]() -> int {
+    if (comm_dead(s)) return -1;
     char* buf = static_cast<char*>(s->X[cur]);
     const size_t count = (size_t)s->L.n_local * 4;
     GS_HIP(hipStreamWaitEvent(s->s_comm, s->ev_ready, 0));
@@ -100,6 +101,15 @@ bool abort_comm(gs_stepper* s) {
   return true;
 }
 
+// A communicator the watchdog thread (or a timeout / async error) aborted must not be used
+// again: have_comm stays true on the main thread until it notices, but s->comm is freed once
+// comm_live is null. Every RCCL call site checks this first.
+bool comm_dead(gs_stepper* s) {
+  if (!s->have_comm || s->emulate || s->comm_live.load() != nullptr) return false;
+  gs_set_error("RCCL communicator aborted (watchdog, timeout or async error)");
+  return true;
+}
+
 int ring_src(const gs_stepper* s, int sub) {
   const int P = s->cfg.nranks;
   return ((s->cfg.rank - sub) % P + P) % P;
@@ -117,6 +127,7 @@ void rank_chunks(const gs_stepper* s, int src, int* c0, int* c1) {
 // Enqueue the transfer of ring sub-step `sub` (1..P-1) on the comm stream: send the slice
 // received at sub-step sub-1 (own slice for sub = 1) right, receive slice ring_src(sub) left.
 int ring_xfer_rccl(gs_stepper* s, int cur, int sub) {
+  if (comm_dead(s)) return -1;
   const int P = s->cfg.nranks, r = s->cfg.rank;
   char* buf = static_cast<char*>(s->X[cur]);
   const ncclDataType_t dt = s->esz == 4 ? ncclFloat32 : ncclFloat64;
@@ -172,6 +183,7 @@ int sym_reduce_exchange(gs_stepper* s, const gs::SymArgs& a0) {
     if (comm_do(s, [s, g, kb, ke, first, last]() -> int {
           const int P = s->cfg.nranks, r = s->cfg.rank;
           const size_t e = s->esz, nl = (size_t)s->L.n_local, my = (size_t)s->nn[r];
+          if (comm_dead(s)) return -1;
           GS_HIP(hipStreamWaitEvent(s->s_comm, s->ev_stage[g], 0));
           if (first) GS_MARK(x0, x, s->s_comm);
           if (s->emulate) {
@@ -346,6 +358,10 @@ int32_t gs_stepper_abort(gs_stepper* s) { return s && abort_comm(s) ? 1 : 0; }
 
 int gs_stepper_comm_check(gs_stepper* s) {
   if (!s->have_comm) return 0;
+  if (comm_dead(s)) {  // aborted from another thread: the handle is gone
+    s->have_comm = false;
+    return -1;
+  }
   ncclResult_t async = ncclSuccess;
   GS_NCCL(ncclCommGetAsyncError(s->comm, &async));
   if (async != ncclSuccess && async != ncclInProgress) {

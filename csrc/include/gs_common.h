@@ -112,6 +112,13 @@ GS_HD int32_t sym_node_count(int32_t lo, int32_t hi) {
   return n;
 }
 
+// Unit-map entries of the gated sym launch (layout.cpp gs_sym_unit_map_*, nbody_sym.hip
+// local_first_unit): unit (segment or diagonal part) in bits 0-11, row in bits 12-27, flags
+// in bits 28-31 (31 remote; all-gather order: 30 part unit, 28-29 its part; ring: 28-30 stage).
+constexpr int kUnitRowShift = 12;
+constexpr int32_t kUnitMax = 0xfff;      // largest unit index (S + D - 1 < 4096)
+constexpr int32_t kUnitRowMax = 0xffff;  // most rows a map can hold
+
 // Threads per one-sided force-kernel workgroup (i-bodies per workgroup = kForceBlock * ipl):
 // 4 waves (profiles/r1_block_sweep.jsonl).
 constexpr int kForceBlock = 256;

@@ -104,7 +104,7 @@ struct SymArgs {
   int32_t gate_n;        // flags finalize re-arms: 1 (all-gather) or 8 (ring stages)
   unsigned* defer;
   unsigned* defer_max;
-  const int32_t* lf;    // units 6 order: unit -> row << 16 | segment (bit 31: remote unit)
+  const int32_t* lf;    // units 6 order: unit -> row, segment (bit 31: remote unit)
   int32_t defer_grid;   // units 7: workgroups walking the deferred list
   int32_t defer_index;  // (device-side) the deferred entry a units-7 workgroup is running
   // Unit timeline probe (GRAVSIM_UNIT_TRACE, diagnostics only; nullptr otherwise): per force

@@ -137,7 +137,7 @@ struct gs_stepper {
   // deferred past the gather (since the last phase_stats call). defer: count + unit list.
   unsigned* gate_buf = nullptr;
   unsigned* defer = nullptr;
-  int32_t* sym_lf = nullptr;  // units-6 order: unit -> row << 16 | segment (bit 31 remote)
+  int32_t* sym_lf = nullptr;  // units-6 order: unit -> row, segment (bit 31 remote)
   // Ring strategy of the sym schedule: P-1 neighbour stages instead of one all-gather; the
   // gated launch waits per stage (ring_gate[8 * buffer + stage], set after each stage's
   // receive) and its unit map orders the remote units by stage.
@@ -148,6 +148,7 @@ struct gs_stepper {
   struct PhaseEv {
     hipEvent_t t0, end, g0, g1, w0, w1, x0, x1, j0, j1;
     bool g, w, x, j;
+    int nsteps;  // steps t0 .. end spans: 1, or 2 for a one-rank graph period
   };
   std::vector<PhaseEv> pev;
   int pev_used = 0;
@@ -272,6 +273,8 @@ int sym_reduce_exchange(gs_stepper* s, const gs::SymArgs& a);
 void maybe_install_crash_trace();
 // ncclCommAbort once (the watchdog thread, a timeout or an async error may all ask for it).
 bool abort_comm(gs_stepper* s);
+// The communicator was aborted (comm_live null while have_comm): sets the error, true.
+bool comm_dead(gs_stepper* s);
 
 // stepper.hip: buffers, step enqueue, phase events.
 gs_stepper::PhaseEv* phase_begin(gs_stepper* s);

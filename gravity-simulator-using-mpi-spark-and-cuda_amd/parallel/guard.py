@@ -42,8 +42,13 @@ def job_dir(rank: int = 0, world: int = 1) -> str:
     if not d:
         # torchrun's ranks share their parent (the elastic agent) and MASTER_PORT; a single
         # process keys on its own pid
+        # (plus torchrun's rendezvous run id when it names the job: a directory reused by an
+        # earlier job of the same parent pid and port cannot leak its records into this one)
+        run_id = os.environ.get("TORCHELASTIC_RUN_ID", "none")
         tag = (f"{os.getppid()}_{os.environ.get('MASTER_PORT', '0')}" if world > 1
                else f"{os.getpid()}_single")
+        if world > 1 and run_id not in ("", "none"):
+            tag += "_" + re.sub(r"[^\w.-]", "_", run_id)[:40]
         d = os.path.join(tempfile.gettempdir(), f"gravsim_job_{tag}")
     os.makedirs(d, exist_ok=True)
     return d
@@ -87,8 +92,9 @@ class RunGuard:
         self.report = report
         self.poll_s, self.ack_wait_s = poll_s, ack_wait_s
         self.out = out  # stream of rank 0's JSON line (default: file descriptor 1)
+        self.t_start = time.time()
         self.rec: dict = {"rank": rank, "pid": os.getpid(), "stage": "start", "status": "running",
-                          "t_stage": time.time()}
+                          "t_stage": self.t_start, "t_start": self.t_start}
         self._deadline: Optional[float] = None
         self._aborts: list[Callable[[], None]] = []
         self._probes: list[Callable[[], dict]] = []
@@ -208,13 +214,19 @@ class RunGuard:
                                    f"{rec.get('stage')}: {rec.get('error', '')[:500]}")
 
     def _peer_records(self) -> list[dict]:
+        """Peer records of THIS job: a record left in a reused directory by an earlier job (its
+        process gone, or started long before this guard) is ignored until the peer of this job
+        overwrites it, so it cannot fire a false error."""
         out = []
         for r in range(1, self.world):
             try:
                 with open(self._path(r)) as f:
-                    out.append(json.load(f))
+                    rec = json.load(f)
             except (OSError, ValueError):
-                pass
+                continue
+            if _pid_alive(rec.get("pid")) and float(rec.get("t_start") or 0.0) >= \
+                    self.t_start - STALE_RECORD_S:
+                out.append(rec)
         return out
 
     def _fire(self, reason: str) -> None:
@@ -259,6 +271,21 @@ class RunGuard:
             except Exception:  # noqa: BLE001
                 pass
         os._exit(EXIT_CODE)
+
+
+# A peer record whose guard started this long before rank 0's belongs to an earlier job (the
+# ranks of one job start their guards within seconds of each other).
+STALE_RECORD_S = 120.0
+
+
+def _pid_alive(pid) -> bool:
+    try:
+        os.kill(int(pid), 0)
+    except (TypeError, ValueError, ProcessLookupError):
+        return False
+    except PermissionError:
+        return True
+    return True
 
 
 STEP_TIMEOUT_FLOOR_S = 60.0

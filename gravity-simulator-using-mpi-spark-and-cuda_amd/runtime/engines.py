@@ -145,9 +145,12 @@ class HipEngine:
         """Wait for the enqueued steps. With a timeout (or the engine's step timeout: P > 1
         cfg.step_timeout_s, or set_step_timeout) the wait polls RCCL async errors and aborts the
         communicator when no step completes for that long (it bounds progress, not the length
-        of the run)."""
+        of the run). One rank without a timeout passed here waits with a blocking stream sync:
+        there is no collective to hang on, and the poll's 200 us sleep would land inside a
+        timed region (up to 2.7 % of a 10-step 65K run); the run guard's stage
+        deadline still bounds it."""
         if timeout_s <= 0:
-            timeout_s = self.step_timeout_s
+            timeout_s = self.step_timeout_s if self.nranks > 1 else 0.0
         if timeout_s > 0:
             _native.check(self.lib, self.lib.gs_stepper_wait(self._s, timeout_s), "wait")
         else:
@@ -167,10 +170,11 @@ class HipEngine:
         _native.check(self.lib, self.lib.gs_stepper_phase_stats(self._s, out), "phase stats")
         v = list(out)
         steps, planned = int(v[0]), int(v[7])
-        # how the timed steps ran: from the segmented plan the untimed run replays, eagerly,
-        # or both (a step count that is not a whole number of two-step periods)
-        graph = ("segmented" if planned == steps else "eager" if planned == 0 else
-                 f"segmented ({planned} of {steps} steps)") if steps else None
+        # how the timed steps ran: replayed (one rank: the step graph; several: the segmented
+        # plan), eagerly, or both (a step count that is not a whole number of two-step periods)
+        rep = "segmented" if self.nranks > 1 else "graph"
+        graph = (rep if planned == steps else "eager" if planned == 0 else
+                 f"{rep} ({planned} of {steps} steps)") if steps else None
         return {"steps": steps, "step_ms": v[1], "gather_ms": v[2], "exchange_ms": v[3],
                 "exposed_gather_ms": v[4], "exposed_exchange_ms": v[5],
                 "deferred_units": int(v[6]), "comm_ms": v[2] + v[3],

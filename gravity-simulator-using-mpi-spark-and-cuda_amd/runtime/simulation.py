@@ -117,6 +117,11 @@ class Simulation:
                     self.engine.set_step_timeout(step_timeout(per_step))
             stage("ics", INIT_TIMEOUT_S)
         else:
+            # CPU engine (gloo for P > 1): no RCCL to hang on, and set-up includes O(N^2) work
+            # (a leapfrog half-kick), so the start-up deadline of gloo_init is cleared here
+            # instead of killing a slow but healthy start; gloo's own timeouts
+            # bound its collectives.
+            stage("cpu_setup", None)
             self.engine = CpuEngine(cfg, d.rank, d.world, dist=d)
         self.step0 = 0
         self.trajectory: list[np.ndarray] = []

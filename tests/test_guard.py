@@ -170,3 +170,30 @@ def test_bench_two_ranks_stalled_init_reports_within_budget(tmp_path):
     assert "HSA_ENABLE_IPC_MODE_LEGACY" in e["config"]["launch"]
     assert took < 60, took
     del EXIT_CODE
+
+
+def test_stale_peer_record_of_an_earlier_job_is_ignored(tmp_path):
+    """A reused guard directory still holds a 'failed' record of rank 1 from an earlier job
+    (its process gone): rank 0 of the new job must not fire on it, and a record of
+    a live peer of this job still counts."""
+    import io
+
+    from gravsim.parallel import guard as gd
+
+    stale = {"rank": 1, "pid": 2 ** 22 + 12345, "stage": "timed", "status": "failed",
+             "error": "old job", "t_stage": time.time() - 3600, "t_start": time.time() - 3600}
+    (tmp_path / "rank1.json").write_text(json.dumps(stale))
+    g = gd.RunGuard(0, 2, lambda reason, recs: {"error": reason}, directory=str(tmp_path),
+                    poll_s=0.05, out=io.StringIO())
+    try:
+        assert g._peer_records() == []
+        time.sleep(0.3)
+        assert not g._fired
+        with g._lock:
+            g._closed = True  # (stop the watchdog before a live 'failed' record appears)
+        time.sleep(0.15)
+        live = dict(stale, pid=os.getpid(), t_start=time.time(), error="this job")
+        (tmp_path / "rank1.json").write_text(json.dumps(live))
+        assert [r["error"] for r in g._peer_records()] == ["this job"]
+    finally:
+        g._closed = True

@@ -70,8 +70,8 @@ def test_unit_map_permutation_and_locality(n_pad, P, fill):
         assert n == rows * (S + D)
         m = np.frombuffer(out, dtype=np.uint32)
         remote = (m >> 31).astype(bool)
-        row = (m >> 16) & 0x7FFF
-        unit = m & 0xFFFF
+        row = (m >> 12) & 0xFFFF
+        unit = m & 0xFFF
         key = row.astype(np.int64) * (S + D) + unit
         assert np.array_equal(np.sort(key), np.arange(rows * (S + D)))  # a permutation
         A = a0 + row.astype(np.int64)
@@ -107,8 +107,8 @@ def test_ring_unit_map_stages(n_pad, P, fill):
         m = np.frombuffer(out, dtype=np.uint32)
         remote = (m >> 31).astype(bool)
         stage = ((m >> 28) & 7).astype(np.int64)
-        row = ((m >> 16) & 0xFFF).astype(np.int64)
-        unit = (m & 0xFFFF).astype(np.int64)
+        row = ((m >> 12) & 0xFFFF).astype(np.int64)
+        unit = (m & 0xFFF).astype(np.int64)
         key = row * (S + D) + unit
         assert np.array_equal(np.sort(key), np.arange(rows * (S + D)))
         assert np.array_equal(remote, stage > 0)
@@ -128,8 +128,8 @@ def test_ring_unit_map_stages(n_pad, P, fill):
         assert (np.diff(stage[local_prefix:]) >= 0).all()  # stage order after the prefix
         if fill != 0:
             assert not remote[:min(fill if fill > 0 else n, int((~remote).sum()))].any()
-    # too many rows for the 12-bit row field: no gated ring map (the launch stays ungated)
-    big = 1 << 25
+    # too many rows for the 16-bit row field: no gated ring map (the launch stays ungated)
+    big = 1 << 28
     assert lib.gs_sym_unit_map_ring(big, 0, 1, -1, None, 0) == 0
 
 
@@ -212,7 +212,7 @@ def test_split_segment_map(n_pad, P, np_):
     """The last Kr shell segments of every row (Kr = S / 16 when a segment has >= 2 tiles) are
     split into Np parts (gs_sym_split_parts: 4 when a segment spans >= 4 quanta, else 2): the
     gated order lists every other unit once and each split segment as Np part units (bit 30,
-    part in bits 28-29, rows in bits 16-27) at the very end, with the segment's locality."""
+    part in bits 28-29, rows in bits 12-27) at the very end, with the segment's locality."""
     lib, g = _geo(n_pad)
     S, D = g["S"], g["D"]
     kr = lib.gs_sym_split_segments(n_pad)
@@ -234,11 +234,11 @@ def test_split_segment_map(n_pad, P, np_):
         m = np.frombuffer(out, dtype=np.uint32)
         split = ((m >> 30) & 1).astype(bool)
         part = (m >> 28) & 3
-        row = (m >> 16) & 0xFFF
-        unit = m & 0xFFFF
+        row = (m >> 12) & 0xFFFF
+        unit = m & 0xFFF
         n_part = rows * kr * npart
         assert split[len(m) - n_part:].all() and not split[:len(m) - n_part].any()  # at the end
-        whole = unit[~split].astype(np.int64) + ((m[~split] >> 16) & 0x7FFF).astype(np.int64) * (S + D)
+        whole = unit[~split].astype(np.int64) + ((m[~split] >> 12) & 0xFFFF).astype(np.int64) * (S + D)
         expect = [r * (S + D) + u for r in range(rows) for u in range(S + D)
                   if not (S - kr <= u < S)]
         assert np.array_equal(np.sort(whole), np.array(expect, dtype=np.int64))
@@ -248,10 +248,26 @@ def test_split_segment_map(n_pad, P, np_):
         assert np.array_equal(np.sort(hk), np.array(want, dtype=np.int64))
         # a split segment's parts carry its locality (remote = reads gathered rows)
         pm = np.frombuffer(plain, dtype=np.uint32)
-        rem_plain = {(int((x >> 16) & 0x7FFF), int(x & 0xFFFF)): bool(x >> 31) for x in pm}
+        rem_plain = {(int((x >> 12) & 0xFFFF), int(x & 0xFFF)): bool(x >> 31) for x in pm}
         for x in m[split]:
-            key = (int((x >> 16) & 0xFFF), int(x & 0xFFFF))
+            key = (int((x >> 12) & 0xFFFF), int(x & 0xFFF))
             assert bool(x >> 31) == rem_plain[key]
+
+
+def test_unit_map_holds_16m_on_two_ranks():
+    """16M bodies on 2 ranks: 4096 rows per rank. Round 4's 12-bit row field returned no map
+    there, so the gated launch was silently replaced by the ungated one; the
+    16-bit row field holds it, with split parts, for every P."""
+    lib, g = _geo(1 << 24)
+    S, D = g["S"], g["D"]
+    kr, npart = lib.gs_sym_split_segments(1 << 24), lib.gs_sym_split_parts(1 << 24)
+    for P in (1, 2, 3, 8):
+        a0, rows = partition.sym_rank_rows(1 << 24, P, 0)
+        total = rows * (S + D + (npart - 1) * kr)
+        out = (ctypes.c_int32 * total)()
+        assert lib.gs_sym_unit_map_parts(1 << 24, 0, P, 2048, kr, npart, out, total) == total
+        m = np.frombuffer(out, dtype=np.uint32)
+        assert int(((m >> 12) & 0xFFFF).max()) == rows - 1
 
 
 @pytest.mark.parametrize("B", [4, 8, 64, 256])
