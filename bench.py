@@ -103,9 +103,9 @@ def parse(argv=None) -> argparse.Namespace:
     ap.add_argument("--no-energy", dest="energy", action="store_false",
                     help="skip the conserved-quantity passes (total energy with the exact-cutoff "
                          "potential, momenta) before the warmup and after the timed steps")
-    ap.add_argument("--exact-steps", type=int, default=3,
-                    help="steps timed with the reference's exact cutoff select after the "
-                         "headline (0 = skip)")
+    ap.add_argument("--exact-steps", type=int, default=10,
+                    help="steps timed with the reference's exact cutoff after the headline, on "
+                         "the headline's schedule (graph / segmented-plan replay; 0 = skip)")
     ap.add_argument("--init-timeout", type=float, default=180.0,
                     help="seconds each start-up stage (gloo, device, engine, RCCL init and "
                          "warm-up, the first step) may take before the run is stopped with an "
@@ -185,9 +185,10 @@ ACC_BOUND_C = 128.0
 def sampled_error(eng, cfg, samples: int, seed: int = 7) -> tuple[float, float]:
     """(max relative error, max bound ratio) over sampled own bodies: |a_gpu - a_ref| / |a_ref|
     and |a_gpu - a_ref| / (eps * sum_j |term_ij|) per component, where a_gpu is the step's own
-    force path (sym kernels, configured cutoff mode) and a_ref, sum |term| an fp64 row sum over
-    all N bodies by the native CPU engine (4 blocks of samples/4 contiguous rows). The bound
-    ratio must stay <= ACC_BOUND_C. Collective."""
+    force path (sym kernels, configured cutoff mode) and a_ref, sum |term| a row sum over all N
+    bodies by the native CPU engine (fp64 for an fp32 run, long double for an fp64 run; 4
+    blocks of samples/4 contiguous rows). The bound ratio must stay <= ACC_BOUND_C, for either
+    dtype. Collective."""
     import numpy as np
 
     from gravsim.ops import _native
@@ -207,14 +208,16 @@ def sampled_error(eng, cfg, samples: int, seed: int = 7) -> tuple[float, float]:
     X[:, 3] = mu.astype(np.float32) if cfg.dtype == "fp32" else mu  # mu as the kernel sees it
     lib = _native.cpu_lib()
     eps = 2.0 ** -24 if cfg.dtype == "fp32" else 2.0 ** -53
+    # the reference: an fp64 row sum for fp32 runs, a long-double one for fp64 runs (an fp64
+    # sum's own rounding is of the fp64 kernel's order)
+    ref_fn = lib.gs_cpu_accel_abs_f64 if cfg.dtype == "fp32" else lib.gs_cpu_accel_abs_ld
     worst, ratio = 0.0, 0.0
     eps2 = cfg.softening ** 2  # the intended physics: hard cutoff, no core
     for s0 in starts:
         g0 = L.local_begin + s0
         out = np.zeros((blk, 8))
-        _native.check(lib, lib.gs_cpu_accel_abs_f64(_native.dptr(X), cfg.n, g0, g0 + blk,
-                                                    cfg.cutoff ** 2, eps2, _native.dptr(out)),
-                      "cpu accel abs")
+        _native.check(lib, ref_fn(_native.dptr(X), cfg.n, g0, g0 + blk, cfg.cutoff ** 2, eps2,
+                                  _native.dptr(out)), "cpu accel abs")
         ref, absref = out[:, :3], out[:, 4:7]
         got = a_gpu[s0:s0 + blk, :3]
         err = np.linalg.norm(got - ref, axis=1) / np.maximum(np.linalg.norm(ref, axis=1), 1e-300)
@@ -518,9 +521,13 @@ def run(a, g) -> int:
     fmode = eng.force_mode()
     exact_ms = None
     if a.exact_steps > 0:
-        g.stage("exact", budget(2 + 2 * a.exact_steps))
+        # the same schedule as the headline: the replayed step graph (segmented plan for
+        # P > 1) rebuilt for the exact kernels, timed from a period start
+        g.stage("exact", budget(4 + 2 * a.exact_steps))
         eng.set_cutoff_mode("exact")
         eng.step(2)
+        if a.graph:
+            eng.align_period()
         eng.sync()
         comm.barrier(dist)
         t0 = time.perf_counter()

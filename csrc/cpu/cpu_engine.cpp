@@ -6,6 +6,9 @@
 // canonical chunk order shared with the GPU kernels so that results do not depend on the
 // number of ranks. Serves BASELINE config #1 ("1,024 bodies on CPU") and as a fast oracle.
 #include <math.h>
+
+#include <cmath>
+#include <type_traits>
 #include <stdint.h>
 #include <string.h>
 #ifdef _OPENMP
@@ -218,20 +221,27 @@ int step_range(const T* X4, T* Xn4, T* vel4, int64_t n_real, int64_t i0, int64_t
 // values: out8[8 * (i - i0) + d] = a_d, out8[8 * (i - i0) + 4 + d] = sum_j |term_ij,d|
 // (d < 3; entries 3 and 7 are 0). A floating-point sum of the terms is judged against that
 // scale: |a_gpu - a| <= c * eps * sum |terms| (the accuracy gates of bench.py and the 1M test).
+// A = double (the fp32 gates) or long double (x87 extended, 64-bit significand: the fp64 gates,
+// where an fp64 reference's own rounding is of the fp64 kernel's order).
+template <typename A>
 int accel_abs_range(const double* X4, int64_t n_real, int64_t i0, int64_t i1, double cut2,
                     double eps2, double* out8) {
   if (i1 < i0) { gs_set_error("cpu_accel_abs: bad arguments"); return -1; }
 #pragma omp parallel for schedule(dynamic, 1)
   for (int64_t i = i0; i < i1; ++i) {
-    const double xi = X4[4 * i], yi = X4[4 * i + 1], zi = X4[4 * i + 2];
-    double a[3] = {0, 0, 0}, s_abs[3] = {0, 0, 0};
+    const A xi = X4[4 * i], yi = X4[4 * i + 1], zi = X4[4 * i + 2];
+    A a[3] = {0, 0, 0}, s_abs[3] = {0, 0, 0};
     for (int64_t j = 0; j < n_real; ++j) {
-      const double dx = X4[4 * j] - xi, dy = X4[4 * j + 1] - yi, dz = X4[4 * j + 2] - zi;
-      const double r2 = std::fma(dz, dz, std::fma(dy, dy, std::fma(dx, dx, eps2)));
-      if (!(r2 >= cut2)) continue;
-      const double inv = 1.0 / std::sqrt(r2);
-      const double s = X4[4 * j + 3] * inv * inv * inv;
-      const double t[3] = {s * dx, s * dy, s * dz};
+      const A dx = (A)X4[4 * j] - xi, dy = (A)X4[4 * j + 1] - yi, dz = (A)X4[4 * j + 2] - zi;
+      A r2;
+      if constexpr (std::is_same<A, double>::value)
+        r2 = std::fma(dz, dz, std::fma(dy, dy, std::fma(dx, dx, eps2)));
+      else
+        r2 = dx * dx + dy * dy + dz * dz + (A)eps2;  // (fmal is a libm software call)
+      if (!(r2 >= (A)cut2)) continue;
+      const A inv = (A)1 / std::sqrt(r2);
+      const A s = (A)X4[4 * j + 3] * inv * inv * inv;
+      const A t[3] = {s * dx, s * dy, s * dz};
       for (int d = 0; d < 3; ++d) {
         a[d] += t[d];
         s_abs[d] += std::fabs(t[d]);
@@ -239,8 +249,8 @@ int accel_abs_range(const double* X4, int64_t n_real, int64_t i0, int64_t i1, do
     }
     double* o = out8 + 8 * (i - i0);
     for (int d = 0; d < 3; ++d) {
-      o[d] = a[d];
-      o[4 + d] = s_abs[d];
+      o[d] = (double)a[d];
+      o[4 + d] = (double)s_abs[d];
     }
     o[3] = o[7] = 0.0;
   }
@@ -253,7 +263,11 @@ extern "C" {
 
 int gs_cpu_accel_abs_f64(const double* X4, int64_t n_real, int64_t i0, int64_t i1, double cut2,
                          double eps2, double* out8) {
-  return accel_abs_range(X4, n_real, i0, i1, cut2, eps2, out8);
+  return accel_abs_range<double>(X4, n_real, i0, i1, cut2, eps2, out8);
+}
+int gs_cpu_accel_abs_ld(const double* X4, int64_t n_real, int64_t i0, int64_t i1, double cut2,
+                        double eps2, double* out8) {
+  return accel_abs_range<long double>(X4, n_real, i0, i1, cut2, eps2, out8);
 }
 
 int gs_cpu_accel_f64(const double* X4, int64_t n_real, int64_t i0, int64_t i1, int32_t chunk,

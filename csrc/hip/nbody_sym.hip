@@ -177,7 +177,7 @@ __device__ __forceinline__ void run_tiles(const SymArgs& a, ISetK<T>& is, TileSe
 #pragma unroll
     for (int j = 0; j < J; ++j) cs.cx[j] = cs.cy[j] = cs.cz[j] = T(0);
     if constexpr (kJpack<T>) {
-      sym::tile_lds_jp<G::I, SYM, EXACT>(is, cs, sm.jt[cur], eps2, cut2);
+      sym::tile_lds_jp<G::I, SYM, EXACT>(is, cs, sm.jt[cur], eps2, sym::f2{a.cut_k, a.cut_c});
     } else {
       sym::tile_lds64<G::I, SYM, EXACT>(is, cs, sm.jt[cur], eps2, cut2);
     }

@@ -168,6 +168,7 @@ gs::SymArgs sym_args(gs_stepper* s, int cur) {
   a.eps2 = s->eps2;
   a.exact = s->exact ? 1 : 0;
   a.cut2 = s->cfg.cutoff * s->cfg.cutoff;
+  gs::sym_cut_mask(a.cut2, &a.cut_k, &a.cut_c);
   a.band0 = 0;
   a.band_rows = a.rows;
   a.gate = nullptr;

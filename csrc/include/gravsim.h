@@ -141,6 +141,9 @@ int gs_cpu_accel_f32(const float* X4, int64_t n_real, int64_t i0, int64_t i1, in
 // row: a_x, a_y, a_z, 0, |.|_x, |.|_y, |.|_z, 0): the scale of a rounding-error bound.
 int gs_cpu_accel_abs_f64(const double* X4, int64_t n_real, int64_t i0, int64_t i1, double cut2,
                          double eps2, double* out8);
+// The same in long double (x87 extended): the reference of the fp64 accuracy gates.
+int gs_cpu_accel_abs_ld(const double* X4, int64_t n_real, int64_t i0, int64_t i1, double cut2,
+                        double eps2, double* out8);
 int gs_cpu_step_f64(const double* X4, double* Xnext4, double* vel4, int64_t n_real, int64_t i0,
                     int64_t i1, int32_t chunk, double dt, double cut2, double eps2);
 int gs_cpu_step_f32(const float* X4, float* Xnext4, float* vel4, int64_t n_real, int64_t i0,

@@ -1,6 +1,7 @@
 // Internal kernel-launch interface between nbody_kernels.hip and the Stepper runtime.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <math.h>
 #include <stdint.h>
 
 namespace gs {
@@ -96,6 +97,9 @@ struct SymArgs {
                        // first, remote units gated on `gate`, 7 the units the units-6 launch
                        // deferred (after the gather)
   double dt, eps2, cut2;
+  // fp32 exact cutoff as a clamp mask (gs_sym_tile.h cutoff_mask_r2): {-K, K cut2} with K a
+  // power of two scaling (float)cut2 to ~2^40 (sym_cut_mask); both 0 when cut2 is 0.
+  float cut_k, cut_c;
   // Gather gate (units 6/7): set on the comm stream right after the all-gather; a remote unit
   // that finds it still closed appends itself to defer[1..] (count defer[0]) and exits, and
   // the units-7 launch behind the gather event runs them. Finalize clears gate and count.
@@ -128,6 +132,22 @@ struct SymArgs {
 };
 
 hipError_t launch_force_sym(const SymArgs& a, hipStream_t s);
+// SymArgs::cut_k / cut_c for a cutoff^2 (as the fp32 tile sees it: (float)cut2).
+inline void sym_cut_mask(double cut2, float* k, float* c) {
+  const float c2 = (float)cut2;
+  if (!(c2 > 0.f)) {
+    *k = *c = 0.f;
+    return;
+  }
+  int e = 0;
+  (void)frexpf(c2, &e);  // c2 = f 2^e, f in [0.5, 1)
+  int s = 40 - e;
+  if (s > 126) s = 126;
+  if (s < -126) s = -126;
+  const float K = ldexpf(1.f, s);
+  *k = -K;
+  *c = K * c2;  // exact (a power-of-two scaling inside the normal range)
+}
 // Modeled collective (per-rank emulation) and the gather gate (comm_model.hip).
 hipError_t launch_comm_model(const void* src, void* dst, size_t bytes, uint64_t ticks, int wgs,
                              hipStream_t s);

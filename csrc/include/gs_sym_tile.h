@@ -27,7 +27,8 @@
 // packed value. fp64: 20 f64 ops + 1 v_rsq_f64 per pair (tile_lds).
 //
 // Numerics: the pair term uses the fast-cutoff core (r^2 + eps2, nbody_kernels.hip FM_FAST)
-// or, with EXACT, the reference hard cutoff as a select; r^-3 = (y*y)*y with y = rsq(r^2 +
+// or, with EXACT, the reference hard cutoff (fp32: a clamp mask on r^2, cutoff_mask_r2; fp64:
+// a select); r^-3 = (y*y)*y with y = rsq(r^2 +
 // eps2) (fp64: the refined r^-3 of the one-sided fp64 path). The j-side term of a pair is the
 // exact negation of what body j would compute for body i (x_i - x_j = -(x_j - x_i) in IEEE).
 //
@@ -109,6 +110,26 @@ struct ISetT {
 using f2 = float __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ f2 pk_fma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+
+// Reference hard cutoff for the packed fp32 tile (EXACT), bit-identical to the select
+// `r2 >= cut2 ? r^-3 : 0` in two packed ops instead of two compares and two v_cndmask:
+//   m  = clamp(fma(r2, -K, K cut2), 0, 1)   (ck = {-K, K cut2}, K a power of two, K cut2 ~ 2^40:
+//        the fma is exact before its rounding, so its sign is that of cut2 - r2, and any
+//        nonzero difference is >= one ulp of cut2, i.e. >= 2^16 after scaling: m is exactly 1
+//        below the cutoff and exactly 0 at or above it; the VOP3P clamp bit is not emitted
+//        for an elementwise min/max, hence the asm)
+//   r2 = fma(m, FLT_MAX, r2)                (unchanged when m = 0; FLT_MAX below the cutoff, so
+//        rsq ~ 5.4e-20 and its cube underflows to +0: the pair's r^-3 is exactly the select's
+//        +0, and r = 0 never reaches the rsq as an inf)
+// The ops this replaces cost the exact path +12.6 % over the fast core at 1M
+// (profiles/r4s2_bench1m_kernel_stats_final.csv: 185.9 vs 165.0 ms).
+__device__ __forceinline__ f2 cutoff_mask_r2(f2 r2, f2 ck) {
+  f2 m;
+  asm("v_pk_fma_f32 %0, %1, %2, %2 op_sel:[0,0,1] op_sel_hi:[1,0,1] clamp"
+      : "=v"(m)
+      : "v"(r2), "s"(ck));
+  return pk_fma(m, f2(3.40282347e38f), r2);
+}
 
 // Carriers of a lane's j-slots: the j-side accumulators travelling with the j-bodies.
 template <typename T, int J>
@@ -211,7 +232,7 @@ constexpr int kGroupI = 4;
 // 159.98 vs 162.4 ms (profiles/r3s2_sched_barrier_ab.jsonl, r3s2_barrier_mask_ab.jsonl).
 template <int I, bool SYM, bool EXACT>
 __device__ __forceinline__ void meet_jp(ISetP<I>& a, f2 xj, f2 yj, f2 zj, f2 mj, float eps2,
-                                        f2& tx, f2& ty, f2& tz, float cut2) {
+                                        f2& tx, f2& ty, f2& tz, f2 ck) {
   constexpr int U = I % kGroupI == 0 ? kGroupI : 1;
 #pragma unroll
   for (int i0 = 0; i0 < I; i0 += U) {
@@ -228,6 +249,10 @@ __device__ __forceinline__ void meet_jp(ISetP<I>& a, f2 xj, f2 yj, f2 zj, f2 mj,
     for (int u = 0; u < U; ++u) r2[u] = pk_fma(dy[u], dy[u], r2[u]);
 #pragma unroll
     for (int u = 0; u < U; ++u) r2[u] = pk_fma(dz[u], dz[u], r2[u]);
+    if constexpr (EXACT) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) r2[u] = cutoff_mask_r2(r2[u], ck);
+    }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       y[u].x = __builtin_amdgcn_rsqf(r2[u].x);
@@ -237,13 +262,6 @@ __device__ __forceinline__ void meet_jp(ISetP<I>& a, f2 xj, f2 yj, f2 zj, f2 mj,
     for (int u = 0; u < U; ++u) y3[u] = y[u] * y[u];
 #pragma unroll
     for (int u = 0; u < U; ++u) y3[u] = y3[u] * y[u];
-    if constexpr (EXACT) {
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        y3[u].x = r2[u].x >= cut2 ? y3[u].x : 0.f;
-        y3[u].y = r2[u].y >= cut2 ? y3[u].y : 0.f;
-      }
-    }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int i = i0 + u;
@@ -274,7 +292,7 @@ __device__ __forceinline__ void meet_jp(ISetP<I>& a, f2 xj, f2 yj, f2 zj, f2 mj,
 // closes the step, so every ds_read stays inside it.
 template <int I, bool SYM, bool EXACT, int K>
 __device__ __forceinline__ void lds_step_jp(ISetP<I>& a, CSetT<float, 2>& c, const float4* base,
-                                            float4& p, float4& q, float eps2, float cut2) {
+                                            float4& p, float4& q, float eps2, f2 ck) {
   float4 pn, qn;
   if constexpr (K + 1 < 16) {
     pn = base[2 * (K + 1)];
@@ -282,7 +300,7 @@ __device__ __forceinline__ void lds_step_jp(ISetP<I>& a, CSetT<float, 2>& c, con
   }
   f2 tx, ty, tz;
   meet_jp<I, SYM, EXACT>(a, f2{p.x, p.y}, f2{p.z, p.w}, f2{q.x, q.y}, f2{q.z, q.w}, eps2, tx,
-                         ty, tz, cut2);
+                         ty, tz, ck);
   if constexpr (SYM) {
     c.cx[0] = row_from<1>(c.cx[0]) - tx.x;
     c.cx[1] = row_from<1>(c.cx[1]) - tx.y;
@@ -300,23 +318,23 @@ __device__ __forceinline__ void lds_step_jp(ISetP<I>& a, CSetT<float, 2>& c, con
 
 template <int I, bool SYM, bool EXACT, int... Ks>
 __device__ __forceinline__ void lds_row_pass_jp(ISetP<I>& a, CSetT<float, 2>& c,
-                                                const float4* base, float eps2, float cut2,
+                                                const float4* base, float eps2, f2 ck,
                                                 std::integer_sequence<int, Ks...>) {
   float4 p = base[0], q = base[1];
-  (lds_step_jp<I, SYM, EXACT, Ks>(a, c, base, p, q, eps2, cut2), ...);
+  (lds_step_jp<I, SYM, EXACT, Ks>(a, c, base, p, q, eps2, ck), ...);
 }
 
 // All (64 I) x 128 pairs against the pair-staged j-tile (LDS). Carriers return home.
 template <int I, bool SYM, bool EXACT>
 __device__ __forceinline__ void tile_lds_jp(ISetP<I>& a, CSetT<float, 2>& c, const float4* tile,
-                                            float eps2, float cut2) {
+                                            float eps2, f2 ck) {
   const int lane = static_cast<int>(__lane_id());
   const int R = lane >> 4, col = lane & 15;
   const int addr = ((lane + 48) & 63) << 2;
 #pragma unroll 1
   for (int p = 0; p < 4; ++p) {
     const float4* base = tile + 2 * (((R - p) & 3) * 32 + (16 - col));
-    lds_row_pass_jp<I, SYM, EXACT>(a, c, base, eps2, cut2,
+    lds_row_pass_jp<I, SYM, EXACT>(a, c, base, eps2, ck,
                                    std::make_integer_sequence<int, 16>{});
     if constexpr (SYM) {
 #pragma unroll

@@ -128,6 +128,8 @@ def cpu_lib():
                  [P, P, P, c_int64, c_int64, c_int64, c_int32, T, T, T])
         _sig(lib, "gs_cpu_accel_abs_f64", c_int32, [_PD, c_int64, c_int64, c_int64, c_double,
                                                     c_double, _PD])
+        _sig(lib, "gs_cpu_accel_abs_ld", c_int32, [_PD, c_int64, c_int64, c_int64, c_double,
+                                                    c_double, _PD])
         _sig(lib, "gs_cpu_num_threads", c_int32, [])
         _sig(lib, "gs_cpu_set_threads", c_int32, [c_int32])
         _cpu = lib

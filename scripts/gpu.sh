@@ -21,6 +21,8 @@
 #                             (e.g. abv/r3tree: round 3's code) and this one, same box
 #   perturb                   smoke() and the 1M accuracy test on a deliberately broken build
 #                             (scripts/perturb_build.py -> abv/perturbed): both must FAIL
+#   perturb64                 the fp64 512K test and bench --dtype fp64 on abv/perturbed64 (the
+#                             fp64 carrier perturbed): both must FAIL
 #   ipc                       two-process HIP IPC with / without HSA_ENABLE_IPC_MODE_LEGACY=0
 #   span[:<bench args>]       reduce-phase span per step of the default schedule
 # Outputs land in gpurun_out/<task>*.log.
@@ -127,6 +129,20 @@ for task in "$@"; do
           --no-replay-audit $a
         t=$(find $d -name "*kernel_trace.csv" | head -1)
         echo "default $(python scripts/reduce_span.py $t)" | tee -a $out/span.txt
+      done ;;
+    perturb64)
+      # the fp64 gates on a build whose fp64 x carrier moves by the wrong DPP offset
+      # (scripts/perturb_build.py --what carrier64 --out abv/perturbed64): both must FAIL
+      : > $out/perturb64.txt
+      for t in scale bench; do
+        if [ $t = scale ]; then cmd=(python -u -m pytest tests/test_gpu_scale.py -x -q -k fp64_512k --timeout 300)
+        else cmd=(python bench.py --dtype fp64 --n 524288 --steps 2 --warmup 1 --exact-steps 0 --phase-steps 0 --no-replay-audit --no-energy); fi
+        timeout -k 10 400 env GRAVSIM_NATIVE_DIR=abv/perturbed64 "${cmd[@]}" > $out/perturb64_$t.log 2>&1
+        rc=$?
+        echo "perturbed fp64 build, $t: rc=$rc (a gate that bites exits non-zero)" | tee -a $out/perturb64.txt
+        grep -E "AssertionError|assert|work_audit|error" $out/perturb64_$t.log | tail -3 | cut -c1-400 | tee -a $out/perturb64.txt
+        if [ $rc -eq 124 ] || [ $rc -eq 137 ]; then exit $rc; fi
+        if [ $rc -eq 0 ]; then echo "!! the fp64 $t gate passed a broken kernel"; exit 1; fi
       done ;;
     ipc)
       # two-process HIP IPC (memory + event) with the launcher's dmabuf setting and without it

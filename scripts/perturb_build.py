@@ -18,6 +18,10 @@ sys.path.insert(0, os.path.join(ROOT, "csrc"))
 PERTURB = {
     "carrier": ("    c.cx[0] = row_from<1>(c.cx[0]) - tx.x;",
                 "    c.cx[0] = row_from<2>(c.cx[0]) - tx.x;"),
+    # the fp64 tile's x carrier (tests/test_gpu_scale.py::test_sym_fp64_512k_bands_accel_sampled
+    # and bench.py --dtype fp64's sampled gate must fail on it)
+    "carrier64": ("    c.cx[0] = row_from<1>(c.cx[0]) - tx;",
+                  "    c.cx[0] = row_from<2>(c.cx[0]) - tx;"),
 }
 
 

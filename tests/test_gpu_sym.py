@@ -164,6 +164,34 @@ def test_sym_exact_cutoff(hip, dtype):
     assert np.abs(got["sym"] - ref).max() / scale < tol * 10
 
 
+@pytest.mark.parametrize("dtype", ["fp32", "fp64"])
+def test_sym_exact_cutoff_boundary(hip, dtype):
+    """The select's boundary exactly: a pair exactly one cutoff apart (r^2 == cutoff^2 in the
+    kernel's arithmetic) keeps its force, a pair one metre closer gets none, and nothing turns
+    into inf/NaN (fp32 runs the clamp-mask form of the select, gs_sym_tile.h cutoff_mask_r2)."""
+    from gravsim.runtime.engines import HipEngine
+
+    acc = {}
+    for dist in (1000.0, 999.0):
+        b = ic.solar_random(20000, seed=3)
+        b.pos[4] = np.array([0.0, 1e11, 0.0])
+        b.pos[5] = np.array([dist, 1e11, 0.0])  # dx exact in fp32: r^2 == 1e6 at 1000 m
+        b.mass[5] = 1e24
+        e = HipEngine(SimConfig(n=b.n, dtype=dtype, device="gpu", mode="sym", cutoff=1e3))
+        try:
+            e.load(b)
+            assert e.force_mode()["exact"]
+            a = e.accel(step_path=True)[: b.n, :3]
+        finally:
+            e.close()
+        assert np.all(np.isfinite(a))
+        acc[dist] = a
+    pull = G_SI() * 1e24 / 1e6  # body 5 on body 4 at exactly the cutoff (~6.7e7 m/s^2)
+    assert abs(acc[1000.0][4, 0] - pull) < 1e-3 * pull
+    assert np.abs(acc[999.0][4]).max() < 1e-3 * pull  # inside the cutoff: no pair force
+    assert np.abs(acc[999.0][5]).max() < 1e-3 * pull
+
+
 def G_SI():
     from gravsim.config import G_SI as g
 
