@@ -43,7 +43,76 @@ __global__ void gate_set_kernel(unsigned* gate) {
   }
 }
 
+// ---- device-side stream ordering (flag sync: the multi-rank sym step as ONE graph) --------
+// A cross-stream ordering point of the multi-rank step (the comm stream waiting for the node
+// sums of an exchange stage, the compute stream waiting for the exchange...) was a hipEvent
+// record / wait pair; inside a segmented plan every such point cut the step graph, and each
+// cut cost 15-25 us of GPU idle time (profiles/r4s2_rank8_timeline.txt: 5 cuts per step at
+// 1M / 8). Here a point is a device counter instead: the producing stream runs a one-lane
+// signal kernel behind the producing work (stream order: that work has completed and its
+// writes were released at its kernel boundary), the consuming stream a one-workgroup wait
+// kernel in front of the consuming work, which polls the counter until it has passed the
+// number of signals the consumer has already taken (`seen`, a word only this consumer's
+// wait kernels touch, in stream order). Every signal is matched by exactly one wait, in FIFO
+// order per counter, so graph replays and eager steps interleave freely. The wait kernel is
+// one wave with a handful of registers: it never holds the CUs an RCCL kernel or the force
+// launch needs (round 2's in-kernel spin held them and deadlocked), and the kernel after it
+// starts with the dispatch's acquire. A level flag (the gather gate, re-armed by finalize)
+// works the same way without `seen`. Each wait adds its stall (s_memrealtime ticks) to
+// stats[0] and one to stats[1]: the exposed comm of the replayed step, which a single graph
+// cannot bracket with host events. The spin gives up after `limit` ticks (the native step
+// timeout) and counts that in stats[2], so a dead peer never leaves a kernel spinning.
+// `clear` (optional): a level flag this point re-arms first (the gather gate of the buffer
+// the signalled gather fills: the gate's wait on the compute stream must not see a gate left
+// set by an earlier gather of that buffer, e.g. a state read's, once init has reset the step).
+__global__ void sync_signal_kernel(unsigned* count, unsigned* clear) {
+  if (threadIdx.x == 0) {
+    if (clear) __hip_atomic_store(clear, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_fetch_add(count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+__global__ void sync_wait_kernel(const unsigned* flag, unsigned* seen,
+                                 unsigned long long* stats, uint64_t limit) {
+  if (threadIdx.x != 0) return;
+  const unsigned want = seen ? seen[0] + 1u : 1u;  // a level flag: any nonzero value
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  uint64_t t = t0;
+  bool ok = true;
+  for (;;) {
+    const unsigned v = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (seen ? (int)(v - want) >= 0 : v != 0u) break;
+    __builtin_amdgcn_s_sleep(8);
+    t = __builtin_amdgcn_s_memrealtime();
+    if (t - t0 > limit) {
+      ok = false;
+      break;
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  if (seen) seen[0] = want;
+  if (stats) {
+    __hip_atomic_fetch_add(stats, (unsigned long long)(t - t0), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add(stats + 1, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (!ok) __hip_atomic_fetch_add(stats + 2, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 }  // namespace
+
+hipError_t launch_sync_signal(unsigned* count, unsigned* clear, hipStream_t s) {
+  hipLaunchKernelGGL(sync_signal_kernel, dim3(1), dim3(64), 0, s, count, clear);
+  return hipGetLastError();
+}
+
+hipError_t launch_sync_wait(const unsigned* flag, unsigned* seen, unsigned long long* stats,
+                            uint64_t limit_ticks, hipStream_t s) {
+  hipLaunchKernelGGL(sync_wait_kernel, dim3(1), dim3(64), 0, s, flag, seen, stats, limit_ticks);
+  return hipGetLastError();
+}
 
 hipError_t launch_comm_model(const void* src, void* dst, size_t bytes, uint64_t ticks, int wgs,
                              hipStream_t s) {

@@ -750,6 +750,9 @@ __global__ __launch_bounds__(256) void sym_finalize_kernel(SymArgs a) {
   if (a.gate && li < a.gate_n)
     __hip_atomic_store(a.gate + li, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (a.gate && li == 0) __hip_atomic_store(a.defer, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // re-arm the dynamic unit counter of this step's force launch (as sym_tail_kernel does): the
+  // next step's launch skips its memset (SymArgs::work_zero)
+  if (a.work && li == 0) __hip_atomic_store(a.work, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (li >= a.n_local) return;
   const int64_t gi = a.i_begin + li;
   V4* vel = static_cast<V4*>(a.vel);

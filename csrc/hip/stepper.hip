@@ -384,24 +384,27 @@ bool fused_tail(const gs_stepper* s) {
   return size_ok && s->cfg.nranks == 1 && !multi(s) && s->sym_band >= s->sym_NC;
 }
 
-int sym_force(gs_stepper* s, gs::SymArgs a, bool overlap_gather, bool exchange = false) {
+// `gated`: the units-6 launch (a.gate: the gather's gate flag, which its remote units test);
+// `gflag`: the gate flag the compute stream's wait on the gather polls under flag sync.
+int sym_force(gs_stepper* s, gs::SymArgs a, bool overlap_gather, bool exchange = false,
+              bool gated = false, const unsigned* gflag = nullptr) {
   for (int b0 = 0; b0 < a.rows; b0 += s->sym_band) {
     a.band0 = b0;
     a.band_rows = s->sym_band < a.rows - b0 ? s->sym_band : a.rows - b0;
     a.units = 0;
     const bool one_band = a.band_rows == a.rows;
-    if (overlap_gather && b0 == 0 && one_band && a.gate) {
+    if (overlap_gather && b0 == 0 && one_band && gated) {
       // 3: one launch with the local units first; remote units run in it once the gather is
-      // published, or are deferred to a second launch queued behind the gather event.
+      // published, or are deferred to a second launch queued behind the gather.
       a.units = 6;
       GS_HIP(force_sym_launch(s, a, s->s_comp));
-      if (comp_wait(s, s->ev_gathered, kMarkGather)) return -1;
+      if (comp_wait_comm(s, s->ev_gathered, kMarkGather, -1, gflag)) return -1;
       a.units = 7;
       GS_HIP(force_sym_launch(s, a, s->s_comp));
       a.units = 0;
     } else {
       if (overlap_gather && b0 == 0) {
-        if (comp_wait(s, s->ev_gathered, kMarkGather)) return -1;
+        if (comp_wait_comm(s, s->ev_gathered, kMarkGather, -1, gflag)) return -1;
       }
       GS_HIP(force_sym_launch(s, a, s->s_comp));
     }
@@ -412,16 +415,18 @@ int sym_force(gs_stepper* s, gs::SymArgs a, bool overlap_gather, bool exchange =
     // (reduce phase at 1M 1533-1592 us per step against 1342-1381 in sequence;
     // profiles/r3_reduce_fork_split_ab.txt).
     if (a.Bbuf) GS_HIP(gs::launch_sym_block_reduce(a, s->s_comp));  // the band's leaves
+    bool exchanged = false;
     if (last) {
       if (exchange) {
-        if (sym_reduce_exchange(s, a)) return -1;  // node reduce pipelined with the sends
+        // node reduce pipelined with the sends
+        if (sym_reduce_exchange(s, a, &exchanged)) return -1;
       } else {
         GS_HIP(gs::launch_sym_node_reduce(a, s->s_comp));
       }
     }
     GS_HIP(gs::launch_sym_row_reduce(a, s->s_comp));
-    if (exchange && last) {
-      if (comp_wait(s, s->ev_sym, kMarkExchange)) return -1;
+    if (exchanged) {
+      if (comp_wait_comm(s, s->ev_sym, kMarkExchange, kSyncExch)) return -1;
     }
   }
   return 0;
@@ -434,7 +439,10 @@ int enqueue_sym(gs_stepper* s, int cur, bool need_gather, bool gathered_external
   // this stepper (RCCL or modeled) and one band (the gated launch covers every unit).
   const bool gated = part == 3 && need_gather && !gathered_externally && xcomm(s) &&
                      s->sym_overlap == 3 && s->sym_band >= a.rows && s->sym_lf;
-  if (gated) {
+  // Flag sync: every gather of this buffer is published by its gate flag, which finalize
+  // re-arms for the gather two steps on (a.gate; the force kernel tests it in units 6 only).
+  const bool fs = fsync(s) && !gathered_externally;
+  if (gated || fs) {
     a.gate = s->sym_ring ? s->ring_gate + 8 * cur : s->gate_buf + cur;
     a.gate_n = s->sym_ring ? 8 : 1;
   }
@@ -443,16 +451,19 @@ int enqueue_sym(gs_stepper* s, int cur, bool need_gather, bool gathered_external
       if (gathered_externally) s->full[cur] = true;
       else if (gather(s, cur, gated)) return -1;
     }
-    if (sym_force(s, a, need_gather, xcomm(s))) return -1;
+    if (sym_force(s, a, need_gather, xcomm(s), gated, fs ? s->gate_buf + cur : nullptr))
+      return -1;
     if (timed) GS_HIP(hipEventRecord(s->ev_local, s->s_comp));
   }
   if (part & 2) {
     if (fused_tail(s)) {
       GS_HIP(gs::launch_sym_tail(a, s->s_comp));
-      s->work_zero = true;  // the tail re-armed the unit counter
     } else {
       GS_HIP(gs::launch_sym_finalize(a, s->s_comp));
     }
+    // both re-armed the dynamic unit counter of this step's force launch: the next step's
+    // launch needs no memset (one launch fewer per step)
+    s->work_zero = true;
   }
   return 0;
 }
@@ -655,10 +666,10 @@ int accel_impl(gs_stepper* s, double* acc4, bool step_path) {
       if (sym_force(s, sa, false, xcomm(s))) return -1;
       if (fused_tail(s)) {
         GS_HIP(gs::launch_sym_tail(sa, s->s_comp));
-        s->work_zero = true;
       } else {
         GS_HIP(gs::launch_sym_finalize(sa, s->s_comp));
       }
+      s->work_zero = true;  // (both re-arm the unit counter)
       GS_HIP(hipStreamSynchronize(s->s_comp));
       std::vector<T> A((size_t)s->L.n_local * 4);
       GS_HIP(hipMemcpy(A.data(), s->acc, A.size() * sizeof(T), hipMemcpyDeviceToHost));
@@ -727,6 +738,9 @@ int gs_stepper_create(const gs_config* cfg, gs_stepper** out) {
   }
   if (s->esz == 8) s->dyn_cap = 4;  // fp64: 512K 101.9-102.0 ms at 4 vs 102.0-102.5 at 2
   if (const char* v = getenv("GRAVSIM_FAULT_SKIP_UNITS")) s->fault_skip = (unsigned)atoi(v);
+  // GRAVSIM_SYNC=events: the multi-rank step orders its streams by hipEvents (and replays a
+  // segmented plan) instead of device counters (flag sync, one graph per period)
+  if (const char* v = getenv("GRAVSIM_SYNC")) s->sync_events = strcmp(v, "events") == 0;
   const int64_t own_first = s->L.local_begin / s->L.chunk;
   const int64_t own_last = (s->L.local_begin + s->L.n_local) / s->L.chunk;
   s->own_c0 = (int)(own_first < s->L.n_chunks ? own_first : s->L.n_chunks);
@@ -807,6 +821,14 @@ int gs_stepper_create(const gs_config* cfg, gs_stepper** out) {
   // [0..1] gather gates, [2..3] deferral stats, [4] dynamic unit-fetch counter
   ALLOC_CLEAN(&s->gate_buf, 8 * sizeof(unsigned), "gate");
   FAIL_CLEAN(hipMemsetAsync(s->gate_buf, 0, 8 * sizeof(unsigned), s->s_comp));
+  if (cfg->nranks > 1 || getenv("GRAVSIM_FORCE_COMM")) {
+    // flag-sync counters of the multi-rank step (signals / waits per point) and the waits'
+    // stall statistics
+    ALLOC_CLEAN(&s->sync_buf, 2 * kSyncCount * sizeof(unsigned), "sync");
+    FAIL_CLEAN(hipMemsetAsync(s->sync_buf, 0, 2 * kSyncCount * sizeof(unsigned), s->s_comp));
+    ALLOC_CLEAN(&s->sync_stats, 9 * sizeof(unsigned long long), "sync_stats");
+    FAIL_CLEAN(hipMemsetAsync(s->sync_stats, 0, 9 * sizeof(unsigned long long), s->s_comp));
+  }
   if (s->L.mode == GS_MODE_SYM) {
     // the work audit's unit counter (its cost is within noise: profiles/r3_abaudit*)
     ALLOC_CLEAN(&s->audit, sizeof(unsigned long long), "audit");
@@ -1007,6 +1029,10 @@ int gs_stepper_set_timing(gs_stepper* s, int32_t on) {
   s->timed = on != 0;
   s->pev_used = 0;
   s->pev_plan = 0;
+  // (the wait kernels' stall counters restart with the timed steps; stream-ordered behind
+  // every compute-stream wait enqueued before)
+  if (s->sync_stats)
+    GS_HIP(hipMemsetAsync(s->sync_stats, 0, 9 * sizeof(unsigned long long), s->s_comp));
   return 0;
 }
 
@@ -1134,17 +1160,34 @@ int gs_stepper_phase_stats(gs_stepper* s, double* out8) {
     GS_HIP(hipStreamSynchronize(st));
   s->prog_done = s->prog_rec;
   const int n_ev = s->pev_used;
-  int n = 0;  // steps (a one-rank graph period's event set spans two)
+  int n = 0;  // steps (a graph period's event set spans two; its partner set, none)
   for (int i = 0; i < n_ev; ++i) {
     const gs_stepper::PhaseEv& p = s->pev[i];
     n += p.nsteps;
     float v = 0.f;
-    GS_HIP(hipEventElapsedTime(&v, p.t0, p.end));
-    out8[1] += v;
+    if (p.nsteps > 0) {
+      GS_HIP(hipEventElapsedTime(&v, p.t0, p.end));
+      out8[1] += v;
+    }
     if (p.g) { GS_HIP(hipEventElapsedTime(&v, p.g0, p.g1)); out8[2] += v; }
     if (p.x) { GS_HIP(hipEventElapsedTime(&v, p.x0, p.x1)); out8[3] += v; }
     if (p.w) { GS_HIP(hipEventElapsedTime(&v, p.w0, p.w1)); out8[4] += v; }
     if (p.j) { GS_HIP(hipEventElapsedTime(&v, p.j0, p.j1)); out8[5] += v; }
+  }
+  if (s->sync_stats) {
+    // flag sync: the compute stream's stalls are the wait kernels' own (device counters of
+    // s_memrealtime ticks), not host-recorded event pairs
+    unsigned long long st[9];
+    GS_HIP(hipMemcpy(st, s->sync_stats, sizeof(st), hipMemcpyDeviceToHost));
+    if (st[1] || st[4]) {
+      out8[4] = st[0] / s->clk_khz;
+      out8[5] = st[3] / s->clk_khz;
+    }
+    if (st[2] || st[5] || st[8]) {
+      gs_set_error("flag sync: a wait kernel gave up after the step timeout");
+      return -1;
+    }
+    GS_HIP(hipMemsetAsync(s->sync_stats, 0, sizeof(st), s->s_comp));
   }
   if (n > 0)
     for (int i = 1; i < 6; ++i) out8[i] /= n;

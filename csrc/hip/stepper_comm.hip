@@ -45,13 +45,20 @@ void rank_slice(const gs_stepper* s, int q, int64_t* b0, int64_t* cnt) {
 // slices already received can start.
 int gather(gs_stepper* s, int cur, bool gate) {
   if (!xcomm(s) || s->full[cur]) return 0;
-  if (comp_record(s, s->ev_ready)) return -1;
+  // Flag sync publishes every gather through the gate flag of its buffer, gated launch or
+  // not: the compute stream's wait on the gather polls it. The READY signal re-arms it first,
+  // on the compute stream, so no wait behind this point can see a gate left set by an earlier
+  // gather of the buffer (a state read's, before init reset the step count).
+  if (comp_signal(s, s->ev_ready, kSyncReady,
+                  fsync(s) && !s->sym_ring ? s->gate_buf + cur : nullptr))
+    return -1;
   s->full[cur] = true;
+  if (fsync(s)) gate = true;
   return comm_do(s, [s, cur, gate]() -> int {
     if (comm_dead(s)) return -1;
     char* buf = static_cast<char*>(s->X[cur]);
     const size_t count = (size_t)s->L.n_local * 4;
-    GS_HIP(hipStreamWaitEvent(s->s_comm, s->ev_ready, 0));
+    if (comm_wait_comp(s, s->ev_ready, kSyncReady)) return -1;
     GS_MARK(g0, g, s->s_comm);
     const ncclDataType_t dt = s->esz == 4 ? ncclFloat32 : ncclFloat64;
     if (s->sym_ring && use_sym(s)) {
@@ -167,7 +174,7 @@ static int node_reduce_dests(gs_stepper* s, const gs::SymArgs& a0, int kb, int k
 // computed, instead of the whole exchange waiting for the whole node reduce (1M / 8 ranks:
 // a 190 us exchange behind a 100 us node reduce). Same kernels and sums per body: same bits.
 // The compute stream joins the exchange later (comp_wait on ev_sym before finalize).
-int sym_reduce_exchange(gs_stepper* s, const gs::SymArgs& a0) {
+int sym_reduce_exchange(gs_stepper* s, const gs::SymArgs& a0, bool* exchanged) {
   const int P = s->cfg.nranks, r = s->cfg.rank;
   // stage g: shifts [k_lo[g], k_lo[g + 1]). Stage 1 is the smaller one (a third of the
   // shifts): its reduce is short, so the messages start early, and the larger stage 2 reduce
@@ -177,14 +184,14 @@ int sym_reduce_exchange(gs_stepper* s, const gs::SymArgs& a0) {
   const int k_lo[3] = {1, stages == 2 ? 1 + k1 : P, P};
   for (int g = 0; g < stages; ++g) {
     if (node_reduce_dests(s, a0, k_lo[g], k_lo[g + 1])) return -1;
-    if (comp_record(s, s->ev_stage[g])) return -1;
+    if (comp_signal(s, s->ev_stage[g], kSyncStage0 + g)) return -1;
     const int kb = k_lo[g], ke = k_lo[g + 1];
     const bool first = g == 0, last = g + 1 == stages;
     if (comm_do(s, [s, g, kb, ke, first, last]() -> int {
           const int P = s->cfg.nranks, r = s->cfg.rank;
           const size_t e = s->esz, nl = (size_t)s->L.n_local, my = (size_t)s->nn[r];
           if (comm_dead(s)) return -1;
-          GS_HIP(hipStreamWaitEvent(s->s_comm, s->ev_stage[g], 0));
+          if (comm_wait_comp(s, s->ev_stage[g], kSyncStage0 + g)) return -1;
           if (first) GS_MARK(x0, x, s->s_comm);
           if (s->emulate) {
             // the bytes this rank receives in this stage, read from its receive buffer
@@ -205,15 +212,15 @@ int sym_reduce_exchange(gs_stepper* s, const gs::SymArgs& a0) {
           }
           if (last) {
             GS_MARK(x1, x, s->s_comm);
-            GS_HIP(hipEventRecord(s->ev_sym, s->s_comm));
+            if (comm_signal_comp(s, s->ev_sym, kSyncExch)) return -1;
           }
           return 0;
         }))
       return -1;
   }
   if (node_reduce_dests(s, a0, 0, 1)) return -1;  // the own sums, last
-  // (a live 1-rank communicator: nothing to exchange; the join below is then immediate)
-  if (stages == 0 && comp_record(s, s->ev_sym)) return -1;
+  // (a live 1-rank communicator: nothing to exchange, and nothing for finalize to wait for)
+  *exchanged = stages > 0;
   return 0;
 }
 

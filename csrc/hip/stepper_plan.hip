@@ -95,10 +95,60 @@ int comp_wait(gs_stepper* s, hipEvent_t ev, int mark) {
 }
 
 // Work on the comm stream (a collective and its event bookkeeping): run now, or replayed
-// eagerly at this point of the plan.
+// eagerly at this point of the plan. With flag sync the comm stream never waits on a host-
+// visible point of the compute stream, so the op is kept without cutting the open segment
+// (a replay issues a period's comm ops, then its one compute graph).
 int comm_do(gs_stepper* s, std::function<int()> fn) {
   if (!s->rec) return fn();
+  if (fsync(s)) {
+    gs_stepper::PlanOp op{gs_stepper::PlanOp::kHost, nullptr, nullptr, std::move(fn)};
+    op.step = s->rec_step;
+    s->plan.push_back(std::move(op));
+    return 0;
+  }
   return plan_push(s, {gs_stepper::PlanOp::kHost, nullptr, nullptr, std::move(fn)});
+}
+
+// ---- cross-stream points: events, or device counters (flag sync) ------------------------
+namespace {
+uint64_t sync_limit_ticks(const gs_stepper* s) {
+  const double t = s->step_timeout_s > 0 ? s->step_timeout_s : 600.0;
+  return (uint64_t)(t * s->clk_khz * 1e3);
+}
+}  // namespace
+
+int comp_signal(gs_stepper* s, hipEvent_t ev, int id, unsigned* clear) {
+  if (!fsync(s)) return comp_record(s, ev);
+  GS_HIP(gs::launch_sync_signal(s->sync_buf + 2 * id, clear, s->s_comp));
+  return 0;
+}
+
+int comm_wait_comp(gs_stepper* s, hipEvent_t ev, int id) {
+  if (!fsync(s)) {
+    GS_HIP(hipStreamWaitEvent(s->s_comm, ev, 0));
+    return 0;
+  }
+  GS_HIP(gs::launch_sync_wait(s->sync_buf + 2 * id, s->sync_buf + 2 * id + 1, s->sync_stats + 6,
+                              sync_limit_ticks(s), s->s_comm));
+  return 0;
+}
+
+int comm_signal_comp(gs_stepper* s, hipEvent_t ev, int id) {
+  GS_HIP(hipEventRecord(ev, s->s_comm));  // (eager users: download / accel queries)
+  if (fsync(s)) GS_HIP(gs::launch_sync_signal(s->sync_buf + 2 * id, nullptr, s->s_comm));
+  return 0;
+}
+
+int comp_wait_comm(gs_stepper* s, hipEvent_t ev, int mark, int id, const unsigned* flag) {
+  if (!fsync(s)) return comp_wait(s, ev, mark);
+  unsigned long long* st = s->sync_stats + (mark == kMarkExchange ? 3 : 0);
+  if (flag) {
+    GS_HIP(gs::launch_sync_wait(flag, nullptr, st, sync_limit_ticks(s), s->s_comp));
+  } else {
+    GS_HIP(gs::launch_sync_wait(s->sync_buf + 2 * id, s->sync_buf + 2 * id + 1, st,
+                                sync_limit_ticks(s), s->s_comp));
+  }
+  return 0;
 }
 
 void drop_graphs(gs_stepper* s) {
@@ -110,6 +160,7 @@ void drop_graphs(gs_stepper* s) {
     if (op.g) (void)hipGraphExecDestroy(op.g);
   s->plan.clear();
   s->plan_graphs = 0;
+  s->plan_fsync = false;
 }
 
 int build_graph(gs_stepper* s) {
@@ -117,10 +168,13 @@ int build_graph(gs_stepper* s) {
   const int64_t k0 = s->k;
   const bool f0 = s->full[0], f1 = s->full[1];
   hipGraph_t g = nullptr;
-  // A replayed graph cannot rely on the counter state at capture time: its first sym force
-  // launch always re-zeroes the unit counter (a later one may skip it after a fused tail
-  // inside the graph; the flag left by the capture then matches every replay's end state).
-  s->work_zero = false;
+  // The dynamic unit counter is 0 between steps in every reachable state: zeroed at creation,
+  // and every step's last kernel (finalize or the fused tail) re-arms it after the step's force
+  // launches, so a replay may start without a memset. (Round 2's graphs assumed this while
+  // only the fused tail re-armed the counter, and replays after a non-fused step skipped
+  // units; tests/test_gpu_sym.py test_sym_graph_replays_rezero_unit_counter and the work audit
+  // of every bench and CLI run guard it.)
+  s->work_zero = true;
   GS_HIP(hipStreamBeginCapture(s->s_comp, hipStreamCaptureModeThreadLocal));
   int rc = enqueue_step_any(s, true);
   if (rc == 0) rc = enqueue_step_any(s, true);
@@ -147,7 +201,8 @@ int build_plan(gs_stepper* s) {
   const int64_t k0 = s->k;
   const bool f0 = s->full[0], f1 = s->full[1];
   drop_graphs(s);
-  s->work_zero = false;  // (as build_graph: a replay re-zeroes the dynamic unit counter)
+  s->plan_fsync = fsync(s);
+  s->work_zero = true;  // (as build_graph: the counter is 0 between steps)
   s->rec_step = 0;
   if (seg_open(s)) return -1;
   s->rec = true;
@@ -171,7 +226,45 @@ int build_plan(gs_stepper* s) {
   return 0;
 }
 
+// A flag-sync plan: the period's comm ops (eager, in order; their spans recorded per step),
+// then its one compute graph (timed as a whole: one event set of two steps; the compute
+// stream's stalls come from the wait kernels' device counters).
+int run_plan_fsync(gs_stepper* s) {
+  gs_stepper::PhaseEv* pe[2] = {nullptr, nullptr};
+  if (s->timed) {
+    for (auto& p : pe)
+      if (!(p = phase_begin(s))) break;
+    if (pe[0] && pe[1]) {
+      pe[0]->nsteps = 2;
+      pe[1]->nsteps = 0;  // (comm spans of step 1 only)
+    } else {
+      pe[0] = pe[1] = nullptr;
+    }
+  }
+  for (auto& op : s->plan) {
+    if (op.kind != gs_stepper::PlanOp::kHost) continue;
+    s->pe = pe[op.step & 1];
+    const int rc = op.fn();
+    s->pe = nullptr;
+    if (rc) return -1;
+  }
+  if (pe[0]) GS_HIP(hipEventRecord(pe[0]->t0, s->s_comp));
+  for (auto& op : s->plan) {
+    if (op.kind == gs_stepper::PlanOp::kGraph) GS_HIP(hipGraphLaunch(op.g, s->s_comp));
+    else if (op.kind != gs_stepper::PlanOp::kHost) {
+      gs_set_error("run_plan: a flag-sync plan holds only graphs and comm ops");
+      return -1;
+    }
+  }
+  if (pe[0]) {
+    GS_HIP(hipEventRecord(pe[0]->end, s->s_comp));
+    s->pev_plan += 2;
+  }
+  return 0;
+}
+
 int run_plan(gs_stepper* s) {
+  if (s->plan_fsync) return run_plan_fsync(s);
   // Phase timing (gs_stepper_set_timing): one event set per step of the period. Step 0 starts
   // before the first op, step 1 at its first op (a segment belongs to the step it began in);
   // the collectives' spans are recorded on s_comm by the host ops (GS_MARK with `pe` set).

@@ -152,6 +152,14 @@ inline void sym_cut_mask(double cut2, float* k, float* c) {
 hipError_t launch_comm_model(const void* src, void* dst, size_t bytes, uint64_t ticks, int wgs,
                              hipStream_t s);
 hipError_t launch_gate_set(unsigned* gate, hipStream_t s);
+// Device-side stream ordering (comm_model.hip): signal = one release add to a counter (after
+// zeroing the level flag `clear`, if given); wait =
+// one wave polling `flag` until it passes seen[0] (a counter; seen nullptr: a level flag),
+// adding its stall to stats[0] (s_memrealtime ticks) and 1 to stats[1]; gives up after
+// limit_ticks (counted in stats[2]).
+hipError_t launch_sync_signal(unsigned* count, unsigned* clear, hipStream_t s);
+hipError_t launch_sync_wait(const unsigned* flag, unsigned* seen, unsigned long long* stats,
+                            uint64_t limit_ticks, hipStream_t s);
 hipError_t launch_sym_block_reduce(const SymArgs& a, hipStream_t s);  // band leaves -> Bbuf
 hipError_t launch_sym_node_reduce(const SymArgs& a, hipStream_t s);   // own nodes -> Sbuf
 hipError_t launch_sym_row_reduce(const SymArgs& a, hipStream_t s);    // the band's rows -> Ti

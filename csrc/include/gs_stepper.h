@@ -201,6 +201,16 @@ struct gs_stepper {
     const char* tag;
   };
   std::vector<MemEntry> mem;
+  // Flag sync (fsync(): the multi-rank all-gather sym schedule): the cross-stream ordering
+  // points are device counters with signal / wait kernels (comm_model.hip) instead of hipEvent
+  // record / wait, so a replayed period is ONE compute graph plus the comm stream's eager ops,
+  // no cut points. sync_buf[2 id] = signals of point id, [2 id + 1] = waits taken (kSync*);
+  // sync_stats[3 k] = {stall ticks, waits, timeouts} of the compute stream's gather (k 0) and
+  // exchange (k 1) waits, k 2 the comm stream's waits. GRAVSIM_SYNC=events keeps the events.
+  unsigned* sync_buf = nullptr;
+  unsigned long long* sync_stats = nullptr;
+  bool sync_events = false;  // GRAVSIM_SYNC=events
+  bool plan_fsync = false;   // the recorded plan is one graph (flag sync) + comm host ops
 };
 
 #define GS_MARK(field, flag, stream)                             \
@@ -215,6 +225,10 @@ namespace gs::rt {
 
 // What a compute-stream wait on another stream's event stands for, in the phase timing.
 enum : int { kMarkNone = 0, kMarkGather = 1, kMarkExchange = 2 };
+// Flag-sync points (gs_stepper::sync_buf): own slice of X written (compute -> comm, the
+// all-gather's input), node sums of exchange stage 0 / 1 reduced (compute -> comm), exchange
+// received (comm -> compute). The gather itself is published by the gate flag (level).
+enum : int { kSyncReady = 0, kSyncStage0 = 1, kSyncStage1 = 2, kSyncExch = 3, kSyncCount = 4 };
 
 inline size_t row_bytes(const gs_stepper* s) { return 4 * s->esz; }
 
@@ -245,6 +259,14 @@ inline bool xcomm(const gs_stepper* s) { return s->have_comm || s->emulate; }
 inline bool multi(const gs_stepper* s) { return s->have_comm || s->emulate || s->virt; }
 // The sym kernels implement both cutoff paths (fast core and exact select).
 inline bool use_sym(const gs_stepper* s) { return s->L.mode == GS_MODE_SYM; }
+// Cross-stream ordering by device counters (flag sync) rather than events: the multi-rank
+// sym schedule with the all-gather (the ring keeps its per-stage events).
+// (--graph-comm captures the collectives into the step graph: that capture follows the comm
+// stream through event edges, so it keeps the events.)
+inline bool fsync(const gs_stepper* s) {
+  return !s->sync_events && s->sync_buf && use_sym(s) && xcomm(s) && !s->sym_ring &&
+         s->cfg.use_graph <= 1;
+}
 
 // ---- shared by the runtime's translation units -----------------------------------------
 // stepper_plan.hip: compute-stream ordering points (eager, or cut points of a recorded
@@ -254,6 +276,15 @@ int seg_open(gs_stepper* s);
 int comp_record(gs_stepper* s, hipEvent_t ev);
 int comp_wait(gs_stepper* s, hipEvent_t ev, int mark = kMarkNone);
 int comm_do(gs_stepper* s, std::function<int()> fn);
+// Cross-stream points that switch between events and flag sync (fsync): compute -> comm
+// (comp_signal on s_comp now, comm_wait_comp inside the comm op), comm -> compute
+// (comm_signal_comp inside the comm op, comp_wait_comm on s_comp now). `ev` is the event of
+// the event path; `id` the kSync point; `flag` a level flag for comp_wait_comm (the gate)
+// instead of a counter.
+int comp_signal(gs_stepper* s, hipEvent_t ev, int id, unsigned* clear = nullptr);
+int comm_wait_comp(gs_stepper* s, hipEvent_t ev, int id);
+int comm_signal_comp(gs_stepper* s, hipEvent_t ev, int id);
+int comp_wait_comm(gs_stepper* s, hipEvent_t ev, int mark, int id, const unsigned* flag = nullptr);
 void drop_graphs(gs_stepper* s);
 int build_graph(gs_stepper* s);
 bool plan_ok(const gs_stepper* s);
@@ -269,7 +300,7 @@ int gather(gs_stepper* s, int cur, bool gate = false);
 int ring_src(const gs_stepper* s, int sub);
 void rank_chunks(const gs_stepper* s, int src, int* c0, int* c1);
 int ring_xfer_rccl(gs_stepper* s, int cur, int sub);
-int sym_reduce_exchange(gs_stepper* s, const gs::SymArgs& a);
+int sym_reduce_exchange(gs_stepper* s, const gs::SymArgs& a, bool* exchanged);
 void maybe_install_crash_trace();
 // ncclCommAbort once (the watchdog thread, a timeout or an async error may all ask for it).
 bool abort_comm(gs_stepper* s);

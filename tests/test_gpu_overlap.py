@@ -27,13 +27,19 @@ def _emu(monkeypatch, n, P, rank, gbps, overlap, strategy="allgather", graph=Tru
     return e
 
 
-@pytest.mark.parametrize("strategy,overlap", [("allgather", 3), ("allgather", 0),
-                                              ("ring", 3)])
-def test_segmented_plan_matches_eager(hip, monkeypatch, strategy, overlap):
-    """Multi-rank steps replay a segmented plan by default: the compute work between two
-    collectives is captured as graph segments and the collectives (here the emulation's
-    modeled ones, on a real node RCCL) run eagerly between them. Same bits as eager steps,
-    every unit run once per step, and the plan is what ran."""
+@pytest.mark.parametrize("strategy,overlap,sync", [("allgather", 3, "flags"),
+                                                   ("allgather", 0, "flags"),
+                                                   ("allgather", 3, "events"),
+                                                   ("ring", 3, "events")])
+def test_segmented_plan_matches_eager(hip, monkeypatch, strategy, overlap, sync):
+    """Multi-rank steps replay a plan by default: the collectives (here the emulation's modeled
+    ones, on a real node RCCL) run eagerly on the comm stream, the compute work is replayed
+    from graphs. With flag sync (the all-gather default) the streams order each other through
+    device counters and a period is ONE compute graph; with events (GRAVSIM_SYNC=events, and
+    the ring) every cross-stream point cuts the period into segments. Same bits as eager steps
+    either way, every unit run once per step, and the plan is what ran."""
+    if sync == "events":
+        monkeypatch.setenv("GRAVSIM_SYNC", "events")
     res = {}
     for graph in (True, False):
         e = _emu(monkeypatch, 262144, 8, 6, 64, overlap, strategy=strategy, graph=graph)
@@ -46,7 +52,10 @@ def test_segmented_plan_matches_eager(hip, monkeypatch, strategy, overlap):
         gi = e.graph_info()
         assert gi["mode"] == ("segmented" if graph else "eager"), gi
         if graph:
-            assert gi["segments"] >= 4, gi
+            if sync == "flags":
+                assert gi["segments"] == 1, gi  # one compute graph per period
+            else:
+                assert gi["segments"] >= 4, gi
         b = e.state()
         own = e.layout.real_local
         res[graph] = (b.pos[own.start:own.stop].copy(), b.vel[own.start:own.stop].copy())
