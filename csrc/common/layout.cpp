@@ -389,6 +389,30 @@ extern "C" int64_t gs_sym_unit_map_ring(int64_t n_pad, int32_t rank, int32_t nra
   return k;
 }
 
+// Whether the node sums rank `src` sends rank `dst` can be nonzero (1) or are +0.0 for every
+// body by the geometry alone (0): no row of src's holds a chunk of dst's in its shell (chunk X
+// is in row A's shell iff d = (X - A) mod NC is in [1, NC/2 - 1], or d = NC/2 and row A takes
+// its antipodal chunk). The j-side sums of such a pair skip every row and stay +0.0, the
+// identity of the receiver's tree merge, so the send can be skipped: the receiver's slots for
+// those nodes hold the +0.0 they were zeroed to. At P = 8 three of a rank's seven destinations
+// are far side (d > NC/2): 43 % less exchange. -1 on bad arguments.
+extern "C" int32_t gs_sym_pair_live(int64_t n_pad, int32_t nranks, int32_t src, int32_t dst) {
+  int32_t sa0, srows, da0, drows;
+  if (src == dst) return 1;
+  if (gs_sym_rank_rows(n_pad, nranks, src, &sa0, &srows) ||
+      gs_sym_rank_rows(n_pad, nranks, dst, &da0, &drows))
+    return -1;
+  const int32_t NC = (int32_t)(n_pad / 2048);
+  for (int32_t A = sa0; A < sa0 + srows; ++A) {
+    const bool anti = gs_sym_shell_len(A, NC) == NC / 2;
+    for (int32_t X = da0; X < da0 + drows; ++X) {
+      const int32_t d = ((X - A) % NC + NC) % NC;
+      if ((d >= 1 && d < NC / 2) || (d == NC / 2 && anti)) return 1;
+    }
+  }
+  return 0;
+}
+
 // Partial-slot bytes of rank 0 (the largest share) if all of its rows were held at once (one
 // band): Pi + Px (the split segments' extra parts) + Pj + Pd (3 elements per body per slot),
 // the node sums it sends (nn x 3 per body of the run) and the ones it receives (NN x 3 per own

@@ -18,6 +18,7 @@
 //     ranks; a rank owns whole row blocks by mpi.c:184-187's remainder rule).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "gravsim.h"
 #include "gs_common.h"
@@ -542,23 +543,30 @@ __device__ __forceinline__ void push_leaves(TreeAcc<T, C>& t, int lo, int n, Lea
 // d = X - A + wrap lies in [1, NC/2], so only the antipodal row (d = NC/2) needs the shell
 // test; row A's partial sits (H - 1) x 3 x kSymC elements after row A - 1's. The loads of U
 // rows are issued ahead of their ordered adds.
-template <typename T, int C>
+// (A: the accumulated type, T or a vector of V consecutive bodies' T, loaded as one 16-byte
+// access: the reduce kernels' vector forms; every body's sum keeps its order)
+template <typename A, typename T>
+__device__ __forceinline__ A ld(const T* p) {
+  return *reinterpret_cast<const A*>(p);
+}
+
+template <typename T, int C, typename A = T>
 __device__ __forceinline__ void pj_range_add(const SymArgs& a, int A_lo, int A_hi, int X,
                                              int wrap, const T* pjc, int64_t comp_stride,
-                                             T* out) {
+                                             A* out) {
   constexpr int U = 8;
   const int64_t step = (int64_t)(a.H - 1) * 3 * kSymC;
   const T* p0 = pjc + ((int64_t)(A_lo - a.a0 - a.band0) * a.H + (X - A_lo + wrap - 1)) * 3 * kSymC;
   for (int A0 = A_lo; A0 < A_hi; A0 += U, p0 += U * step) {
-    T v[U][C];
+    A v[U][C];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int A = A0 + u;
-      const int d = X - A + wrap;
-      const bool ok = A < A_hi && (d != a.NC / 2 || shell_len(A, a.NC) == a.NC / 2);
+      const int Ar = A0 + u;
+      const int d = X - Ar + wrap;
+      const bool ok = Ar < A_hi && (d != a.NC / 2 || shell_len(Ar, a.NC) == a.NC / 2);
       const T* p = p0 + u * step;
 #pragma unroll
-      for (int k = 0; k < C; ++k) v[u][k] = ok ? p[k * comp_stride] : T(0);
+      for (int k = 0; k < C; ++k) v[u][k] = ok ? ld<A>(p + k * comp_stride) : A(0);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u)
@@ -572,17 +580,17 @@ __device__ __forceinline__ void pj_range_add(const SymArgs& a, int A_lo, int A_h
 // NC/2 rows, at most two linear pieces, visited in ascending order. Skipping the other rows
 // keeps the bits of adding +0.0 for them (a sum started at +0.0 never becomes -0.0) and
 // halves the loop.
-template <typename T, int C>
+template <typename T, int C, typename A = T>
 __device__ __forceinline__ void pj_row_sum(const SymArgs& a, int A_lo, int A_hi, int X,
-                                           const T* pjc, int64_t comp_stride, T* out) {
+                                           const T* pjc, int64_t comp_stride, A* out) {
 #pragma unroll
-  for (int k = 0; k < C; ++k) out[k] = T(0);
+  for (int k = 0; k < C; ++k) out[k] = A(0);
   const int s0 = X - a.NC / 2;  // the shell rows of X: [s0, X - 1] cyclically
   if (s0 >= 0) {
-    pj_range_add<T, C>(a, max(A_lo, s0), min(A_hi, X), X, 0, pjc, comp_stride, out);
+    pj_range_add<T, C, A>(a, max(A_lo, s0), min(A_hi, X), X, 0, pjc, comp_stride, out);
   } else {
-    pj_range_add<T, C>(a, A_lo, min(A_hi, X), X, 0, pjc, comp_stride, out);
-    pj_range_add<T, C>(a, max(A_lo, s0 + a.NC), A_hi, X, a.NC, pjc, comp_stride, out);
+    pj_range_add<T, C, A>(a, A_lo, min(A_hi, X), X, 0, pjc, comp_stride, out);
+    pj_range_add<T, C, A>(a, max(A_lo, s0 + a.NC), A_hi, X, a.NC, pjc, comp_stride, out);
   }
 }
 
@@ -661,6 +669,50 @@ __global__ __launch_bounds__(256) void sym_node_reduce_kernel(SymArgs a) {
   o[2 * nlq] = r[2];
 }
 
+// The same, one component per thread (blockIdx.z) and V = 16 / sizeof(T) consecutive bodies
+// per thread as one 16-byte access per row: the per-body sums and their order are the scalar
+// kernel's (same bits); 4-byte loads left the node reduce at ~4 TB/s (1M: 0.68 ms for 3.2 GB).
+template <typename T>
+__global__ __launch_bounds__(256) void sym_node_reduce_vec_kernel(SymArgs a) {
+  constexpr int V = 16 / (int)sizeof(T);
+  using A = T __attribute__((ext_vector_type(V)));
+  const int k3 = (int)blockIdx.z;
+  const int64_t nb = (int64_t)a.real_chunks * kSymC;
+  const int64_t tx = ((int64_t)blockIdx.x * 256 + threadIdx.x) * V;
+  if (a.x_count > 0 && tx >= a.x_count) return;
+  int64_t x = a.x_lo + tx;
+  if (x >= (int64_t)a.NC * kSymC) x -= (int64_t)a.NC * kSymC;  // (a cyclic range of ranks)
+  if (x >= nb) return;
+  const int X = (int)(x / kSymC), c = (int)(x % kSymC);
+  const int own_lo = a.blk_lo[a.rank], own_hi = a.blk_lo[a.rank + 1];
+  int lo = own_lo, l = sym_dyadic_level(lo, own_hi);
+  for (int k = 0; k < (int)blockIdx.y; ++k) {
+    lo += 1 << l;
+    l = sym_dyadic_level(lo, own_hi);
+  }
+  TreeAcc<A, 1> t;
+  t.pos = 0;
+  const T* Bb = static_cast<const T*>(a.Bbuf);
+  const T* pjc = static_cast<const T*>(a.Pj) + k3 * kSymC + c;
+  auto leaf = [&](int b, A* v) {
+    if (Bb) {
+      v[0] = ld<A>(Bb + (int64_t)(b - own_lo) * 3 * nb + (int64_t)k3 * nb + x);
+    } else {
+      const int A_lo = b * a.RB, A_hi = min((b + 1) * a.RB, a.real_chunks);
+      pj_row_sum<T, 1, A>(a, A_lo, max(A_lo, A_hi), X, pjc, kSymC, v);
+    }
+  };
+  push_leaves(t, lo, 1 << l, leaf);
+  A r[1];
+  t.result(r);
+  const int q = sym_row_owner(a, X);
+  const int64_t bq = (int64_t)a.blk_lo[q] * a.RB * kSymC;
+  const int64_t nlq = (int64_t)(a.blk_lo[q + 1] - a.blk_lo[q]) * a.RB * kSymC;
+  T* o = static_cast<T*>(a.Sbuf) + (int64_t)a.nn * 3 * bq + (int64_t)blockIdx.y * 3 * nlq +
+         (int64_t)k3 * nlq + (x - bq);
+  *reinterpret_cast<A*>(o) = r[0];
+}
+
 // S(x) for an own body: every rank's nodes in global order, merged into the full tree; the
 // other ranks' from Rbuf[node][3][n_local] (received), this rank's own nodes straight from
 // its Sbuf block (they never leave the GPU: no copy on the comm stream's critical path).
@@ -689,15 +741,15 @@ __device__ __forceinline__ void sym_tree_all(const SymArgs& a, int64_t li, T* S)
 // The split segments [s, segs) of band row br added to acc in segment order, each as
 // (((part 0 + part 1) + part 2) + ...): part 0 from Pi (p: this body and component's Pi
 // column), parts 1 .. Np-1 from Px (off: the body and component offset within a slot).
-template <typename T>
-__device__ __forceinline__ T split_parts_add(const SymArgs& a, int br, int s, int segs,
-                                             int64_t off, const T* p, T acc) {
+template <typename T, typename A = T>
+__device__ __forceinline__ A split_parts_add(const SymArgs& a, int br, int s, int segs,
+                                             int64_t off, const T* p, A acc) {
   const T* px =
       static_cast<const T*>(a.Px) + (int64_t)br * a.Kr * (a.Np - 1) * 3 * kSymC + off;
   for (; s < segs; ++s) {
     const int sp = s - (a.S - a.Kr);
-    T t = p[(int64_t)s * 3 * kSymC];
-    for (int q = 0; q + 1 < a.Np; ++q) t += px[((int64_t)sp * (a.Np - 1) + q) * 3 * kSymC];
+    A t = ld<A>(p + (int64_t)s * 3 * kSymC);
+    for (int q = 0; q + 1 < a.Np; ++q) t += ld<A>(px + ((int64_t)sp * (a.Np - 1) + q) * 3 * kSymC);
     acc += t;
   }
   return acc;
@@ -736,6 +788,44 @@ __global__ __launch_bounds__(256) void sym_row_reduce_kernel(SymArgs a) {
   for (; s < ns; ++s) acc += __builtin_nontemporal_load(p + (int64_t)s * 3 * kSymC);
   if (s < segs) acc = split_parts_add(a, br, s, segs, k * kSymC + c, p, acc);
   static_cast<T*>(a.Ti)[(int64_t)k * a.n_local + (int64_t)(a.band0 + br) * kSymC + c] = acc;
+}
+
+// The same, V = 16 / sizeof(T) consecutive bodies per thread as one 16-byte access per slot
+// (same sums, same order per body: same bits).
+template <typename T>
+__global__ __launch_bounds__(256) void sym_row_reduce_vec_kernel(SymArgs a) {
+  constexpr int V = 16 / (int)sizeof(T);
+  using A = T __attribute__((ext_vector_type(V)));
+  const int64_t b = ((int64_t)blockIdx.x * 256 + threadIdx.x) * V;  // first body in the band
+  if (b >= (int64_t)a.band_rows * kSymC) return;
+  const int br = (int)(b / kSymC), c = (int)(b % kSymC);
+  const int k = blockIdx.y;  // component
+  const int Ar = a.a0 + a.band0 + br;
+  if ((int64_t)Ar * kSymC >= a.n_real) return;  // all-ghost row
+  const T* __restrict__ pd = static_cast<const T*>(a.Pd) + (int64_t)br * a.D * 3 * kSymC +
+                             k * kSymC + c;
+  A acc = ld<A>(pd);
+  for (int q = 1; q < a.D; ++q) acc += ld<A>(pd + q * 3 * kSymC);
+  const int h = shell_len(Ar, a.NC);
+  const int segs = (16 * h + a.L - 1) / a.L;
+  const T* __restrict__ p = static_cast<const T*>(a.Pi) + (int64_t)br * a.S * 3 * kSymC +
+                            k * kSymC + c;
+  const int ns = min(segs, a.S - a.Kr);
+  constexpr int U = 8;
+  int s = 0;
+  for (; s + U <= ns; s += U) {
+    A v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      v[u] = __builtin_nontemporal_load(reinterpret_cast<const A*>(p + (int64_t)(s + u) * 3 * kSymC));
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc += v[u];
+  }
+  for (; s < ns; ++s)
+    acc += __builtin_nontemporal_load(reinterpret_cast<const A*>(p + (int64_t)s * 3 * kSymC));
+  if (s < segs) acc = split_parts_add<T, A>(a, br, s, segs, k * kSymC + c, p, acc);
+  *reinterpret_cast<A*>(static_cast<T*>(a.Ti) + (int64_t)k * a.n_local +
+                        (int64_t)(a.band0 + br) * kSymC + c) = acc;
 }
 
 // a = Ti + S (the canonical tree over all ranks' nodes), then kick-drift (cuda.cu:73-76,
@@ -949,12 +1039,29 @@ hipError_t launch_sym_block_reduce(const SymArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
+// GRAVSIM_REDUCE_VEC=0 keeps the scalar (one body per thread) reduce kernels for A/B; both
+// give the same bits.
+static bool reduce_vec() {
+  static const bool on = [] {
+    const char* v = getenv("GRAVSIM_REDUCE_VEC");
+    return !(v && v[0] == '0');
+  }();
+  return on;
+}
+
 hipError_t launch_sym_node_reduce(const SymArgs& a, hipStream_t s) {
   // leaves from Pj need every own row in the slots (one band), else from Bbuf
   if (!a.Bbuf && (a.band0 != 0 || a.band_rows != a.rows)) return hipErrorInvalidValue;
   const int64_t nb = (int64_t)a.real_chunks * kSymC;
   const int64_t bodies = a.x_count > 0 ? a.x_count : nb;
   if (bodies <= 0) return hipSuccess;
+  if (reduce_vec()) {
+    const int64_t per = 256 * (a.fp64 ? 2 : 4);
+    const dim3 grid((unsigned)((bodies + per - 1) / per), (unsigned)a.nn, 3);
+    if (a.fp64) hipLaunchKernelGGL(sym_node_reduce_vec_kernel<double>, grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL(sym_node_reduce_vec_kernel<float>, grid, dim3(256), 0, s, a);
+    return hipGetLastError();
+  }
   const dim3 grid((unsigned)((bodies + 255) / 256), (unsigned)a.nn);
   if (a.fp64) hipLaunchKernelGGL(sym_node_reduce_kernel<double>, grid, dim3(256), 0, s, a);
   else hipLaunchKernelGGL(sym_node_reduce_kernel<float>, grid, dim3(256), 0, s, a);
@@ -963,6 +1070,13 @@ hipError_t launch_sym_node_reduce(const SymArgs& a, hipStream_t s) {
 
 hipError_t launch_sym_row_reduce(const SymArgs& a, hipStream_t s) {
   const int64_t bodies = (int64_t)a.band_rows * kSymC;
+  if (reduce_vec()) {
+    const int64_t per = 256 * (a.fp64 ? 2 : 4);
+    const dim3 grid((unsigned)((bodies + per - 1) / per), 3);
+    if (a.fp64) hipLaunchKernelGGL(sym_row_reduce_vec_kernel<double>, grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL(sym_row_reduce_vec_kernel<float>, grid, dim3(256), 0, s, a);
+    return hipGetLastError();
+  }
   const dim3 grid((unsigned)((bodies + 255) / 256), 3);
   if (a.fp64) hipLaunchKernelGGL(sym_row_reduce_kernel<double>, grid, dim3(256), 0, s, a);
   else hipLaunchKernelGGL(sym_row_reduce_kernel<float>, grid, dim3(256), 0, s, a);

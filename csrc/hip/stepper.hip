@@ -84,7 +84,10 @@ size_t gather_bytes(const gs_stepper* s) {
   return (size_t)(s->L.n_pad - s->L.n_local) * row_bytes(s);
 }
 size_t exchange_bytes(const gs_stepper* s) {
-  return (size_t)(s->sym_NN - s->nn[s->cfg.rank]) * 3 * s->L.n_local * s->esz;
+  size_t nodes = 0;  // the other ranks' nodes this rank receives (live pairs only)
+  for (int q = 0; q < s->cfg.nranks; ++q)
+    if (q != s->cfg.rank && s->pair_live(q, s->cfg.rank)) nodes += (size_t)s->nn[q];
+  return nodes * 3 * s->L.n_local * s->esz;
 }
 
 
@@ -212,6 +215,13 @@ int ensure_sym(gs_stepper* s) {
     s->uniform = s->uniform && s->rcnt[q] == s->rcnt[0];
   }
   for (int q = 0; q <= P && q < 9; ++q) s->blk_lo[q] = gs::sym_blk_lo(s->sym_B, P, q);
+  s->live.assign((size_t)P * P, 1);
+  for (int q = 0; q < P; ++q)
+    for (int d = 0; d < P; ++d) {
+      const int32_t v = gs_sym_pair_live(s->L.n_pad, P, q, d);
+      if (v < 0) return -1;
+      s->live[(size_t)q * P + d] = (char)v;
+    }
   const size_t nl = (size_t)s->L.n_local, rows = nl / gs::kSymC;
   const size_t e = s->esz;
   // Rows per band: the partial slots of one band stay within the budget: half of the free

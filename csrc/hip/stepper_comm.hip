@@ -155,6 +155,10 @@ int ring_xfer_rccl(gs_stepper* s, int cur, int sub) {
 // land in the Sbuf blocks of those ranks).
 static int node_reduce_dests(gs_stepper* s, const gs::SymArgs& a0, int kb, int ke) {
   const int P = s->cfg.nranks, r = s->cfg.rank;
+  // (destinations whose sums are +0.0 by the geometry at either end of the range are left out:
+  // their node sums are never sent)
+  while (kb < ke && !s->pair_live(r, (r + kb) % P)) ++kb;
+  while (ke > kb && !s->pair_live(r, (r + ke - 1) % P)) --ke;
   gs::SymArgs a = a0;
   a.x_lo = s->rbeg[(r + kb) % P];
   a.x_count = 0;
@@ -193,20 +197,28 @@ int sym_reduce_exchange(gs_stepper* s, const gs::SymArgs& a0, bool* exchanged) {
           if (comm_dead(s)) return -1;
           if (comm_wait_comp(s, s->ev_stage[g], kSyncStage0 + g)) return -1;
           if (first) GS_MARK(x0, x, s->s_comm);
+          // Pairs whose node sums are +0.0 by the geometry (gs_sym_pair_live) are neither sent
+          // nor received: the receiver's slots keep the +0.0 they were zeroed to (both sides
+          // evaluate the same table, so every send still meets its receive).
           if (s->emulate) {
             // the bytes this rank receives in this stage, read from its receive buffer
             size_t bytes = 0;
-            for (int k = kb; k < ke; ++k) bytes += (size_t)s->nn[(r - k + P) % P] * 3 * nl * e;
+            for (int k = kb; k < ke; ++k) {
+              const int src = (r - k + P) % P;
+              if (s->pair_live(src, r)) bytes += (size_t)s->nn[src] * 3 * nl * e;
+            }
             if (comm_model(s, s->sym_R, bytes, (size_t)s->sym_NN * 3 * nl * e)) return -1;
           } else {
             const ncclDataType_t dt = s->esz == 8 ? ncclFloat64 : ncclFloat32;
             GS_NCCL(ncclGroupStart());
             for (int k = kb; k < ke; ++k) {
               const int q = (r + k) % P, src = (r - k + P) % P;
-              GS_NCCL(ncclSend(s->sym_S + my * 3 * (size_t)s->rbeg[q] * e, my * 3 * s->rcnt[q],
-                               dt, q, s->comm, s->s_comm));
-              GS_NCCL(ncclRecv(s->sym_R + (size_t)s->nbase[src] * 3 * nl * e,
-                               (size_t)s->nn[src] * 3 * nl, dt, src, s->comm, s->s_comm));
+              if (s->pair_live(r, q))
+                GS_NCCL(ncclSend(s->sym_S + my * 3 * (size_t)s->rbeg[q] * e,
+                                 my * 3 * s->rcnt[q], dt, q, s->comm, s->s_comm));
+              if (s->pair_live(src, r))
+                GS_NCCL(ncclRecv(s->sym_R + (size_t)s->nbase[src] * 3 * nl * e,
+                                 (size_t)s->nn[src] * 3 * nl, dt, src, s->comm, s->s_comm));
             }
             GS_NCCL(ncclGroupEnd());
           }

@@ -105,6 +105,9 @@ double gs_sym_imbalance(int64_t n_pad, int32_t nranks);
 // Shell length of chunk row A (the antipodal pairs split between rows by parity).
 int32_t gs_sym_shell_len(int32_t A, int32_t NC);
 // Unit order of the gated sym launch for one rank (see layout.cpp); returns the entry count.
+// 1 if rank src's node sums for rank dst's bodies can be nonzero, 0 if the geometry makes
+// them +0.0 for every body (the exchange skips that send), -1 on bad arguments.
+int32_t gs_sym_pair_live(int64_t n_pad, int32_t nranks, int32_t src, int32_t dst);
 int64_t gs_sym_unit_map(int64_t n_pad, int32_t rank, int32_t nranks, int64_t fill,
                         int32_t* out, int64_t cap);
 // ... with the last kr shell segments of every row split into np part units at the end (bit

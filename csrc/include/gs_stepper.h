@@ -112,6 +112,12 @@ struct gs_stepper {
   std::vector<int64_t> rbeg, rcnt;
   std::vector<int32_t> nn, nbase;
   bool uniform = true;  // every rank owns the same body count (P | B: ncclAllGather)
+  // live[src * P + dst]: rank src's node sums for rank dst's bodies can be nonzero
+  // (gs_sym_pair_live); the exchange skips the other pairs (their sums are +0.0)
+  std::vector<char> live;
+  bool pair_live(int src, int dst) const {
+    return live.empty() || live[(size_t)src * cfg.nranks + dst] != 0;
+  }
   hipEvent_t ev_sym = nullptr;
   hipEvent_t ev_stage[2] = {nullptr, nullptr};  // node sums of an exchange stage reduced
   // Per-rank emulation with modeled collectives (GRAVSIM_EMU_COMM GB/s > 0): every all-gather

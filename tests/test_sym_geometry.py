@@ -291,3 +291,29 @@ def test_split_geometry_matches_native(n_pad):
     lib = _native.cpu_lib()
     assert (lib.gs_sym_split_segments(n_pad), lib.gs_sym_split_parts(n_pad)) == \
         partition.sym_split(n_pad)
+
+
+@pytest.mark.parametrize("n_pad", [65536, 1 << 20])
+@pytest.mark.parametrize("P", [2, 3, 4, 5, 6, 7, 8])
+def test_pair_live_matches_the_shell_definition(n_pad, P):
+    """gs_sym_pair_live: rank src's node sums for rank dst are +0.0 for every body (the
+    exchange skips the pair) exactly when no row of src's holds a chunk of dst's in its shell
+    (distance 1 .. NC/2 - 1, or NC/2 for the rows that take the antipodal chunk). At P = 8 the
+    three far-side destinations of every rank are dead: 24 of 56 sends skipped."""
+    lib, g = _geo(n_pad)
+    NC = g["NC"]
+    takes = np.array([lib.gs_sym_shell_len(A, NC) == NC // 2 for A in range(NC)])
+    rows = [partition.sym_rank_rows(n_pad, P, q) for q in range(P)]
+    dead = 0
+    for src in range(P):
+        A = np.arange(rows[src][0], rows[src][0] + rows[src][1])[:, None]
+        for dst in range(P):
+            X = np.arange(rows[dst][0], rows[dst][0] + rows[dst][1])[None, :]
+            d = (X - A) % NC
+            want = src == dst or bool((((d >= 1) & (d < NC // 2)) |
+                                       ((d == NC // 2) & takes[A])).any())
+            got = lib.gs_sym_pair_live(n_pad, P, src, dst)
+            assert got == int(want), (src, dst)
+            dead += not want
+    if P == 8:
+        assert dead == 24
