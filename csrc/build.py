@@ -198,6 +198,12 @@ def build_graph_event_probe(force: bool = False) -> Path:
         _run([hipcc(), "-O2", "-std=c++17", f"--offload-arch={ARCH}", str(GEV_SRC), "-o",
               str(tmp)])
         os.replace(tmp, GEV_BIN)
+    lib = OUT / "libgraph_event_probe.so"  # the same probe, loaded under torch's HIP runtime
+    if GEV_SRC.exists() and (force or _stale(lib, [GEV_SRC])):
+        tmp = lib.with_suffix(".so.tmp")
+        _run([hipcc(), "-O2", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-shared",
+              "-DGS_PROBE_LIB", str(GEV_SRC), "-o", str(tmp)])
+        os.replace(tmp, lib)
     return GEV_BIN
 
 

@@ -430,14 +430,41 @@ __device__ __forceinline__ void force_sym_entry(SymArgs a) {
     __shared__ unsigned next_s;
     const int cap = (int)blockIdx.x < a.first_wave ? 1 : a.unit_cap;
     unsigned done = 0;  // audit weight of the units this workgroup ran: one add at exit
-    for (int k = 0; k < cap; ++k) {
+    if (a.prefetch) {
+      // The next unit's index is taken when this unit starts, so its fetch latency hides
+      // behind the unit (short units at small N pay it once per ~2 tiles) - except near the
+      // end of the queue (fewer than first_wave units left), where a unit held back behind a
+      // running one would lengthen the launch tail: there it is taken after the unit.
       if (threadIdx.x == 0)
         next_s = __hip_atomic_fetch_add(a.work, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __syncthreads();
-      const unsigned u = next_s;
-      if (u >= (unsigned)a.n_units) break;
-      done += force_sym_body<T, EXACT>(a, (int)u);
-      __syncthreads();  // next_s and the LDS tiles are rewritten by the next unit
+      unsigned u = next_s;
+      for (int k = 0; k < cap && u < (unsigned)a.n_units; ++k) {
+        const bool more = k + 1 < cap;
+        const bool early = more && u + (unsigned)a.first_wave < (unsigned)a.n_units;
+        unsigned nx = ~0u;
+        if (threadIdx.x == 0 && early)
+          nx = __hip_atomic_fetch_add(a.work, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        done += force_sym_body<T, EXACT>(a, (int)u);
+        __syncthreads();  // every wave is done with next_s and the LDS tiles
+        if (threadIdx.x == 0)
+          next_s = early ? nx
+                   : more ? __hip_atomic_fetch_add(a.work, 1u, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT)
+                          : ~0u;
+        __syncthreads();
+        u = next_s;
+      }
+    } else {
+      for (int k = 0; k < cap; ++k) {
+        if (threadIdx.x == 0)
+          next_s = __hip_atomic_fetch_add(a.work, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
+        const unsigned u = next_s;
+        if (u >= (unsigned)a.n_units) break;
+        done += force_sym_body<T, EXACT>(a, (int)u);
+        __syncthreads();  // next_s and the LDS tiles are rewritten by the next unit
+      }
     }
     if (done) audit_unit(a, done);
   } else {

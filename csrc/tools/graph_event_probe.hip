@@ -59,9 +59,12 @@ __global__ void kern_c(const unsigned* counter, unsigned* seen, unsigned long lo
   }
 }
 
-int main(int argc, char** argv) {
-  const int iters = argc > 1 ? atoi(argv[1]) : 6;
-  const unsigned long long spin_ticks = 100ull * (argc > 2 ? atoi(argv[2]) : 20000);  // us
+// Also built as a shared library (-DGS_PROBE_LIB -shared): scripts/graph_event_probe_torch.py
+// loads it into a process that imported torch first, so the probe runs on the HIP runtime the
+// stepper itself runs on there (torch bundles its own libamdhip64.so.7, and the stepper's
+// DT_NEEDED soname resolves to that already-loaded copy), not on /opt/rocm's.
+extern "C" int gs_graph_event_probe(int iters, int spin_us) {
+  const unsigned long long spin_ticks = 100ull * (unsigned long long)spin_us;
   hipStream_t s1, s2;
   CHECK(hipStreamCreateWithFlags(&s1, hipStreamNonBlocking));
   CHECK(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
@@ -243,5 +246,18 @@ int main(int argc, char** argv) {
   }
   CHECK(hipGraphExecDestroy(x));
   CHECK(hipGraphDestroy(g));
+  {
+    int rt = 0, drv = 0;
+    (void)hipRuntimeGetVersion(&rt);
+    (void)hipDriverGetVersion(&drv);
+    printf("{\"hip_runtime_version\": %d, \"hip_driver_version\": %d}\n", rt, drv);
+  }
+  fflush(stdout);
   return bad_value ? 2 : 0;
 }
+
+#ifndef GS_PROBE_LIB
+int main(int argc, char** argv) {
+  return gs_graph_event_probe(argc > 1 ? atoi(argv[1]) : 6, argc > 2 ? atoi(argv[2]) : 20000);
+}
+#endif

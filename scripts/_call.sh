@@ -25,3 +25,6 @@ t=$(find $O/trace5 -name "*kernel_trace.csv" | head -1)
 python scripts/post_force_chain.py "$t" --print-steps 2 > $O/r5_chain_flags.txt
 head -1 $O/r5_chain_flags.txt
 timeout -k 10 300 python bench/unit_timeline.py --n 65536 --ranks 1 --out $O/ut65k_r5.npz > $O/ut65k_r5.txt 2>&1 && tail -1 $O/ut65k_r5.txt | cut -c1-300
+timeout -k 10 120 ./gravity-simulator-using-mpi-spark-and-cuda_amd/_native/graph_event_probe 4 5000 > $O/gev_standalone.txt 2>&1; echo "standalone rc=$?" >> $O/gev_standalone.txt
+timeout -k 10 180 python scripts/graph_event_probe_torch.py 4 5000 > $O/gev_torch.txt 2>&1; echo "torch rc=$?" >> $O/gev_torch.txt
+tail -4 $O/gev_standalone.txt $O/gev_torch.txt
