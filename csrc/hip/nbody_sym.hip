@@ -427,38 +427,43 @@ __device__ __forceinline__ void force_sym_entry(SymArgs a) {
     // throughput, bench/unit_timeline.py) sets the launch's end. Here a workgroup keeps taking
     // units (up to unit_cap; the first wave one each, so slots free up early for a concurrent
     // collective), and faster XCDs simply take more. Same units, same slots: same bits.
+    // The first wave (the resident slots) takes one unit each, unit = blockIdx.x, with no
+    // fetch: 512 workgroups pulling one counter at launch start serialise on it (one word
+    // saturates at ~88 dequeues/us, MI355X_MICROARCH.md dequeue row: ~6 us per launch, 0.9 %
+    // of a 65K step). Every later fetch returns first_wave + the counter's next value, so the
+    // counter still starts at 0 (the memset / finalize re-arm) and every unit runs once.
     __shared__ unsigned next_s;
-    const int cap = (int)blockIdx.x < a.first_wave ? 1 : a.unit_cap;
+    const bool fw = (int)blockIdx.x < a.first_wave;
+    const int cap = fw ? 1 : a.unit_cap;
+    const unsigned base = (unsigned)a.first_wave;
+    auto fetch = [&]() -> unsigned {
+      return base + __hip_atomic_fetch_add(a.work, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    };
     unsigned done = 0;  // audit weight of the units this workgroup ran: one add at exit
-    if (a.prefetch) {
+    if (fw) {
+      if ((int)blockIdx.x < a.n_units) done += force_sym_body<T, EXACT>(a, (int)blockIdx.x);
+    } else if (a.prefetch) {
       // The next unit's index is taken when this unit starts, so its fetch latency hides
       // behind the unit (short units at small N pay it once per ~2 tiles) - except near the
       // end of the queue (fewer than first_wave units left), where a unit held back behind a
       // running one would lengthen the launch tail: there it is taken after the unit.
-      if (threadIdx.x == 0)
-        next_s = __hip_atomic_fetch_add(a.work, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (threadIdx.x == 0) next_s = fetch();
       __syncthreads();
       unsigned u = next_s;
       for (int k = 0; k < cap && u < (unsigned)a.n_units; ++k) {
         const bool more = k + 1 < cap;
-        const bool early = more && u + (unsigned)a.first_wave < (unsigned)a.n_units;
+        const bool early = more && u + base < (unsigned)a.n_units;
         unsigned nx = ~0u;
-        if (threadIdx.x == 0 && early)
-          nx = __hip_atomic_fetch_add(a.work, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (threadIdx.x == 0 && early) nx = fetch();
         done += force_sym_body<T, EXACT>(a, (int)u);
         __syncthreads();  // every wave is done with next_s and the LDS tiles
-        if (threadIdx.x == 0)
-          next_s = early ? nx
-                   : more ? __hip_atomic_fetch_add(a.work, 1u, __ATOMIC_RELAXED,
-                                                   __HIP_MEMORY_SCOPE_AGENT)
-                          : ~0u;
+        if (threadIdx.x == 0) next_s = early ? nx : more ? fetch() : ~0u;
         __syncthreads();
         u = next_s;
       }
     } else {
       for (int k = 0; k < cap; ++k) {
-        if (threadIdx.x == 0)
-          next_s = __hip_atomic_fetch_add(a.work, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (threadIdx.x == 0) next_s = fetch();
         __syncthreads();
         const unsigned u = next_s;
         if (u >= (unsigned)a.n_units) break;

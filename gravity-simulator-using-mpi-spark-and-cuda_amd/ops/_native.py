@@ -93,7 +93,7 @@ def _declare_common(lib) -> None:
     _sig(lib, "gs_sym_rank_rows", c_int32, [c_int64, c_int32, c_int32, POINTER(c_int32),
                                             POINTER(c_int32)])
     _sig(lib, "gs_sym_nodes", c_int32, [c_int64, c_int32, c_int32] + [POINTER(c_int32)] * 5)
-    _sig(lib, "gs_sym_pair_live", c_int32, [c_int64, c_int32, c_int32, c_int32])
+    _sig(lib, "gs_sym_pair_live", c_int32, [c_int64, c_int32, c_int32, c_int32], optional=True)
     _sig(lib, "gs_sym_unit_map", c_int64, [c_int64, c_int32, c_int32, c_int64,
                                            POINTER(c_int32), c_int64])
     _sig(lib, "gs_sym_unit_map_ring", c_int64, [c_int64, c_int32, c_int32, c_int64,

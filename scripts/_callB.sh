@@ -32,3 +32,9 @@ for P in sorted({r["P"] for r in rows}):
     ms=max(r["ms_per_step"] for r in rows if r["P"]==P)
     print(P, round(ms,3), round(base/(P*ms),4))
 PY
+C=1048576:fp32:auto:1,1048576:fp32:auto:8,1048576:fp32:auto:7
+timeout -k 10 400 python -u scripts/state_hash.py --steps 2 --cases $C > $O/hash2_new.jsonl 2>&1 || exit 1
+grep -h sha $O/hash2_new.jsonl
+timeout -k 10 120 ./gravity-simulator-using-mpi-spark-and-cuda_amd/_native/graph_event_probe 4 5000 > $O/gev_standalone.txt 2>&1; echo "standalone rc=$?" >> $O/gev_standalone.txt
+timeout -k 10 180 python scripts/graph_event_probe_torch.py 4 5000 > $O/gev_torch.txt 2>&1; echo "torch rc=$?" >> $O/gev_torch.txt
+tail -4 $O/gev_standalone.txt $O/gev_torch.txt
