@@ -442,11 +442,13 @@ __device__ __forceinline__ void force_sym_entry(SymArgs a) {
     unsigned done = 0;  // audit weight of the units this workgroup ran: one add at exit
     if (fw) {
       if ((int)blockIdx.x < a.n_units) done += force_sym_body<T, EXACT>(a, (int)blockIdx.x);
-    } else if (a.prefetch) {
+    } else {
       // The next unit's index is taken when this unit starts, so its fetch latency hides
       // behind the unit (short units at small N pay it once per ~2 tiles) - except near the
       // end of the queue (fewer than first_wave units left), where a unit held back behind a
       // running one would lengthen the launch tail: there it is taken after the unit.
+      // (65K 0.708-0.710 vs 0.713-0.714 ms, 1M 163.78-163.91 vs 164.16-164.32 ms, alternating
+      // on one box: profiles/r5_prefetch_ab.jsonl.)
       if (threadIdx.x == 0) next_s = fetch();
       __syncthreads();
       unsigned u = next_s;
@@ -460,15 +462,6 @@ __device__ __forceinline__ void force_sym_entry(SymArgs a) {
         if (threadIdx.x == 0) next_s = early ? nx : more ? fetch() : ~0u;
         __syncthreads();
         u = next_s;
-      }
-    } else {
-      for (int k = 0; k < cap; ++k) {
-        if (threadIdx.x == 0) next_s = fetch();
-        __syncthreads();
-        const unsigned u = next_s;
-        if (u >= (unsigned)a.n_units) break;
-        done += force_sym_body<T, EXACT>(a, (int)u);
-        __syncthreads();  // next_s and the LDS tiles are rewritten by the next unit
       }
     }
     if (done) audit_unit(a, done);
@@ -575,8 +568,10 @@ __device__ __forceinline__ void push_leaves(TreeAcc<T, C>& t, int lo, int n, Lea
 // d = X - A + wrap lies in [1, NC/2], so only the antipodal row (d = NC/2) needs the shell
 // test; row A's partial sits (H - 1) x 3 x kSymC elements after row A - 1's. The loads of U
 // rows are issued ahead of their ordered adds.
-// (A: the accumulated type, T or a vector of V consecutive bodies' T, loaded as one 16-byte
-// access: the reduce kernels' vector forms; every body's sum keeps its order)
+// (A: the accumulated type; T here. A 16-byte vector of consecutive bodies' T, one load per
+// row, gave the same bits but measured no faster at 1M on one GPU and slower at the 1M / 8
+// rank shape (node reduce 53 + 41 + 31 vs 52 + 37 + 19 us, row reduce 97-99 vs 96 us:
+// profiles/r5_reduce_vec_ab.jsonl), so the kernels load one body per thread.)
 template <typename A, typename T>
 __device__ __forceinline__ A ld(const T* p) {
   return *reinterpret_cast<const A*>(p);
@@ -701,50 +696,6 @@ __global__ __launch_bounds__(256) void sym_node_reduce_kernel(SymArgs a) {
   o[2 * nlq] = r[2];
 }
 
-// The same, one component per thread (blockIdx.z) and V = 16 / sizeof(T) consecutive bodies
-// per thread as one 16-byte access per row: the per-body sums and their order are the scalar
-// kernel's (same bits); 4-byte loads left the node reduce at ~4 TB/s (1M: 0.68 ms for 3.2 GB).
-template <typename T>
-__global__ __launch_bounds__(256) void sym_node_reduce_vec_kernel(SymArgs a) {
-  constexpr int V = 16 / (int)sizeof(T);
-  using A = T __attribute__((ext_vector_type(V)));
-  const int k3 = (int)blockIdx.z;
-  const int64_t nb = (int64_t)a.real_chunks * kSymC;
-  const int64_t tx = ((int64_t)blockIdx.x * 256 + threadIdx.x) * V;
-  if (a.x_count > 0 && tx >= a.x_count) return;
-  int64_t x = a.x_lo + tx;
-  if (x >= (int64_t)a.NC * kSymC) x -= (int64_t)a.NC * kSymC;  // (a cyclic range of ranks)
-  if (x >= nb) return;
-  const int X = (int)(x / kSymC), c = (int)(x % kSymC);
-  const int own_lo = a.blk_lo[a.rank], own_hi = a.blk_lo[a.rank + 1];
-  int lo = own_lo, l = sym_dyadic_level(lo, own_hi);
-  for (int k = 0; k < (int)blockIdx.y; ++k) {
-    lo += 1 << l;
-    l = sym_dyadic_level(lo, own_hi);
-  }
-  TreeAcc<A, 1> t;
-  t.pos = 0;
-  const T* Bb = static_cast<const T*>(a.Bbuf);
-  const T* pjc = static_cast<const T*>(a.Pj) + k3 * kSymC + c;
-  auto leaf = [&](int b, A* v) {
-    if (Bb) {
-      v[0] = ld<A>(Bb + (int64_t)(b - own_lo) * 3 * nb + (int64_t)k3 * nb + x);
-    } else {
-      const int A_lo = b * a.RB, A_hi = min((b + 1) * a.RB, a.real_chunks);
-      pj_row_sum<T, 1, A>(a, A_lo, max(A_lo, A_hi), X, pjc, kSymC, v);
-    }
-  };
-  push_leaves(t, lo, 1 << l, leaf);
-  A r[1];
-  t.result(r);
-  const int q = sym_row_owner(a, X);
-  const int64_t bq = (int64_t)a.blk_lo[q] * a.RB * kSymC;
-  const int64_t nlq = (int64_t)(a.blk_lo[q + 1] - a.blk_lo[q]) * a.RB * kSymC;
-  T* o = static_cast<T*>(a.Sbuf) + (int64_t)a.nn * 3 * bq + (int64_t)blockIdx.y * 3 * nlq +
-         (int64_t)k3 * nlq + (x - bq);
-  *reinterpret_cast<A*>(o) = r[0];
-}
-
 // S(x) for an own body: every rank's nodes in global order, merged into the full tree; the
 // other ranks' from Rbuf[node][3][n_local] (received), this rank's own nodes straight from
 // its Sbuf block (they never leave the GPU: no copy on the comm stream's critical path).
@@ -820,44 +771,6 @@ __global__ __launch_bounds__(256) void sym_row_reduce_kernel(SymArgs a) {
   for (; s < ns; ++s) acc += __builtin_nontemporal_load(p + (int64_t)s * 3 * kSymC);
   if (s < segs) acc = split_parts_add(a, br, s, segs, k * kSymC + c, p, acc);
   static_cast<T*>(a.Ti)[(int64_t)k * a.n_local + (int64_t)(a.band0 + br) * kSymC + c] = acc;
-}
-
-// The same, V = 16 / sizeof(T) consecutive bodies per thread as one 16-byte access per slot
-// (same sums, same order per body: same bits).
-template <typename T>
-__global__ __launch_bounds__(256) void sym_row_reduce_vec_kernel(SymArgs a) {
-  constexpr int V = 16 / (int)sizeof(T);
-  using A = T __attribute__((ext_vector_type(V)));
-  const int64_t b = ((int64_t)blockIdx.x * 256 + threadIdx.x) * V;  // first body in the band
-  if (b >= (int64_t)a.band_rows * kSymC) return;
-  const int br = (int)(b / kSymC), c = (int)(b % kSymC);
-  const int k = blockIdx.y;  // component
-  const int Ar = a.a0 + a.band0 + br;
-  if ((int64_t)Ar * kSymC >= a.n_real) return;  // all-ghost row
-  const T* __restrict__ pd = static_cast<const T*>(a.Pd) + (int64_t)br * a.D * 3 * kSymC +
-                             k * kSymC + c;
-  A acc = ld<A>(pd);
-  for (int q = 1; q < a.D; ++q) acc += ld<A>(pd + q * 3 * kSymC);
-  const int h = shell_len(Ar, a.NC);
-  const int segs = (16 * h + a.L - 1) / a.L;
-  const T* __restrict__ p = static_cast<const T*>(a.Pi) + (int64_t)br * a.S * 3 * kSymC +
-                            k * kSymC + c;
-  const int ns = min(segs, a.S - a.Kr);
-  constexpr int U = 8;
-  int s = 0;
-  for (; s + U <= ns; s += U) {
-    A v[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-      v[u] = __builtin_nontemporal_load(reinterpret_cast<const A*>(p + (int64_t)(s + u) * 3 * kSymC));
-#pragma unroll
-    for (int u = 0; u < U; ++u) acc += v[u];
-  }
-  for (; s < ns; ++s)
-    acc += __builtin_nontemporal_load(reinterpret_cast<const A*>(p + (int64_t)s * 3 * kSymC));
-  if (s < segs) acc = split_parts_add<T, A>(a, br, s, segs, k * kSymC + c, p, acc);
-  *reinterpret_cast<A*>(static_cast<T*>(a.Ti) + (int64_t)k * a.n_local +
-                        (int64_t)(a.band0 + br) * kSymC + c) = acc;
 }
 
 // a = Ti + S (the canonical tree over all ranks' nodes), then kick-drift (cuda.cu:73-76,
@@ -1071,29 +984,12 @@ hipError_t launch_sym_block_reduce(const SymArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-// GRAVSIM_REDUCE_VEC=0 keeps the scalar (one body per thread) reduce kernels for A/B; both
-// give the same bits.
-static bool reduce_vec() {
-  static const bool on = [] {
-    const char* v = getenv("GRAVSIM_REDUCE_VEC");
-    return !(v && v[0] == '0');
-  }();
-  return on;
-}
-
 hipError_t launch_sym_node_reduce(const SymArgs& a, hipStream_t s) {
   // leaves from Pj need every own row in the slots (one band), else from Bbuf
   if (!a.Bbuf && (a.band0 != 0 || a.band_rows != a.rows)) return hipErrorInvalidValue;
   const int64_t nb = (int64_t)a.real_chunks * kSymC;
   const int64_t bodies = a.x_count > 0 ? a.x_count : nb;
   if (bodies <= 0) return hipSuccess;
-  if (reduce_vec()) {
-    const int64_t per = 256 * (a.fp64 ? 2 : 4);
-    const dim3 grid((unsigned)((bodies + per - 1) / per), (unsigned)a.nn, 3);
-    if (a.fp64) hipLaunchKernelGGL(sym_node_reduce_vec_kernel<double>, grid, dim3(256), 0, s, a);
-    else hipLaunchKernelGGL(sym_node_reduce_vec_kernel<float>, grid, dim3(256), 0, s, a);
-    return hipGetLastError();
-  }
   const dim3 grid((unsigned)((bodies + 255) / 256), (unsigned)a.nn);
   if (a.fp64) hipLaunchKernelGGL(sym_node_reduce_kernel<double>, grid, dim3(256), 0, s, a);
   else hipLaunchKernelGGL(sym_node_reduce_kernel<float>, grid, dim3(256), 0, s, a);
@@ -1102,13 +998,6 @@ hipError_t launch_sym_node_reduce(const SymArgs& a, hipStream_t s) {
 
 hipError_t launch_sym_row_reduce(const SymArgs& a, hipStream_t s) {
   const int64_t bodies = (int64_t)a.band_rows * kSymC;
-  if (reduce_vec()) {
-    const int64_t per = 256 * (a.fp64 ? 2 : 4);
-    const dim3 grid((unsigned)((bodies + per - 1) / per), 3);
-    if (a.fp64) hipLaunchKernelGGL(sym_row_reduce_vec_kernel<double>, grid, dim3(256), 0, s, a);
-    else hipLaunchKernelGGL(sym_row_reduce_vec_kernel<float>, grid, dim3(256), 0, s, a);
-    return hipGetLastError();
-  }
   const dim3 grid((unsigned)((bodies + 255) / 256), 3);
   if (a.fp64) hipLaunchKernelGGL(sym_row_reduce_kernel<double>, grid, dim3(256), 0, s, a);
   else hipLaunchKernelGGL(sym_row_reduce_kernel<float>, grid, dim3(256), 0, s, a);

@@ -185,7 +185,6 @@ gs::SymArgs sym_args(gs_stepper* s, int cur) {
     a.work = s->gate_buf + 4;
     a.unit_cap = s->dyn_cap;
     a.first_wave = s->sym_first_wave;
-    a.prefetch = s->sym_prefetch ? 1 : 0;
   }
   a.trace_defer0 = (int32_t)s->utrace_main;
   a.audit = s->audit;
@@ -748,7 +747,6 @@ int gs_stepper_create(const gs_config* cfg, gs_stepper** out) {
     if (got >= 3) s->emu_wgs = wgs;
   }
   if (s->esz == 8) s->dyn_cap = 4;  // fp64: 512K 101.9-102.0 ms at 4 vs 102.0-102.5 at 2
-  if (const char* v = getenv("GRAVSIM_SYM_PREFETCH")) s->sym_prefetch = atoi(v) != 0;
   if (const char* v = getenv("GRAVSIM_FAULT_SKIP_UNITS")) s->fault_skip = (unsigned)atoi(v);
   // GRAVSIM_SYNC=events: the multi-rank step orders its streams by hipEvents (and replays a
   // segmented plan) instead of device counters (flag sync, one graph per period)

@@ -122,7 +122,6 @@ struct SymArgs {
   // on the stream before every such launch. n_units: set by the launcher.
   unsigned* work;
   int32_t n_units, unit_cap, first_wave;
-  int32_t prefetch;  // take the next unit's index when a unit starts (GRAVSIM_SYM_PREFETCH)
   // work[0] is already 0 on this stream (the fused tail kernel that ran after the previous
   // dynamic launch re-armed it): the launcher skips its memset.
   int32_t work_zero;

@@ -136,7 +136,6 @@ struct gs_stepper {
   // keeps 4 (no gain from 2: profiles/r4s2_fp64_i8_dyncap_ab.jsonl).
   int dyn_cap = 3;
   int sym_first_wave = 0;
-  bool sym_prefetch = false;  // GRAVSIM_SYM_PREFETCH: the next unit's index taken early (A/B)
   int64_t utrace_main = 0;               // entries of the main launch (deferred ones follow)
   size_t emu_cap = 0;
   double clk_khz = 100000.0;  // device wall clock (wall_clock64) rate

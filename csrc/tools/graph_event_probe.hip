@@ -65,6 +65,13 @@ __global__ void kern_c(const unsigned* counter, unsigned* seen, unsigned long lo
 // DT_NEEDED soname resolves to that already-loaded copy), not on /opt/rocm's.
 extern "C" int gs_graph_event_probe(int iters, int spin_us) {
   const unsigned long long spin_ticks = 100ull * (unsigned long long)spin_us;
+  {
+    int rt = 0, drv = 0;
+    (void)hipRuntimeGetVersion(&rt);
+    (void)hipDriverGetVersion(&drv);
+    printf("{\"hip_runtime_version\": %d, \"hip_driver_version\": %d}\n", rt, drv);
+    fflush(stdout);
+  }
   hipStream_t s1, s2;
   CHECK(hipStreamCreateWithFlags(&s1, hipStreamNonBlocking));
   CHECK(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
@@ -246,12 +253,6 @@ extern "C" int gs_graph_event_probe(int iters, int spin_us) {
   }
   CHECK(hipGraphExecDestroy(x));
   CHECK(hipGraphDestroy(g));
-  {
-    int rt = 0, drv = 0;
-    (void)hipRuntimeGetVersion(&rt);
-    (void)hipDriverGetVersion(&drv);
-    printf("{\"hip_runtime_version\": %d, \"hip_driver_version\": %d}\n", rt, drv);
-  }
   fflush(stdout);
   return bad_value ? 2 : 0;
 }

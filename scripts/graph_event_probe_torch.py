@@ -21,7 +21,8 @@ def main() -> int:
 
     torch.cuda.init()  # torch's HIP runtime is now the process's
     maps = sorted({ln.split()[-1] for ln in open("/proc/self/maps") if "amdhip64" in ln})
-    print('{"amdhip64_mapped": %s}' % ([m for m in maps],), flush=True)
+    print('{"amdhip64_mapped": %s, "torch_version_hip": "%s"}' % ([m for m in maps],
+                                                                  torch.version.hip), flush=True)
     lib = ctypes.CDLL(os.path.join(ROOT, "gravity-simulator-using-mpi-spark-and-cuda_amd",
                                    "_native", "libgraph_event_probe.so"))
     iters = int(sys.argv[1]) if len(sys.argv) > 1 else 6
