@@ -127,7 +127,8 @@ def test_ring_stages_same_bits_and_defer(hip, monkeypatch):
 
 def test_phase_split_reports_modeled_comm(hip, monkeypatch):
     """Phase events: the modeled gather (7/8 of 262144 x 16 B = 3.67 MB at 8 GB/s + 15 us =
-    474 us) and exchange (2.75 MB: 359 us) show up as comm time; with overlap 0 the compute
+    474 us) and exchange (the 4 of 7 peers whose node sums can be nonzero, gs_sym_pair_live:
+    1.57 MB in two stages, 197 + 2 x 15 = 227 us) show up as comm time; with overlap 0 the compute
     stream stalls for the whole gather. With overlap 3 the local units run beside it, the
     remote units that find it unfinished are deferred to the launch behind the gather event,
     and the step is no slower."""
@@ -146,7 +147,7 @@ def test_phase_split_reports_modeled_comm(hip, monkeypatch):
     for p in (p0, p3):
         assert p["steps"] == 4
         assert p["gather_ms"] > 0.9 * 0.474, p
-        assert p["exchange_ms"] > 0.9 * 0.359, p
+        assert p["exchange_ms"] > 0.9 * 0.227, p
     assert p0["exposed_gather_ms"] > 0.8 * p0["gather_ms"], p0
     assert p0["deferred_units"] == 0, p0
     assert p3["exposed_gather_ms"] < p0["exposed_gather_ms"], (p0, p3)
