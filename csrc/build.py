@@ -4,14 +4,15 @@
   libgravsim_hip.so : hipcc --offload-arch=gfx950, kernels + Stepper runtime, links RCCL.
   gravsim_bench     : standalone C++ driver (csrc/tools/gravsim_main.cpp), no Python needed.
 
-  probes (--tools)  : microbench, sym_probe, trans_probe, graph_event_probe (csrc/tools/*.hip);
+  probes (--tools)  : microbench, sym_probe, trans_probe, graph_event_probe, overlap_probe
+                      (csrc/tools/*.hip);
                       measurement instruments, never part of the production build: a broken
                       probe cannot fail build_all() (the driver's build check).
 
 Outputs land in <package>/_native/ so they travel with the repo snapshot to the GPU box.
 Rebuilds only when a source or header is newer than the target. Usage:
     python csrc/build.py [--force] [--only cpu|hip|tool|microbench|sym_probe|trans_probe|
-                          graph_event_probe] [--tools]
+                          graph_event_probe|overlap_probe] [--tools]
 """
 from __future__ import annotations
 
@@ -50,6 +51,8 @@ TRANS_SRC = CSRC / "tools" / "trans_probe.hip"
 TRANS_BIN = OUT / "trans_probe"
 GEV_SRC = CSRC / "tools" / "graph_event_probe.hip"
 GEV_BIN = OUT / "graph_event_probe"
+OVL_SRC = CSRC / "tools" / "overlap_probe.hip"
+OVL_BIN = OUT / "overlap_probe"
 
 
 def _stale(target: Path, deps: list[Path]) -> bool:
@@ -207,6 +210,17 @@ def build_graph_event_probe(force: bool = False) -> Path:
     return GEV_BIN
 
 
+def build_overlap_probe(force: bool = False) -> Path:
+    """Reduction-beside-force concurrency probe (csrc/tools/overlap_probe.hip)."""
+    OUT.mkdir(parents=True, exist_ok=True)
+    if OVL_SRC.exists() and (force or _stale(OVL_BIN, [OVL_SRC])):
+        tmp = OVL_BIN.with_suffix(".tmp")
+        _run([hipcc(), "-O3", "-std=c++17", f"--offload-arch={ARCH}", str(OVL_SRC), "-o",
+              str(tmp)])
+        os.replace(tmp, OVL_BIN)
+    return OVL_BIN
+
+
 def build_all(force: bool = False) -> None:
     """The production artefacts only: the CPU engine, the HIP library and gravsim_bench."""
     build_cpu(force)
@@ -220,13 +234,14 @@ def build_tools(force: bool = False) -> None:
     build_sym_probe(force)
     build_trans_probe(force)
     build_graph_event_probe(force)
+    build_overlap_probe(force)
 
 
 def main(argv: list[str] | None = None) -> int:
     ap = argparse.ArgumentParser(description=__doc__)
     ap.add_argument("--force", action="store_true")
     ap.add_argument("--only", choices=["cpu", "hip", "tool", "microbench", "sym_probe",
-                                          "trans_probe", "graph_event_probe"])
+                                          "trans_probe", "graph_event_probe", "overlap_probe"])
     ap.add_argument("--tools", action="store_true", help="also build the measurement probes")
     a = ap.parse_args(argv)
     if a.only == "cpu":
@@ -243,6 +258,8 @@ def main(argv: list[str] | None = None) -> int:
         build_trans_probe(a.force)
     elif a.only == "graph_event_probe":
         build_graph_event_probe(a.force)
+    elif a.only == "overlap_probe":
+        build_overlap_probe(a.force)
     else:
         build_all(a.force)
         if a.tools:

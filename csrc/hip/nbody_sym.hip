@@ -580,7 +580,19 @@ __device__ __forceinline__ A ld(const T* p) {
   return *reinterpret_cast<const A*>(p);
 }
 
-template <typename T, int C, typename A = T>
+// NT: non-temporal loads of Pj (read once per step). At the 1M / 8 rank shape the node reduce
+// stages take 38 instead of 43 us each (chain 257 against 274 us). On one GPU the node reduce
+// drops 677 -> 632 us but the row reduce grows 590 -> 704 us whether it runs before or after
+// it (same row-reduce code): the plain loads of the node reduce are what evict the force
+// launch's dirty lines from the memory-side cache, and without them the row reduce pays the
+// write-backs. One GPU keeps plain loads (profiles/r5_nt_loads_ab.txt).
+template <bool NT, typename A, typename T>
+__device__ __forceinline__ A ld_pj(const T* p) {
+  if constexpr (NT && std::is_same<A, T>::value) return __builtin_nontemporal_load(p);
+  else return *reinterpret_cast<const A*>(p);
+}
+
+template <typename T, int C, typename A = T, bool NT = false>
 __device__ __forceinline__ void pj_range_add(const SymArgs& a, int A_lo, int A_hi, int X,
                                              int wrap, const T* pjc, int64_t comp_stride,
                                              A* out) {
@@ -596,7 +608,7 @@ __device__ __forceinline__ void pj_range_add(const SymArgs& a, int A_lo, int A_h
       const bool ok = Ar < A_hi && (d != a.NC / 2 || shell_len(Ar, a.NC) == a.NC / 2);
       const T* p = p0 + u * step;
 #pragma unroll
-      for (int k = 0; k < C; ++k) v[u][k] = ok ? ld<A>(p + k * comp_stride) : A(0);
+      for (int k = 0; k < C; ++k) v[u][k] = ok ? ld_pj<NT, A>(p + k * comp_stride) : A(0);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u)
@@ -610,17 +622,17 @@ __device__ __forceinline__ void pj_range_add(const SymArgs& a, int A_lo, int A_h
 // NC/2 rows, at most two linear pieces, visited in ascending order. Skipping the other rows
 // keeps the bits of adding +0.0 for them (a sum started at +0.0 never becomes -0.0) and
 // halves the loop.
-template <typename T, int C, typename A = T>
+template <typename T, int C, typename A = T, bool NT = false>
 __device__ __forceinline__ void pj_row_sum(const SymArgs& a, int A_lo, int A_hi, int X,
                                            const T* pjc, int64_t comp_stride, A* out) {
 #pragma unroll
   for (int k = 0; k < C; ++k) out[k] = A(0);
   const int s0 = X - a.NC / 2;  // the shell rows of X: [s0, X - 1] cyclically
   if (s0 >= 0) {
-    pj_range_add<T, C, A>(a, max(A_lo, s0), min(A_hi, X), X, 0, pjc, comp_stride, out);
+    pj_range_add<T, C, A, NT>(a, max(A_lo, s0), min(A_hi, X), X, 0, pjc, comp_stride, out);
   } else {
-    pj_range_add<T, C, A>(a, A_lo, min(A_hi, X), X, 0, pjc, comp_stride, out);
-    pj_range_add<T, C, A>(a, max(A_lo, s0 + a.NC), A_hi, X, a.NC, pjc, comp_stride, out);
+    pj_range_add<T, C, A, NT>(a, A_lo, min(A_hi, X), X, 0, pjc, comp_stride, out);
+    pj_range_add<T, C, A, NT>(a, max(A_lo, s0 + a.NC), A_hi, X, a.NC, pjc, comp_stride, out);
   }
 }
 
@@ -656,8 +668,13 @@ __global__ __launch_bounds__(256) void sym_block_reduce_kernel(SymArgs a) {
 // Latency-bound (a chain of row loads per body): 3 components per thread amortise the row
 // bookkeeping, U = 8 rows of loads are in flight, and only the NC/2 rows that can hold the
 // body in their shell are visited (pj_row_sum).
-template <typename T>
+template <typename T, bool NT>
 __global__ __launch_bounds__(256) void sym_node_reduce_kernel(SymArgs a) {
+  if (a.sig && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {  // (SymArgs::sig)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_fetch_add(a.sig, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
   const int64_t nb = (int64_t)a.real_chunks * kSymC;
   const int64_t tx = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (a.x_count > 0 && tx >= a.x_count) return;
@@ -683,7 +700,7 @@ __global__ __launch_bounds__(256) void sym_node_reduce_kernel(SymArgs a) {
       v[2] = p[2 * nb];
     } else {
       const int A_lo = b * a.RB, A_hi = min((b + 1) * a.RB, a.real_chunks);
-      pj_row_sum<T, 3>(a, A_lo, max(A_lo, A_hi), X, pjc, kSymC, v);
+      pj_row_sum<T, 3, T, NT>(a, A_lo, max(A_lo, A_hi), X, pjc, kSymC, v);
     }
   };
   push_leaves(t, lo, 1 << l, leaf);
@@ -994,8 +1011,14 @@ hipError_t launch_sym_node_reduce(const SymArgs& a, hipStream_t s) {
   const int64_t bodies = a.x_count > 0 ? a.x_count : nb;
   if (bodies <= 0) return hipSuccess;
   const dim3 grid((unsigned)((bodies + 255) / 256), (unsigned)a.nn);
-  if (a.fp64) hipLaunchKernelGGL(sym_node_reduce_kernel<double>, grid, dim3(256), 0, s, a);
-  else hipLaunchKernelGGL(sym_node_reduce_kernel<float>, grid, dim3(256), 0, s, a);
+  const bool nt = a.P > 1;  // (ld_pj)
+  if (a.fp64) {
+    if (nt) hipLaunchKernelGGL((sym_node_reduce_kernel<double, true>), grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((sym_node_reduce_kernel<double, false>), grid, dim3(256), 0, s, a);
+  } else {
+    if (nt) hipLaunchKernelGGL((sym_node_reduce_kernel<float, true>), grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((sym_node_reduce_kernel<float, false>), grid, dim3(256), 0, s, a);
+  }
   return hipGetLastError();
 }
 

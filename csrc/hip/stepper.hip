@@ -425,6 +425,9 @@ int sym_force(gs_stepper* s, gs::SymArgs a, bool overlap_gather, bool exchange =
     // (reduce phase at 1M 1533-1592 us per step against 1342-1381 in sequence;
     // profiles/r3_reduce_fork_split_ab.txt).
     if (a.Bbuf) GS_HIP(gs::launch_sym_block_reduce(a, s->s_comp));  // the band's leaves
+    // (The row reduce on a second stream beside the node stages and the exchange measured
+    // worse at rank 7 of 8, 1M: chain 650 against 257 us, step 22.1-22.2 against 21.4-21.5 ms,
+    // profiles/r5_nt_loads_ab.txt; it stays in sequence.)
     bool exchanged = false;
     if (last) {
       if (exchange) {

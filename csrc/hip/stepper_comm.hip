@@ -153,17 +153,24 @@ int ring_xfer_rccl(gs_stepper* s, int cur, int sub) {
 // Node reduce for the bodies of destination ranks r + kb .. r + ke - 1 (mod P): consecutive
 // ranks own consecutive rows, so that is one cyclic body range and one launch (their sums
 // land in the Sbuf blocks of those ranks).
-static int node_reduce_dests(gs_stepper* s, const gs::SymArgs& a0, int kb, int ke) {
+// `sig`: a flag-sync counter to raise before this work (SymArgs::sig; raised by a signal
+// kernel instead when there is no launch to carry it).
+static int node_reduce_dests(gs_stepper* s, const gs::SymArgs& a0, int kb, int ke,
+                             unsigned* sig = nullptr) {
   const int P = s->cfg.nranks, r = s->cfg.rank;
   // (destinations whose sums are +0.0 by the geometry at either end of the range are left out:
   // their node sums are never sent)
   while (kb < ke && !s->pair_live(r, (r + kb) % P)) ++kb;
   while (ke > kb && !s->pair_live(r, (r + ke - 1) % P)) --ke;
   gs::SymArgs a = a0;
-  a.x_lo = s->rbeg[(r + kb) % P];
+  a.x_lo = kb < ke ? s->rbeg[(r + kb) % P] : 0;
   a.x_count = 0;
   for (int k = kb; k < ke; ++k) a.x_count += s->rcnt[(r + k) % P];
-  if (a.x_count == 0) return 0;
+  if (a.x_count == 0) {
+    if (sig) GS_HIP(gs::launch_sync_signal(sig, nullptr, s->s_comp));
+    return 0;
+  }
+  a.sig = sig;
   GS_HIP(gs::launch_sym_node_reduce(a, s->s_comp));
   return 0;
 }
@@ -186,9 +193,13 @@ int sym_reduce_exchange(gs_stepper* s, const gs::SymArgs& a0, bool* exchanged) {
   const int stages = P - 1 < 2 ? P - 1 : 2;
   const int k1 = (P - 1) / 3 > 1 ? (P - 1) / 3 : 1;
   const int k_lo[3] = {1, stages == 2 ? 1 + k1 : P, P};
+  // With flag sync a stage's signal rides on the next node reduce launch (SymArgs::sig).
+  unsigned* pending = nullptr;
   for (int g = 0; g < stages; ++g) {
-    if (node_reduce_dests(s, a0, k_lo[g], k_lo[g + 1])) return -1;
-    if (comp_signal(s, s->ev_stage[g], kSyncStage0 + g)) return -1;
+    if (node_reduce_dests(s, a0, k_lo[g], k_lo[g + 1], pending)) return -1;
+    pending = nullptr;
+    if (fsync(s)) pending = s->sync_buf + 2 * (kSyncStage0 + g);
+    else if (comp_signal(s, s->ev_stage[g], kSyncStage0 + g)) return -1;
     const int kb = k_lo[g], ke = k_lo[g + 1];
     const bool first = g == 0, last = g + 1 == stages;
     if (comm_do(s, [s, g, kb, ke, first, last]() -> int {
@@ -230,7 +241,7 @@ int sym_reduce_exchange(gs_stepper* s, const gs::SymArgs& a0, bool* exchanged) {
         }))
       return -1;
   }
-  if (node_reduce_dests(s, a0, 0, 1)) return -1;  // the own sums, last
+  if (node_reduce_dests(s, a0, 0, 1, pending)) return -1;  // the own sums, last
   // (a live 1-rank communicator: nothing to exchange, and nothing for finalize to wait for)
   *exchanged = stages > 0;
   return 0;

@@ -129,6 +129,11 @@ struct SymArgs {
   // must be rows x (S + D + (Np - 1) Kr) whatever the launch split, deferral or fetch order (a
   // split segment run whole counts its Np parts).
   unsigned long long* audit;
+  // Flag sync (comm_model.hip sync_signal_kernel): a counter the node reduce launch raises at
+  // its start, for the exchange stage whose sums the launch before it produced (that launch has
+  // completed and released its writes at the kernel boundary). Saves the one-lane signal
+  // kernel between two stages. nullptr: none.
+  unsigned* sig;
 };
 
 hipError_t launch_force_sym(const SymArgs& a, hipStream_t s);
