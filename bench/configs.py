@@ -86,7 +86,7 @@ def main() -> int:
     import gravsim  # noqa: F401
 
     if 2 in want:
-        ms, lay, _ = gpu_run(65536, "fp32", 50, 5)
+        ms, lay, _ = gpu_run(65536, "fp32", 300, 20)  # (bench.py --n 65536 --steps 300)
         rows.append(dict(config="#2 65,536 fp32", gpus=1, how="measured", ms_per_step=ms,
                          body_updates_per_s=65536 / (ms * 1e-3), layout=lay))
         print(json.dumps(rows[-1]), flush=True)
