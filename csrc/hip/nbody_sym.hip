@@ -415,11 +415,30 @@ __device__ __forceinline__ unsigned force_sym_body(const SymArgs& a, int b) {
 // with a stride of the grid. The list is usually empty (the gather finished long before the
 // remote units were dispatched), and a grid of one workgroup per possible unit would cost more
 // than the gather it hides. The main kernel is unchanged by it (same registers, no spills).
-template <typename T, bool EXACT, bool DEFER, bool DYN>
+template <typename T, bool EXACT, bool DEFER, bool DYN, bool PF>
 __device__ __forceinline__ void force_sym_entry(SymArgs a) {
   if constexpr (!DEFER && !DYN) {
     const unsigned w = force_sym_body<T, EXACT>(a, blockIdx.x);
     if (w) audit_unit(a, w);
+  } else if constexpr (DYN && !PF) {
+    // Many units per slot (1M on one GPU: ~300): every workgroup fetches each unit when it
+    // needs it (round 4's loop). The first-wave / early-fetch form below measured 0.1 %
+    // slower there (163.08-163.34 vs 163.01-163.11 ms, alternating) and 1.1 % faster at 65K
+    // (0.696-0.697 vs 0.704 ms), 1M / 8 per rank even (profiles/r5_dyn_loop_ab.jsonl); the
+    // launcher picks by units per resident slot.
+    __shared__ unsigned next_s;
+    const int cap = (int)blockIdx.x < a.first_wave ? 1 : a.unit_cap;
+    unsigned done = 0;  // audit weight of the units this workgroup ran: one add at exit
+    for (int k = 0; k < cap; ++k) {
+      if (threadIdx.x == 0)
+        next_s = __hip_atomic_fetch_add(a.work, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __syncthreads();
+      const unsigned u = next_s;
+      if (u >= (unsigned)a.n_units) break;
+      done += force_sym_body<T, EXACT>(a, (int)u);
+      __syncthreads();  // next_s and the LDS tiles are rewritten by the next unit
+    }
+    if (done) audit_unit(a, done);
   } else if constexpr (DYN) {
     // Dynamic fetch: unit indices in launch order from a device counter. The hardware hands
     // workgroups to the 8 XCDs in a fixed rotation, so a static unit per workgroup gives every
@@ -483,14 +502,14 @@ __device__ __forceinline__ void force_sym_entry(SymArgs a) {
 }
 
 // (separate instantiations: the static kernels keep their own register allocation)
-template <bool EXACT, bool DEFER = false, bool DYN = false>
+template <bool EXACT, bool DEFER = false, bool DYN = false, bool PF = false>
 __global__ __launch_bounds__(Geo<float>::kThreads) void force_sym_kernel_f32(SymArgs a) {
-  force_sym_entry<float, EXACT, DEFER, DYN>(a);
+  force_sym_entry<float, EXACT, DEFER, DYN, PF>(a);
 }
-template <bool EXACT, bool DEFER = false, bool DYN = false>
+template <bool EXACT, bool DEFER = false, bool DYN = false, bool PF = false>
 __global__ __launch_bounds__(Geo<double>::kThreads)
 void force_sym_kernel_f64(SymArgs a) {
-  force_sym_entry<double, EXACT, DEFER, DYN>(a);
+  force_sym_entry<double, EXACT, DEFER, DYN, PF>(a);
 }
 
 // ---- canonical j-side reduction ----------------------------------------------------------
@@ -965,23 +984,30 @@ hipError_t launch_force_sym_t(const SymArgs& a, hipStream_t s) {
   }
   const dim3 grid(g), block(Geo<T>::kThreads);
   const bool d = a.units == 7, y = b.work != nullptr;
+  // the first-wave / early-fetch form of the dynamic loop up to 128 units per resident slot
+  // (force_sym_entry)
+  const bool pf = y && (int64_t)units <= 128LL * (a.first_wave > 0 ? a.first_wave : 1);
   if constexpr (sizeof(T) == 8) {
     if (a.exact) {
       if (d) hipLaunchKernelGGL((force_sym_kernel_f64<true, true>), grid, block, 0, s, b);
+      else if (pf) hipLaunchKernelGGL((force_sym_kernel_f64<true, false, true, true>), grid, block, 0, s, b);
       else if (y) hipLaunchKernelGGL((force_sym_kernel_f64<true, false, true>), grid, block, 0, s, b);
       else hipLaunchKernelGGL((force_sym_kernel_f64<true>), grid, block, 0, s, b);
     } else {
       if (d) hipLaunchKernelGGL((force_sym_kernel_f64<false, true>), grid, block, 0, s, b);
+      else if (pf) hipLaunchKernelGGL((force_sym_kernel_f64<false, false, true, true>), grid, block, 0, s, b);
       else if (y) hipLaunchKernelGGL((force_sym_kernel_f64<false, false, true>), grid, block, 0, s, b);
       else hipLaunchKernelGGL((force_sym_kernel_f64<false>), grid, block, 0, s, b);
     }
   } else {
     if (a.exact) {
       if (d) hipLaunchKernelGGL((force_sym_kernel_f32<true, true>), grid, block, 0, s, b);
+      else if (pf) hipLaunchKernelGGL((force_sym_kernel_f32<true, false, true, true>), grid, block, 0, s, b);
       else if (y) hipLaunchKernelGGL((force_sym_kernel_f32<true, false, true>), grid, block, 0, s, b);
       else hipLaunchKernelGGL((force_sym_kernel_f32<true>), grid, block, 0, s, b);
     } else {
       if (d) hipLaunchKernelGGL((force_sym_kernel_f32<false, true>), grid, block, 0, s, b);
+      else if (pf) hipLaunchKernelGGL((force_sym_kernel_f32<false, false, true, true>), grid, block, 0, s, b);
       else if (y) hipLaunchKernelGGL((force_sym_kernel_f32<false, false, true>), grid, block, 0, s, b);
       else hipLaunchKernelGGL((force_sym_kernel_f32<false>), grid, block, 0, s, b);
     }

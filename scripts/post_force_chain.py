@@ -19,8 +19,11 @@ def short(name: str) -> str:
 
 
 def is_main_force(n: str) -> bool:
-    # force_sym_kernel_f32<EXACT, DEFER, DYN>: every instance but the deferred-unit launch
-    return n.startswith("force_sym_kernel") and ", true, false>" not in n
+    # force_sym_kernel_f32<EXACT, DEFER, DYN[, PF]>: every instance but the deferred-unit launch
+    if not n.startswith("force_sym_kernel"):
+        return False
+    args = [t.strip() for t in n[n.index("<") + 1:n.index(">")].split(",")]
+    return not (len(args) > 1 and args[1] == "true")
 
 
 def main() -> int:

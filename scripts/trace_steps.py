@@ -13,6 +13,14 @@ def short(name: str) -> str:
     return n.replace("void ", "")
 
 
+def is_main_force(n: str) -> bool:
+    # force_sym_kernel_f32<EXACT, DEFER, DYN[, PF]>: every instance but the deferred-unit launch
+    if not n.startswith("force_sym_kernel"):
+        return False
+    args = [t.strip() for t in n[n.index("<") + 1:n.index(">")].split(",")]
+    return not (len(args) > 1 and args[1] == "true")
+
+
 def main(path: str) -> int:
     rows = list(csv.DictReader(open(path)))
     ks = sorted(((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_Name"]),
@@ -20,8 +28,7 @@ def main(path: str) -> int:
     # steps: from one main force launch to the next finalize
     steps, cur = [], None
     for s, e, n, st in ks:
-        if n.startswith("force_sym_kernel") and n.endswith("false>") and "true, true" not in n \
-                and (cur is None or cur.get("fin")):
+        if is_main_force(n) and (cur is None or cur.get("fin")):
             if cur and cur.get("fin"):
                 steps.append(cur)
             cur = {"k": []}
