@@ -453,7 +453,6 @@ __device__ __forceinline__ void force_sym_entry(SymArgs a) {
     // counter still starts at 0 (the memset / finalize re-arm) and every unit runs once.
     __shared__ unsigned next_s;
     const bool fw = (int)blockIdx.x < a.first_wave;
-    const int cap = fw ? 1 : a.unit_cap;
     const unsigned base = (unsigned)a.first_wave;
     auto fetch = [&]() -> unsigned {
       return base + __hip_atomic_fetch_add(a.work, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -462,7 +461,7 @@ __device__ __forceinline__ void force_sym_entry(SymArgs a) {
     // Two inlined copies of the unit body (first wave / fetch loop) on purpose: one call site
     // shrinks the code by half but measured 0.8 % slower at 65K and equal at 1M
     // (profiles/r5_ab_onebody_rejected.jsonl).
-    if (fw) {
+    if (fw && !a.persist) {
       if ((int)blockIdx.x < a.n_units) done += force_sym_body<T, EXACT>(a, (int)blockIdx.x);
     } else {
       // The next unit's index is taken when this unit starts, so its fetch latency hides
@@ -471,9 +470,11 @@ __device__ __forceinline__ void force_sym_entry(SymArgs a) {
       // running one would lengthen the launch tail: there it is taken after the unit.
       // (65K 0.708-0.710 vs 0.713-0.714 ms, 1M 163.78-163.91 vs 164.16-164.32 ms, alternating
       // on one box: profiles/r5_prefetch_ab.jsonl.)
-      if (threadIdx.x == 0) next_s = fetch();
+      // (persistent: every workgroup is in the first wave; its first unit is its blockIdx.x)
+      if (!fw && threadIdx.x == 0) next_s = fetch();
       __syncthreads();
-      unsigned u = next_s;
+      unsigned u = fw ? (unsigned)blockIdx.x : next_s;
+      const int cap = fw ? 0x7fffffff : a.unit_cap;
       for (int k = 0; k < cap && u < (unsigned)a.n_units; ++k) {
         const bool more = k + 1 < cap;
         const bool early = more && u + base < (unsigned)a.n_units;
@@ -979,14 +980,21 @@ hipError_t launch_force_sym_t(const SymArgs& a, hipStream_t s) {
     const int64_t rest = units - a.first_wave;
     const int64_t more = (5 * rest + 4LL * a.unit_cap - 1) / (4LL * a.unit_cap);
     g = (unsigned)(a.first_wave + (more < rest ? more : rest));
+    // Persistent workgroups only with many units per slot (1M on one GPU: 165.21-165.68 vs
+    // 165.49-166.00 ms against round 4's loop, alternating); at 65K the workgroup turnover
+    // measured faster (0.699-0.705 vs 0.715-0.727 ms), as did caps 2-4 against 6-8
+    // (profiles/r5_persist_ab.jsonl, r5_cap_small_n.jsonl).
+    b.persist = a.persist && (int64_t)units > 128LL * a.first_wave ? 1 : 0;
+    if (b.persist) g = (unsigned)a.first_wave;
   } else {
     b.work = nullptr;  // static: unit = blockIdx.x
+    b.persist = 0;
   }
   const dim3 grid(g), block(Geo<T>::kThreads);
   const bool d = a.units == 7, y = b.work != nullptr;
   // the first-wave / early-fetch form of the dynamic loop up to 128 units per resident slot
   // (force_sym_entry)
-  const bool pf = y && (int64_t)units <= 128LL * (a.first_wave > 0 ? a.first_wave : 1);
+  const bool pf = y && (b.persist || (int64_t)units <= 128LL * (a.first_wave > 0 ? a.first_wave : 1));
   if constexpr (sizeof(T) == 8) {
     if (a.exact) {
       if (d) hipLaunchKernelGGL((force_sym_kernel_f64<true, true>), grid, block, 0, s, b);

@@ -185,6 +185,7 @@ gs::SymArgs sym_args(gs_stepper* s, int cur) {
     a.work = s->gate_buf + 4;
     a.unit_cap = s->dyn_cap;
     a.first_wave = s->sym_first_wave;
+    a.persist = s->cfg.nranks == 1 && !xcomm(s) && s->sym_persist ? 1 : 0;
   }
   a.trace_defer0 = (int32_t)s->utrace_main;
   a.audit = s->audit;
@@ -1069,6 +1070,13 @@ int gs_stepper_set_schedule(gs_stepper* s, int32_t use_graph, int32_t dyn_cap) {
 int gs_stepper_set_tuning(gs_stepper* s, int32_t first_wave, int32_t fused_tail) {
   if (first_wave > 0) s->sym_first_wave = first_wave;
   if (fused_tail >= 0) s->fuse_tail = fused_tail ? 1 : 0;
+  s->work_zero = false;
+  drop_graphs(s);
+  return 0;
+}
+
+int gs_stepper_set_persist(gs_stepper* s, int32_t on) {
+  s->sym_persist = on != 0;
   s->work_zero = false;
   drop_graphs(s);
   return 0;

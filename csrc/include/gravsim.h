@@ -209,6 +209,9 @@ int gs_stepper_set_schedule(gs_stepper* s, int32_t use_graph, int32_t dyn_cap);
 // small runs fetch dynamically too); fused_tail 1 / 0 forces the one-rank fused reduction
 // tail / the three-kernel tail (default: fused up to 256K bodies). Same bits either way.
 int gs_stepper_set_tuning(gs_stepper* s, int32_t first_wave, int32_t fused_tail);
+// One-rank sym launches with persistent workgroups (1, the default) or round 4's workgroup
+// turnover (0): same units and slots, same bits.
+int gs_stepper_set_persist(gs_stepper* s, int32_t on);
 // Re-resolve the force path with a new cutoff mode (0 auto, 1 exact select, 2 fast core).
 int gs_stepper_set_cutoff_mode(gs_stepper* s, int32_t mode);
 // Work audit of the sym schedule: force units completed since the last reset (waits for the

@@ -122,6 +122,10 @@ struct SymArgs {
   // on the stream before every such launch. n_units: set by the launcher.
   unsigned* work;
   int32_t n_units, unit_cap, first_wave;
+  // Persistent workgroups (one rank, no collective beside the launch): the grid is the
+  // resident slots only and every workgroup takes units until the queue is empty, so no
+  // workgroup exits early and no replacement has to be dispatched mid-launch.
+  int32_t persist;
   // work[0] is already 0 on this stream (the fused tail kernel that ran after the previous
   // dynamic launch re-armed it): the launcher skips its memset.
   int32_t work_zero;

@@ -136,6 +136,7 @@ struct gs_stepper {
   // keeps 4 (no gain from 2: profiles/r4s2_fp64_i8_dyncap_ab.jsonl).
   int dyn_cap = 3;
   int sym_first_wave = 0;
+  bool sym_persist = true;  // one-rank dynamic launches: persistent workgroups (SymArgs::persist)
   int64_t utrace_main = 0;               // entries of the main launch (deferred ones follow)
   size_t emu_cap = 0;
   double clk_khz = 100000.0;  // device wall clock (wall_clock64) rate

@@ -177,6 +177,7 @@ def hip_lib():
         _sig(lib, "gs_stepper_get_dyn_cap", c_int32, [S])
         _sig(lib, "gs_stepper_set_cutoff_mode", c_int32, [S, c_int32])
         _sig(lib, "gs_stepper_set_tuning", c_int32, [S, c_int32, c_int32])
+        _sig(lib, "gs_stepper_set_persist", c_int32, [S, c_int32], optional=True)
         _sig(lib, "gs_stepper_audit", c_int32, [S, POINTER(c_uint64), POINTER(c_uint64)])
         _sig(lib, "gs_stepper_audit_reset", c_int32, [S])
         _sig(lib, "gs_stepper_graph_info", c_int32, [S, POINTER(c_int32), POINTER(c_int32)])

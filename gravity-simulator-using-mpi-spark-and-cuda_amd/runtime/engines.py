@@ -227,13 +227,19 @@ class HipEngine:
         _native.check(self.lib, self.lib.gs_stepper_set_schedule(self._s, int(graph),
                                                                  int(dyn_cap)), "schedule")
 
-    def set_tuning(self, first_wave: int = 0, fused_tail: int = -1) -> None:
+    def set_tuning(self, first_wave: int = 0, fused_tail: int = -1, persist: int = -1) -> None:
         """Test / A-B tuning of the sym schedule, same bits either way: first_wave > 0 sets
         how many workgroups of a dynamic launch take one unit each (default: the resident
         slots); fused_tail 1 / 0 forces the one-rank fused reduction tail / the three-kernel
-        tail (default -1: fused up to 256K bodies)."""
+        tail (default -1: fused up to 256K bodies); persist 1 / 0: one-rank launches with
+        persistent workgroups (the default) / workgroups that exit after their cap."""
         _native.check(self.lib, self.lib.gs_stepper_set_tuning(self._s, int(first_wave),
                                                                int(fused_tail)), "tuning")
+        if persist >= 0:
+            if not hasattr(self.lib, "gs_stepper_set_persist"):
+                raise RuntimeError("set_tuning(persist=...): this native build has no persist mode")
+            _native.check(self.lib, self.lib.gs_stepper_set_persist(self._s, int(persist)),
+                          "persist")
 
     def set_cutoff_mode(self, mode: str) -> None:
         """Re-resolve the force path: auto | exact (reference hard-cutoff select) | fast."""

@@ -281,6 +281,34 @@ def test_sym_dynamic_unit_fetch_bitwise(hip, n, dtype, P, first_wave):
     assert np.array_equal(out[0].vel, out[1].vel)
 
 
+@pytest.mark.parametrize("n,dtype,first_wave", [
+    (65536, "fp32", 16),     # 4,352 units on 16 persistent workgroups
+    (262144, "fp32", 64),    # 16,640 units on 64
+    (40000, "fp32", 16),
+    (40000, "fp64", 8),
+])
+def test_sym_persistent_workgroups_bitwise(hip, n, dtype, first_wave):
+    """One rank: persistent workgroups (the grid is the first wave, each takes units until
+    the queue is empty; in force above 128 units per first-wave slot, so a small first wave
+    forces it here) run the same units into the same slots as workgroups that exit after
+    their cap: same bits, eager and replayed."""
+    from gravsim.runtime.engines import HipEngine
+
+    out = []
+    for persist in (0, 1):
+        e = HipEngine(SimConfig(n=n, dtype=dtype, device="gpu", mode="sym"))
+        e.set_tuning(first_wave=first_wave, persist=persist)
+        e.init_ics("solar+random", 29)
+        a = e.accel(step_path=True)
+        e.step(5)
+        e.sync()
+        out.append((a, e.state()))
+        e.close()
+    assert np.array_equal(out[0][0], out[1][0])
+    assert np.array_equal(out[0][1].pos, out[1][1].pos)
+    assert np.array_equal(out[0][1].vel, out[1][1].vel)
+
+
 @pytest.mark.parametrize("fused", ["0", "1"])
 def test_sym_graph_replays_rezero_unit_counter(hip, monkeypatch, fused):
     """A fresh engine whose first steps are hipGraph replays (no eager step or accel query
