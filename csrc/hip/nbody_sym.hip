@@ -689,14 +689,14 @@ __global__ __launch_bounds__(256) void sym_block_reduce_kernel(SymArgs a) {
 // bookkeeping, U = 8 rows of loads are in flight, and only the NC/2 rows that can hold the
 // body in their shell are visited (pj_row_sum).
 template <typename T, bool NT>
-__global__ __launch_bounds__(256) void sym_node_reduce_kernel(SymArgs a) {
-  if (a.sig && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {  // (SymArgs::sig)
+__device__ __forceinline__ void sym_node_reduce_body(const SymArgs& a, int bx, int by) {
+  if (a.sig && bx == 0 && by == 0 && threadIdx.x == 0) {  // (SymArgs::sig)
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __hip_atomic_fetch_add(a.sig, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   const int64_t nb = (int64_t)a.real_chunks * kSymC;
-  const int64_t tx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t tx = (int64_t)bx * 256 + threadIdx.x;
   if (a.x_count > 0 && tx >= a.x_count) return;
   int64_t x = a.x_lo + tx;
   if (x >= (int64_t)a.NC * kSymC) x -= (int64_t)a.NC * kSymC;  // (a cyclic range of ranks)
@@ -704,7 +704,7 @@ __global__ __launch_bounds__(256) void sym_node_reduce_kernel(SymArgs a) {
   const int X = (int)(x / kSymC), c = (int)(x % kSymC);
   const int own_lo = a.blk_lo[a.rank], own_hi = a.blk_lo[a.rank + 1];
   int lo = own_lo, l = sym_dyadic_level(lo, own_hi);
-  for (int k = 0; k < (int)blockIdx.y; ++k) {
+  for (int k = 0; k < by; ++k) {
     lo += 1 << l;
     l = sym_dyadic_level(lo, own_hi);
   }
@@ -729,11 +729,15 @@ __global__ __launch_bounds__(256) void sym_node_reduce_kernel(SymArgs a) {
   const int q = sym_row_owner(a, X);
   const int64_t bq = (int64_t)a.blk_lo[q] * a.RB * kSymC;
   const int64_t nlq = (int64_t)(a.blk_lo[q + 1] - a.blk_lo[q]) * a.RB * kSymC;
-  T* o = static_cast<T*>(a.Sbuf) + (int64_t)a.nn * 3 * bq + (int64_t)blockIdx.y * 3 * nlq +
-         (x - bq);
+  T* o = static_cast<T*>(a.Sbuf) + (int64_t)a.nn * 3 * bq + (int64_t)by * 3 * nlq + (x - bq);
   o[0] = r[0];
   o[nlq] = r[1];
   o[2 * nlq] = r[2];
+}
+
+template <typename T, bool NT>
+__global__ __launch_bounds__(256) void sym_node_reduce_kernel(SymArgs a) {
+  sym_node_reduce_body<T, NT>(a, (int)blockIdx.x, (int)blockIdx.y);
 }
 
 // S(x) for an own body: every rank's nodes in global order, merged into the full tree; the
@@ -783,11 +787,10 @@ __device__ __forceinline__ A split_parts_add(const SymArgs& a, int br, int s, in
 // thread: one component per thread triples the loads in flight, and the loads of 8 segments
 // are issued ahead of their (ordered) adds.
 template <typename T>
-__global__ __launch_bounds__(256) void sym_row_reduce_kernel(SymArgs a) {
-  const int64_t b = (int64_t)blockIdx.x * 256 + threadIdx.x;  // body within the band
+__device__ __forceinline__ void sym_row_reduce_body(const SymArgs& a, int bx, int k) {
+  const int64_t b = (int64_t)bx * 256 + threadIdx.x;  // body within the band; k: component
   if (b >= (int64_t)a.band_rows * kSymC) return;
   const int br = (int)(b / kSymC), c = (int)(b % kSymC);
-  const int k = blockIdx.y;  // component
   const int A = a.a0 + a.band0 + br;
   if ((int64_t)A * kSymC >= a.n_real) return;  // all-ghost row
   const T* __restrict__ pd = static_cast<const T*>(a.Pd) + (int64_t)br * a.D * 3 * kSymC +
@@ -811,6 +814,27 @@ __global__ __launch_bounds__(256) void sym_row_reduce_kernel(SymArgs a) {
   for (; s < ns; ++s) acc += __builtin_nontemporal_load(p + (int64_t)s * 3 * kSymC);
   if (s < segs) acc = split_parts_add(a, br, s, segs, k * kSymC + c, p, acc);
   static_cast<T*>(a.Ti)[(int64_t)k * a.n_local + (int64_t)(a.band0 + br) * kSymC + c] = acc;
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void sym_row_reduce_kernel(SymArgs a) {
+  sym_row_reduce_body<T>(a, (int)blockIdx.x, (int)blockIdx.y);
+}
+
+// The rank's own node sums (the last node reduce of the exchange, a.x_lo / x_count) and the
+// row reduce in ONE launch: blocks [0, node_bx * nn) run the node reduce (dispatched first:
+// they are the latency-bound chains), the rest the row reduce. Two memory-bound sums of the
+// post-force chain share the launch's ramp and tail instead of running back to back. Same
+// sums per body, same bits.
+template <typename T, bool NT>
+__global__ __launch_bounds__(256) void sym_node_row_kernel(SymArgs a, int node_bx, int row_bx) {
+  const int nnb = node_bx * a.nn;
+  if ((int)blockIdx.x < nnb) {
+    sym_node_reduce_body<T, NT>(a, (int)blockIdx.x % node_bx, (int)blockIdx.x / node_bx);
+  } else {
+    const int k = (int)blockIdx.x - nnb;
+    sym_row_reduce_body<T>(a, k % row_bx, k / row_bx);
+  }
 }
 
 // a = Ti + S (the canonical tree over all ranks' nodes), then kick-drift (cuda.cu:73-76,
@@ -1052,6 +1076,24 @@ hipError_t launch_sym_node_reduce(const SymArgs& a, hipStream_t s) {
   } else {
     if (nt) hipLaunchKernelGGL((sym_node_reduce_kernel<float, true>), grid, dim3(256), 0, s, a);
     else hipLaunchKernelGGL((sym_node_reduce_kernel<float, false>), grid, dim3(256), 0, s, a);
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_sym_node_row(const SymArgs& a, hipStream_t s) {
+  if (!a.Bbuf && (a.band0 != 0 || a.band_rows != a.rows)) return hipErrorInvalidValue;
+  const int64_t nb = (int64_t)a.real_chunks * kSymC;
+  const int64_t bodies = a.x_count > 0 ? a.x_count : nb;
+  const int node_bx = (int)((bodies + 255) / 256);
+  const int row_bx = (int)(((int64_t)a.band_rows * kSymC + 255) / 256);
+  const dim3 grid((unsigned)(node_bx * a.nn + 3 * row_bx));
+  const bool nt = a.P > 1;  // (ld_pj)
+  if (a.fp64) {
+    if (nt) hipLaunchKernelGGL((sym_node_row_kernel<double, true>), grid, dim3(256), 0, s, a, node_bx, row_bx);
+    else hipLaunchKernelGGL((sym_node_row_kernel<double, false>), grid, dim3(256), 0, s, a, node_bx, row_bx);
+  } else {
+    if (nt) hipLaunchKernelGGL((sym_node_row_kernel<float, true>), grid, dim3(256), 0, s, a, node_bx, row_bx);
+    else hipLaunchKernelGGL((sym_node_row_kernel<float, false>), grid, dim3(256), 0, s, a, node_bx, row_bx);
   }
   return hipGetLastError();
 }

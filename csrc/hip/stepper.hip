@@ -409,6 +409,9 @@ int sym_force(gs_stepper* s, gs::SymArgs a, bool overlap_gather, bool exchange =
       // published, or are deferred to a second launch queued behind the gather.
       a.units = 6;
       GS_HIP(force_sym_launch(s, a, s->s_comp));
+      // (The units-7 launch polling the gate itself instead of a wait kernel in front of it
+      // deadlocked two ranks sharing one GPU: its workgroups, at the force kernel's register
+      // allocation, filled the GPU while the peer rank's launches needed it.)
       if (comp_wait_comm(s, s->ev_gathered, kMarkGather, -1, gflag)) return -1;
       a.units = 7;
       GS_HIP(force_sym_launch(s, a, s->s_comp));
@@ -429,16 +432,16 @@ int sym_force(gs_stepper* s, gs::SymArgs a, bool overlap_gather, bool exchange =
     // (The row reduce on a second stream beside the node stages and the exchange measured
     // worse at rank 7 of 8, 1M: chain 650 against 257 us, step 22.1-22.2 against 21.4-21.5 ms,
     // profiles/r5_nt_loads_ab.txt; it stays in sequence.)
-    bool exchanged = false;
+    bool exchanged = false, row_done = false;
     if (last) {
       if (exchange) {
-        // node reduce pipelined with the sends
-        if (sym_reduce_exchange(s, a, &exchanged)) return -1;
+        // node reduce pipelined with the sends (its last launch carries the row reduce)
+        if (sym_reduce_exchange(s, a, &exchanged, &row_done)) return -1;
       } else {
         GS_HIP(gs::launch_sym_node_reduce(a, s->s_comp));
       }
     }
-    GS_HIP(gs::launch_sym_row_reduce(a, s->s_comp));
+    if (!row_done) GS_HIP(gs::launch_sym_row_reduce(a, s->s_comp));
     if (exchanged) {
       if (comp_wait_comm(s, s->ev_sym, kMarkExchange, kSyncExch)) return -1;
     }

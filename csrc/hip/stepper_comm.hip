@@ -155,8 +155,9 @@ int ring_xfer_rccl(gs_stepper* s, int cur, int sub) {
 // land in the Sbuf blocks of those ranks).
 // `sig`: a flag-sync counter to raise before this work (SymArgs::sig; raised by a signal
 // kernel instead when there is no launch to carry it).
+// `with_row`: the row reduce goes into the same launch (launch_sym_node_row).
 static int node_reduce_dests(gs_stepper* s, const gs::SymArgs& a0, int kb, int ke,
-                             unsigned* sig = nullptr) {
+                             unsigned* sig = nullptr, bool with_row = false) {
   const int P = s->cfg.nranks, r = s->cfg.rank;
   // (destinations whose sums are +0.0 by the geometry at either end of the range are left out:
   // their node sums are never sent)
@@ -168,10 +169,12 @@ static int node_reduce_dests(gs_stepper* s, const gs::SymArgs& a0, int kb, int k
   for (int k = kb; k < ke; ++k) a.x_count += s->rcnt[(r + k) % P];
   if (a.x_count == 0) {
     if (sig) GS_HIP(gs::launch_sync_signal(sig, nullptr, s->s_comp));
+    if (with_row) GS_HIP(gs::launch_sym_row_reduce(a0, s->s_comp));
     return 0;
   }
   a.sig = sig;
-  GS_HIP(gs::launch_sym_node_reduce(a, s->s_comp));
+  if (with_row) GS_HIP(gs::launch_sym_node_row(a, s->s_comp));
+  else GS_HIP(gs::launch_sym_node_reduce(a, s->s_comp));
   return 0;
 }
 
@@ -185,7 +188,7 @@ static int node_reduce_dests(gs_stepper* s, const gs::SymArgs& a0, int kb, int k
 // computed, instead of the whole exchange waiting for the whole node reduce (1M / 8 ranks:
 // a 190 us exchange behind a 100 us node reduce). Same kernels and sums per body: same bits.
 // The compute stream joins the exchange later (comp_wait on ev_sym before finalize).
-int sym_reduce_exchange(gs_stepper* s, const gs::SymArgs& a0, bool* exchanged) {
+int sym_reduce_exchange(gs_stepper* s, const gs::SymArgs& a0, bool* exchanged, bool* row_done) {
   const int P = s->cfg.nranks, r = s->cfg.rank;
   // stage g: shifts [k_lo[g], k_lo[g + 1]). Stage 1 is the smaller one (a third of the
   // shifts): its reduce is short, so the messages start early, and the larger stage 2 reduce
@@ -241,7 +244,11 @@ int sym_reduce_exchange(gs_stepper* s, const gs::SymArgs& a0, bool* exchanged) {
         }))
       return -1;
   }
-  if (node_reduce_dests(s, a0, 0, 1, pending)) return -1;  // the own sums, last
+  // the own sums, last, with the row reduce in the same launch (one band: Pi, Pd, Px hold
+  // every row; multi-band runs reduce their rows band by band)
+  const bool with_row = a0.Bbuf == nullptr && a0.band0 == 0 && a0.band_rows == a0.rows;
+  if (node_reduce_dests(s, a0, 0, 1, pending, with_row)) return -1;
+  *row_done = with_row;
   // (a live 1-rank communicator: nothing to exchange, and nothing for finalize to wait for)
   *exchanged = stages > 0;
   return 0;

@@ -110,12 +110,10 @@ int comm_do(gs_stepper* s, std::function<int()> fn) {
 }
 
 // ---- cross-stream points: events, or device counters (flag sync) ------------------------
-namespace {
 uint64_t sync_limit_ticks(const gs_stepper* s) {
   const double t = s->step_timeout_s > 0 ? s->step_timeout_s : 600.0;
   return (uint64_t)(t * s->clk_khz * 1e3);
 }
-}  // namespace
 
 int comp_signal(gs_stepper* s, hipEvent_t ev, int id, unsigned* clear) {
   if (!fsync(s)) return comp_record(s, ev);

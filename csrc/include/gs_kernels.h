@@ -172,6 +172,8 @@ hipError_t launch_sync_wait(const unsigned* flag, unsigned* seen, unsigned long 
 hipError_t launch_sym_block_reduce(const SymArgs& a, hipStream_t s);  // band leaves -> Bbuf
 hipError_t launch_sym_node_reduce(const SymArgs& a, hipStream_t s);   // own nodes -> Sbuf
 hipError_t launch_sym_row_reduce(const SymArgs& a, hipStream_t s);    // the band's rows -> Ti
+// The own node sums (a.x_lo / x_count) and the row reduce as one launch (same bits).
+hipError_t launch_sym_node_row(const SymArgs& a, hipStream_t s);
 hipError_t launch_sym_finalize(const SymArgs& a, hipStream_t s);
 // One rank, one band: group reduce + row reduce + finalize in one kernel, same bits.
 hipError_t launch_sym_tail(const SymArgs& a, hipStream_t s);

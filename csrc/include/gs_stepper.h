@@ -307,7 +307,9 @@ int gather(gs_stepper* s, int cur, bool gate = false);
 int ring_src(const gs_stepper* s, int sub);
 void rank_chunks(const gs_stepper* s, int src, int* c0, int* c1);
 int ring_xfer_rccl(gs_stepper* s, int cur, int sub);
-int sym_reduce_exchange(gs_stepper* s, const gs::SymArgs& a, bool* exchanged);
+int sym_reduce_exchange(gs_stepper* s, const gs::SymArgs& a0, bool* exchanged, bool* row_done);
+// The flag-sync wait bound in s_memrealtime ticks (the native step timeout, 600 s if none).
+uint64_t sync_limit_ticks(const gs_stepper* s);
 void maybe_install_crash_trace();
 // ncclCommAbort once (the watchdog thread, a timeout or an async error may all ask for it).
 bool abort_comm(gs_stepper* s);
