@@ -437,6 +437,10 @@ int sym_force(gs_stepper* s, gs::SymArgs a, bool overlap_gather, bool exchange =
       if (exchange) {
         // node reduce pipelined with the sends (its last launch carries the row reduce)
         if (sym_reduce_exchange(s, a, &exchanged, &row_done)) return -1;
+      } else if (!a.Bbuf && one_band) {
+        // one launch for the node reduce and the row reduce (launch_sym_node_row)
+        GS_HIP(gs::launch_sym_node_row(a, s->s_comp));
+        row_done = true;
       } else {
         GS_HIP(gs::launch_sym_node_reduce(a, s->s_comp));
       }
