@@ -605,7 +605,9 @@ __device__ __forceinline__ A ld(const T* p) {
 // drops 677 -> 632 us but the row reduce grows 590 -> 704 us whether it runs before or after
 // it (same row-reduce code): the plain loads of the node reduce are what evict the force
 // launch's dirty lines from the memory-side cache, and without them the row reduce pays the
-// write-backs. One GPU keeps plain loads (profiles/r5_nt_loads_ab.txt).
+// write-backs. One GPU keeps plain loads, and so do two ranks (chain 718-723 against 763 us
+// with NT at rank 1 of 2; rank 1 of 4: 409-410 with NT against 426 us without;
+// profiles/r5_nt_loads_ab.txt).
 template <bool NT, typename A, typename T>
 __device__ __forceinline__ A ld_pj(const T* p) {
   if constexpr (NT && std::is_same<A, T>::value) return __builtin_nontemporal_load(p);
@@ -1069,7 +1071,7 @@ hipError_t launch_sym_node_reduce(const SymArgs& a, hipStream_t s) {
   const int64_t bodies = a.x_count > 0 ? a.x_count : nb;
   if (bodies <= 0) return hipSuccess;
   const dim3 grid((unsigned)((bodies + 255) / 256), (unsigned)a.nn);
-  const bool nt = a.P > 1;  // (ld_pj)
+  const bool nt = a.P > 2;  // (ld_pj)
   if (a.fp64) {
     if (nt) hipLaunchKernelGGL((sym_node_reduce_kernel<double, true>), grid, dim3(256), 0, s, a);
     else hipLaunchKernelGGL((sym_node_reduce_kernel<double, false>), grid, dim3(256), 0, s, a);
@@ -1087,7 +1089,7 @@ hipError_t launch_sym_node_row(const SymArgs& a, hipStream_t s) {
   const int node_bx = (int)((bodies + 255) / 256);
   const int row_bx = (int)(((int64_t)a.band_rows * kSymC + 255) / 256);
   const dim3 grid((unsigned)(node_bx * a.nn + 3 * row_bx));
-  const bool nt = a.P > 1;  // (ld_pj)
+  const bool nt = a.P > 2;  // (ld_pj)
   if (a.fp64) {
     if (nt) hipLaunchKernelGGL((sym_node_row_kernel<double, true>), grid, dim3(256), 0, s, a, node_bx, row_bx);
     else hipLaunchKernelGGL((sym_node_row_kernel<double, false>), grid, dim3(256), 0, s, a, node_bx, row_bx);
