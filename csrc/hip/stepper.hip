@@ -762,6 +762,12 @@ int gs_stepper_create(const gs_config* cfg, gs_stepper** out) {
   // GRAVSIM_SYNC=events: the multi-rank step orders its streams by hipEvents (and replays a
   // segmented plan) instead of device counters (flag sync, one graph per period)
   if (const char* v = getenv("GRAVSIM_SYNC")) s->sync_events = strcmp(v, "events") == 0;
+  // Under rocprofv3 --pmc (it exports ROCPROF_COUNTER_COLLECTION) every dispatch is
+  // serialized, so a wait kernel would wait for a signal queued behind it until the step
+  // timeout: counter collection runs with event ordering (GRAVSIM_SYNC=flags overrides).
+  if (getenv("ROCPROF_COUNTER_COLLECTION") &&
+      !(getenv("GRAVSIM_SYNC") && strcmp(getenv("GRAVSIM_SYNC"), "flags") == 0))
+    s->sync_events = true;
   const int64_t own_first = s->L.local_begin / s->L.chunk;
   const int64_t own_last = (s->L.local_begin + s->L.n_local) / s->L.chunk;
   s->own_c0 = (int)(own_first < s->L.n_chunks ? own_first : s->L.n_chunks);
