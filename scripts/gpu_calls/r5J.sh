@@ -1,10 +1,10 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"; mkdir -p gpurun_out; export TMPDIR=/tmp
 O=gpurun_out
-timeout -k 10 1000 python bench/rank_shape.py --n 1048576 --ranks 1,3,5,6,7 --rank all --comm-gbps 64 --steps 10 > $O/r5_predicted_scaling_uneven_final.jsonl 2>&1 || exit 1
+timeout -k 10 1000 python bench/rank_shape.py --n 1048576 --ranks 1,8,2,4 --rank all --comm-gbps 64 --steps 16 > $O/r5_predicted_scaling_final3.jsonl 2>&1 || exit 1
 python - <<'PY'
 import json
-rows=[json.loads(l) for l in open("gpurun_out/r5_predicted_scaling_uneven_final.jsonl") if l.startswith("{")]
+rows=[json.loads(l) for l in open("gpurun_out/r5_predicted_scaling_final3.jsonl") if l.startswith("{")]
 by={}
 for r in rows:
     if r.get("predicted_efficiency") is None and r.get("P")!=1: continue
