@@ -32,7 +32,8 @@ def hip():
 # module imported at collection) would silently alter every later test.
 _PROCESS_KNOBS = ("GRAVSIM_EMULATE_RANK", "GRAVSIM_UNIT_TRACE", "GRAVSIM_EMU_COMM",
                   "GRAVSIM_SYM_BAND_MB", "GRAVSIM_FAULT_SKIP_UNITS", "GRAVSIM_SYM_OVERLAP",
-                  "GRAVSIM_FORCE_COMM", "GRAVSIM_TEST_STALL", "GRAVSIM_SYNC")
+                  "GRAVSIM_FORCE_COMM", "GRAVSIM_TEST_STALL", "GRAVSIM_SYNC",
+                  "ROCPROF_COUNTER_COLLECTION")
 
 
 @pytest.fixture(autouse=True)

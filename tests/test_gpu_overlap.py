@@ -64,6 +64,32 @@ def test_segmented_plan_matches_eager(hip, monkeypatch, strategy, overlap, sync)
     assert np.array_equal(res[True][1], res[False][1])
 
 
+def test_counter_collection_selects_event_ordering(hip, monkeypatch):
+    """rocprofv3 --pmc serializes dispatches (it exports ROCPROF_COUNTER_COLLECTION): a
+    flag-sync wait kernel would wait for a signal queued behind it until the step timeout, so
+    the stepper orders its streams with events then (a segmented plan), unless
+    GRAVSIM_SYNC=flags says otherwise. Same bits either way."""
+    res = {}
+    for env in ("", "1"):
+        if env:
+            monkeypatch.setenv("ROCPROF_COUNTER_COLLECTION", env)
+        else:
+            monkeypatch.delenv("ROCPROF_COUNTER_COLLECTION", raising=False)
+        e = _emu(monkeypatch, 262144, 8, 3, 64, 3)
+        e.init_ics("solar+random", 6)
+        e.step(4)
+        e.sync()
+        gi = e.graph_info()
+        assert gi["mode"] == "segmented", gi
+        assert (gi["segments"] > 1) == bool(env), gi
+        b = e.state()
+        own = e.layout.real_local
+        res[env] = b.pos[own.start:own.stop].copy()
+        e.close()
+    monkeypatch.delenv("ROCPROF_COUNTER_COLLECTION", raising=False)
+    assert np.array_equal(res[""], res["1"])
+
+
 @pytest.mark.parametrize("P,rank", [(3, 0), (3, 2), (5, 4), (6, 5), (7, 0), (7, 6)])
 def test_uneven_rank_emulation_runs(hip, monkeypatch, P, rank):
     """Per-rank emulation of P not dividing the 256 row blocks (1M bodies): rank 0 holds the
