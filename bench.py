@@ -116,6 +116,10 @@ def parse(argv=None) -> argparse.Namespace:
                          "20 x the first measured step), at most 240 s)")
     ap.add_argument("--step-timeout-min", type=float, default=60.0,
                     help="floor of the derived step timeout")
+    ap.add_argument("--p-audit", default="auto", choices=["auto", "on", "off"],
+                    help="P > 1: after the timed run, rank 0 recomputes 2 steps from the same "
+                         "ICs as a 1-rank engine on its own GPU and every rank's rows must have "
+                         "the same bits (auto: up to 4M bodies fp32, 1M fp64)")
     return ap.parse_args(argv)
 
 
@@ -151,11 +155,49 @@ def rccl_transports(path: str | None) -> dict:
 
 
 def device_record(dev: int) -> dict:
+    import socket
+
     import torch
 
     p = torch.cuda.get_device_properties(dev)
     return {"device": dev, "pci": f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}",
-            "arch": p.gcnArchName, "cus": p.multi_processor_count}
+            "arch": p.gcnArchName, "cus": p.multi_processor_count, "host": socket.gethostname()}
+
+
+def p_independence_audit(eng, cfg, dist, comm, dev: int, steps: int = 2) -> str:
+    """Untimed: the P-rank engine steps `steps` times from the benchmark ICs; rank 0 runs the
+    same steps as a 1-rank engine on its own GPU, and every rank's own rows (positions and
+    velocities) must hash equal to the same rows of the 1-rank state. The canonical
+    decomposition makes the bits independent of P (the reference's mpi.c is not: SURVEY.md
+    §2.7 D6). Collective; returns "bitwise" or the ranks that differ."""
+    import hashlib
+
+    from gravsim.runtime.engines import HipEngine
+
+    def sha(x) -> str:
+        return hashlib.sha256(x.tobytes()).hexdigest()[:24]
+
+    eng.init_ics("solar+random", cfg.seed)
+    eng.step(steps)
+    eng.sync()
+    pos, vel, _ = own_state(eng)
+    rows = eng.layout.real_local
+    mine = (rows.start, rows.stop, sha(pos), sha(vel))
+    recs = comm.allgather_object(dist, mine)
+    verdict = ""
+    if dist.rank == 0:
+        one = HipEngine(cfg, 0, 1, device=dev)
+        try:
+            one.init_ics("solar+random", cfg.seed)
+            one.step(steps)
+            one.sync()
+            b = one.state()
+        finally:
+            one.close()
+        bad = [q for q, (r0, r1, hp, hv) in enumerate(recs)
+               if sha(b.pos[r0:r1]) != hp or sha(b.vel[r0:r1]) != hv]
+        verdict = "bitwise" if not bad else f"differs from 1 rank on rank(s) {bad}"
+    return comm.allgather_object(dist, verdict)[0]
 
 
 def own_state(eng):
@@ -305,6 +347,7 @@ def run(a, g) -> int:
     from gravsim.ops import _native
     from gravsim.parallel import comm
     from gravsim.parallel import guard as gd
+    from gravsim.parallel import verify
     from gravsim.runtime.engines import HipEngine
     from gravsim.runtime.simulation import conservation_summary, engine_conserved
 
@@ -334,7 +377,7 @@ def run(a, g) -> int:
     eng = HipEngine(cfg, rank, world, device=dev, dist=dist)
     g.on_abort(eng.abort)
     g.probe(lambda: {"comm_stage": eng.comm_stage()})
-    ranks_info = None
+    ranks_info = topology = None
     if world > 1:
         g.stage("rccl_uid", init_b)
         uid = HipEngine.unique_id() if rank == 0 else None
@@ -342,8 +385,18 @@ def run(a, g) -> int:
         g.stage("comm_init", init_b)  # ncclCommInitRank + warm-up of every connection
         eng.comm_init(uid)
         g.stage("rank_info", init_b)
-        rec = {"rank": rank, **device_record(dev), **rccl_transports(rccl_log)}
+        rec = {"rank": rank, **device_record(dev), **eng.comm_info(),
+               **rccl_transports(rccl_log)}
         ranks_info = comm.allgather_object(dist, rec)
+        # What RCCL formed and what it runs over (parallel/verify.py): one GPU per rank,
+        # the whole job in one communicator, no network transport inside one node. The
+        # one-GPU rehearsal shares device 0 over sockets by design: recorded, not enforced.
+        problems = verify.topology_problems(world, ranks_info)
+        topology = {"enforced": not verify.rehearsal(os.environ), "problems": problems,
+                    **verify.transport_summary(ranks_info)}
+        g.note(topology=topology)
+        if problems and topology["enforced"]:
+            raise SystemExit("multi-GPU topology check failed: " + "; ".join(problems))
 
     # One eager step from the ICs: its time bounds every later stage, and the native step
     # timeout becomes max(60 s, 20 x step), at most 240 s (a 16M / 8-rank step is ~5 s).
@@ -396,6 +449,7 @@ def run(a, g) -> int:
         extra = eng.align_period() if a.graph else 0
         eng.sync()
         eng.audit_reset()
+        eng.clock()  # (reset: the engine-clock record covers the timed steps only)
         torch.cuda.synchronize()
         comm.barrier(dist)
         torch.cuda.synchronize()
@@ -408,6 +462,7 @@ def run(a, g) -> int:
         t1 = time.perf_counter()
         wall = comm.allreduce_max(dist, t1 - t0)
         g.stage("audits", budget(4, 180))
+        clk = eng.clock()  # the timed steps' force launches (sym schedule)
         ginfo = eng.graph_info()
         # HBM the stepper holds (its allocation ledger; RCCL's own buffers excluded), max
         # over ranks
@@ -488,7 +543,7 @@ def run(a, g) -> int:
                 failures.append(f"replay: the independent schedule differs on {int(diff)} rank(s)")
             eng.set_schedule((2 if a.graph_comm else 1) if a.graph else 0, cap)
             eng.set_overlap(overlap)
-        return dict(extra=extra, wall=wall, ginfo=ginfo, mem=mem, hbm_max=hbm_max,
+        return dict(extra=extra, wall=wall, clk=clk, ginfo=ginfo, mem=mem, hbm_max=hbm_max,
                     failures=failures,
                     units=units, bad=bad, drift=drift, err_end=err_end, bound_end=bound_end,
                     conservation=conservation, phase=phase, replay=replay)
@@ -515,6 +570,26 @@ def run(a, g) -> int:
     err_end, conservation, phase, replay = (res["err_end"], res["conservation"], res["phase"],
                                             res["replay"])
     bound_end = res["bound_end"]
+    # Engine clock over the timed steps, per rank (each GPU holds its own DVFS state): the
+    # whole job's workgroup-cycles and the CUs it ran on, for clock-normalised costs
+    clk = res["clk"]
+    ghz_min = comm.allreduce_max(dist, -clk["ghz"]) * -1.0
+    ghz_max = comm.allreduce_max(dist, clk["ghz"])
+    ghz_sum = comm.allreduce_sum(dist, clk["ghz"])
+    wg_cycles = comm.allreduce_sum(dist, clk["wg_cycles"])
+    cus_total = comm.allreduce_sum(dist, float(torch.cuda.get_device_properties(
+        torch.cuda.current_device()).multi_processor_count))
+
+    # P-independence (untimed, P > 1): the multi-rank bits against one rank on rank 0's GPU.
+    p_audit = None
+    small = cfg.n <= ((4 << 20) if a.dtype == "fp32" else (1 << 20))
+    if world > 1 and (a.p_audit == "on" or (a.p_audit == "auto" and small)):
+        g.stage("p_audit", budget(4 * world + 4, 180))
+        p_audit = p_independence_audit(eng, cfg, dist, comm, dev)
+        if p_audit != "bitwise":
+            failures.append(f"P-independence: {p_audit}")
+    elif world > 1:
+        p_audit = "skipped (--p-audit off or size)"
 
     # The reference's exact hard-cutoff select (cuda.cu:39, mpi.c:64), timed on its own.
     lay = eng.native_layout
@@ -541,11 +616,9 @@ def run(a, g) -> int:
         value = cfg.n * a.steps / wall
         mode = _native.MODE_NAMES.get(lay["mode"])
         if mode == "sym":
-            # Newton-3 schedule: each unordered pair once, both sides (nbody_sym.hip).
-            tile = ("8 i x 2 j per lane, j-pair packed fp32" if a.dtype == "fp32"
-                    else "4 i x 1 j per lane, fp64")
-            kernel_info = {"kernel": f"sym: register tile (LDS-staged j, DPP carriers), {tile}, "
-                                     "cyclic half-shell of 2048-body chunks",
+            # Newton-3 schedule: each unordered pair once, both sides (nbody_sym.hip); the
+            # tile shape is the compiled one (gs_sym_tile_shape)
+            kernel_info = {"kernel": _native.sym_kernel_label(a.dtype == "fp64"),
                            "n_pad": lay["n_pad"]}
             exch = ("ring of P-1 neighbour stages" if a.strategy == "ring" else "all-gather") + \
                 " + node-sum send/recv"
@@ -557,6 +630,21 @@ def run(a, g) -> int:
             pairs = float(cfg.n) * cfg.n  # one-sided: every ordered pair evaluated
         parallelism = (f"body-decomposition x{world} (RCCL {exch})" if world > 1
                        else "single GPU")
+        # Clock-normalised cost (a slow box and a slow kernel look alike in ms):
+        # the engine clock the force launches ran at (s_memtime / s_memrealtime per
+        # workgroup, mean over ranks), CU-cycles per pair evaluation of the whole step at that
+        # clock, and the force kernels' own workgroup-cycles per pair (no clock in it at all).
+        ghz = ghz_sum / world if ghz_sum > 0 else None
+        step_pairs = pairs * a.steps
+        clock = {"engine_clock_ghz": ghz,
+                 "engine_clock_ghz_ranks": [ghz_min, ghz_max] if world > 1 else None,
+                 "cycles_per_pair_eval": (wall * ghz * 1e9 * cus_total / step_pairs)
+                 if ghz else None,
+                 "force_wg_cycles_per_pair_eval": wg_cycles / step_pairs if wg_cycles else None,
+                 "cus": int(cus_total),
+                 "method": "per workgroup: s_memtime span / s_memrealtime span x 100 MHz, "
+                           "duration-weighted over the timed steps' force launches; "
+                           "cycles_per_pair_eval = step wall x clock x CUs / pair evals"}
         out = {
             "metric": METRIC,
             "value": value,
@@ -571,6 +659,8 @@ def run(a, g) -> int:
             "dtype": a.dtype,
             "data": DATA,
             "status": "ok" if not failures else "audit failed",
+            "engine_clock_ghz": clock["engine_clock_ghz"],
+            "cycles_per_pair_eval": clock["cycles_per_pair_eval"],
             "config": {
                 "model": MODEL,
                 "n_bodies": cfg.n,
@@ -613,15 +703,18 @@ def run(a, g) -> int:
                 "conservation": conservation,
                 "exact_cutoff_ms_per_step": exact_ms,
                 "nonfinite": int(bad),
+                "clock": clock,
                 "hbm": {"gb_per_rank_max": round(hbm_max / 1e9, 3),
                         "by_buffer_gb_rank0": {k: round(v / 1e9, 4) for k, v in mem.items()}},
             },
             "work_audit": "ok" if not failures else "; ".join(failures),
-            "audit": {"units": units, "replay": replay},
+            "audit": {"units": units, "replay": replay, "p_independence": p_audit},
         }
         if world > 1:
             out["config"]["launch"] = launch_info()
             out["config"]["ranks"] = ranks_info
+            out["config"]["topology"] = topology
+            out["rccl_nranks"] = ranks_info[0].get("rccl_nranks") if ranks_info else None
         if phase is not None:
             out["comm_ms"] = phase["comm_ms"]
             out["exposed_comm_ms"] = phase["exposed_comm_ms"]

@@ -60,8 +60,16 @@ __global__ void gate_set_kernel(unsigned* gate) {
 // starts with the dispatch's acquire. A level flag (the gather gate, re-armed by finalize)
 // works the same way without `seen`. Each wait adds its stall (s_memrealtime ticks) to
 // stats[0] and one to stats[1]: the exposed comm of the replayed step, which a single graph
-// cannot bracket with host events. The spin gives up after `limit` ticks (the native step
-// timeout) and counts that in stats[2], so a dead peer never leaves a kernel spinning.
+// cannot bracket with host events.
+// Give-up: the spin ends after *limit ticks (a device word, so a graph captured
+// before the host changed its step timeout still uses the new bound; set above the host's
+// own progress bound, so the host abort normally wins) or as soon as the sticky failure word
+// `fail` (host-mapped memory) is nonzero: set by an earlier wait that gave up, or by the host
+// when it aborts the communicator. A wait that gives up does NOT advance `seen` (the signal
+// it missed must not satisfy a later wait), counts the timeout in stats[2] and sets `fail`,
+// so every later wait on either stream falls through at once and the host's sync / wait /
+// state read reports the failure instead of returning a step computed from an unfinished
+// gather or exchange.
 // `clear` (optional): a level flag this point re-arms first (the gather gate of the buffer
 // the signalled gather fills: the gate's wait on the compute stream must not see a gate left
 // set by an earlier gather of that buffer, e.g. a state read's, once init has reset the step).
@@ -75,15 +83,23 @@ __global__ void sync_signal_kernel(unsigned* count, unsigned* clear) {
 }
 
 __global__ void sync_wait_kernel(const unsigned* flag, unsigned* seen,
-                                 unsigned long long* stats, uint64_t limit) {
+                                 unsigned long long* stats, const unsigned long long* limit_p,
+                                 unsigned* fail) {
   if (threadIdx.x != 0) return;
   const unsigned want = seen ? seen[0] + 1u : 1u;  // a level flag: any nonzero value
+  const uint64_t limit = __hip_atomic_load(limit_p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   uint64_t t = t0;
   bool ok = true;
-  for (;;) {
+  for (unsigned it = 0;; ++it) {
     const unsigned v = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     if (seen ? (int)(v - want) >= 0 : v != 0u) break;
+    // (the host-mapped failure word: one system-scope read every 256 polls, ~100 us)
+    if ((it & 255u) == 0u &&
+        __hip_atomic_load(fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) {
+      ok = false;
+      break;
+    }
     __builtin_amdgcn_s_sleep(8);
     t = __builtin_amdgcn_s_memrealtime();
     if (t - t0 > limit) {
@@ -92,7 +108,8 @@ __global__ void sync_wait_kernel(const unsigned* flag, unsigned* seen,
     }
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-  if (seen) seen[0] = want;
+  if (ok && seen) seen[0] = want;
+  if (!ok) __hip_atomic_store(fail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   if (stats) {
     __hip_atomic_fetch_add(stats, (unsigned long long)(t - t0), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
@@ -109,8 +126,9 @@ hipError_t launch_sync_signal(unsigned* count, unsigned* clear, hipStream_t s) {
 }
 
 hipError_t launch_sync_wait(const unsigned* flag, unsigned* seen, unsigned long long* stats,
-                            uint64_t limit_ticks, hipStream_t s) {
-  hipLaunchKernelGGL(sync_wait_kernel, dim3(1), dim3(64), 0, s, flag, seen, stats, limit_ticks);
+                            const unsigned long long* limit_ticks, unsigned* fail, hipStream_t s) {
+  hipLaunchKernelGGL(sync_wait_kernel, dim3(1), dim3(64), 0, s, flag, seen, stats, limit_ticks,
+                     fail);
   return hipGetLastError();
 }
 

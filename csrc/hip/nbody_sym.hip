@@ -415,8 +415,42 @@ __device__ __forceinline__ unsigned force_sym_body(const SymArgs& a, int b) {
 // with a stride of the grid. The list is usually empty (the gather finished long before the
 // remote units were dispatched), and a grid of one workgroup per possible unit would cost more
 // than the gather it hides. The main kernel is unchanged by it (same registers, no spills).
+// SymArgs::clk: the workgroup's shader-clock and wall-clock spans, stamped by lane 0 of wave
+// 0. The start stamps wait in LDS, not in registers: held in SGPRs across the unit loop they
+// added 5 SGPR spills to the 1M kernel.
+struct ClockSpan {
+  // {start s_memtime, start s_memrealtime, clk pointer or 0}: the pointer waits there too
+  __device__ __forceinline__ static unsigned long long* slot() {
+    __shared__ unsigned long long t0[3];
+    return t0;
+  }
+  __device__ __forceinline__ static void begin(const SymArgs& a) {
+    if (threadIdx.x == 0) {
+      slot()[2] = reinterpret_cast<unsigned long long>(a.clk);
+      if (a.clk) {
+        slot()[0] = __builtin_amdgcn_s_memtime();
+        slot()[1] = __builtin_amdgcn_s_memrealtime();
+      }
+    }
+  }
+  __device__ __forceinline__ static void end() {
+    if (threadIdx.x == 0) {
+      unsigned long long* clk = reinterpret_cast<unsigned long long*>(slot()[2]);
+      if (clk) {
+        const unsigned long long mt1 = __builtin_amdgcn_s_memtime();
+        const unsigned long long rt1 = __builtin_amdgcn_s_memrealtime();
+        __hip_atomic_fetch_add(clk, mt1 - slot()[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(clk + 1, rt1 - slot()[1], __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(clk + 2, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
+};
+
 template <typename T, bool EXACT, bool DEFER, bool DYN, bool PF>
 __device__ __forceinline__ void force_sym_entry(SymArgs a) {
+  ClockSpan::begin(a);
   if constexpr (!DEFER && !DYN) {
     const unsigned w = force_sym_body<T, EXACT>(a, blockIdx.x);
     if (w) audit_unit(a, w);
@@ -500,6 +534,7 @@ __device__ __forceinline__ void force_sym_entry(SymArgs a) {
     }
     if (done) audit_unit(a, done);
   }
+  ClockSpan::end();
 }
 
 // (separate instantiations: the static kernels keep their own register allocation)
@@ -1054,6 +1089,18 @@ hipError_t launch_force_sym_t(const SymArgs& a, hipStream_t s) {
 hipError_t launch_force_sym(const SymArgs& a, hipStream_t s) {
   return a.fp64 ? launch_force_sym_t<double>(a, s) : launch_force_sym_t<float>(a, s);
 }
+
+}  // namespace gs
+
+extern "C" int gs_sym_tile_shape(int32_t fp64, int32_t* waves, int32_t* ipl, int32_t* jpl) {
+  using namespace gs;
+  if (waves) *waves = fp64 ? Geo<double>::W : Geo<float>::W;
+  if (ipl) *ipl = fp64 ? Geo<double>::I : Geo<float>::I;
+  if (jpl) *jpl = fp64 ? Geo<double>::J : Geo<float>::J;
+  return 0;
+}
+
+namespace gs {
 
 hipError_t launch_sym_block_reduce(const SymArgs& a, hipStream_t s) {
   if (!a.Bbuf || a.band_rows % a.RB || (a.a0 + a.band0) % a.RB) return hipErrorInvalidValue;

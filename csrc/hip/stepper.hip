@@ -189,6 +189,7 @@ gs::SymArgs sym_args(gs_stepper* s, int cur) {
   }
   a.trace_defer0 = (int32_t)s->utrace_main;
   a.audit = s->audit;
+  a.clk = s->clk;
   return a;
 }
 
@@ -644,6 +645,7 @@ int download_state(gs_stepper* s, double* pos, double* vel, double* mass) {
   const bool own_only = s->virt && !s->full[cur];
   GS_HIP(hipStreamSynchronize(s->s_comp));
   GS_HIP(hipStreamSynchronize(s->s_comm));
+  if (sync_failed(s)) return -1;  // (a state a wait gave up on is not returned)
   const int64_t n = s->L.n, nl = s->L.n_local, b = s->L.local_begin;
   if (pos) {
     std::vector<T> X((size_t)s->L.n_pad * 4);
@@ -853,13 +855,26 @@ int gs_stepper_create(const gs_config* cfg, gs_stepper** out) {
     // stall statistics
     ALLOC_CLEAN(&s->sync_buf, 2 * kSyncCount * sizeof(unsigned), "sync");
     FAIL_CLEAN(hipMemsetAsync(s->sync_buf, 0, 2 * kSyncCount * sizeof(unsigned), s->s_comp));
-    ALLOC_CLEAN(&s->sync_stats, 9 * sizeof(unsigned long long), "sync_stats");
-    FAIL_CLEAN(hipMemsetAsync(s->sync_stats, 0, 9 * sizeof(unsigned long long), s->s_comp));
+    // [0..8] stall statistics, [9] the wait kernels' give-up bound (write_sync_limit)
+    ALLOC_CLEAN(&s->sync_stats, 10 * sizeof(unsigned long long), "sync_stats");
+    FAIL_CLEAN(hipMemsetAsync(s->sync_stats, 0, 10 * sizeof(unsigned long long), s->s_comp));
+    FAIL_CLEAN(hipStreamSynchronize(s->s_comp));
+    if (write_sync_limit(s)) {
+      gs_stepper_destroy(s);
+      return -1;
+    }
+    void* hf = nullptr;
+    FAIL_CLEAN(hipHostMalloc(&hf, 64, hipHostMallocMapped | hipHostMallocCoherent));
+    s->sync_fail = static_cast<volatile unsigned*>(hf);
+    s->sync_fail[0] = 0u;
+    FAIL_CLEAN(hipHostGetDevicePointer(reinterpret_cast<void**>(&s->sync_fail_dev), hf, 0));
   }
   if (s->L.mode == GS_MODE_SYM) {
     // the work audit's unit counter (its cost is within noise: profiles/r3_abaudit*)
     ALLOC_CLEAN(&s->audit, sizeof(unsigned long long), "audit");
     FAIL_CLEAN(hipMemsetAsync(s->audit, 0, sizeof(unsigned long long), s->s_comp));
+    ALLOC_CLEAN(&s->clk, 4 * sizeof(unsigned long long), "clock");
+    FAIL_CLEAN(hipMemsetAsync(s->clk, 0, 4 * sizeof(unsigned long long), s->s_comp));
   }
   if (s->L.mode == GS_MODE_SYM) {
     // Deferred-unit list of the gated launch (one band's units) and the local-first order.
@@ -919,6 +934,7 @@ int gs_stepper_destroy(gs_stepper* s) {
   if (s->have_comm && s->comm_live.exchange(nullptr)) (void)ncclCommDestroy(s->comm);
   for (const auto& m : s->mem) (void)hipFree(m.p);
   s->mem.clear();
+  if (s->sync_fail) (void)hipHostFree(const_cast<unsigned*>(s->sync_fail));
   for (hipEvent_t e : {s->ev_ready, s->ev_gathered, s->ev_t0, s->ev_local, s->ev_end,
                        s->ev_remote, s->ev_fork, s->ev_rem2, s->ev_sym, s->ev_stage[0],
                        s->ev_stage[1]})
@@ -1056,10 +1072,17 @@ int gs_stepper_set_timing(gs_stepper* s, int32_t on) {
   s->timed = on != 0;
   s->pev_used = 0;
   s->pev_plan = 0;
-  // (the wait kernels' stall counters restart with the timed steps; stream-ordered behind
-  // every compute-stream wait enqueued before)
-  if (s->sync_stats)
+  // (the wait kernels' stall counters restart with the timed steps. Both streams drain
+  // first: the comm stream's waits add to stats[6..8] and nothing orders them against a
+  // memset on the compute stream, so a comm-side timeout could be erased or an old stall
+  // survive into the timed window. A timeout already counted fails here.)
+  if (s->sync_stats) {
+    GS_HIP(hipStreamSynchronize(s->s_comm));
+    GS_HIP(hipStreamSynchronize(s->s_comp));
+    if (sync_failed(s)) return -1;
     GS_HIP(hipMemsetAsync(s->sync_stats, 0, 9 * sizeof(unsigned long long), s->s_comp));
+    GS_HIP(hipStreamSynchronize(s->s_comp));
+  }
   return 0;
 }
 
@@ -1138,6 +1161,23 @@ int gs_stepper_audit(gs_stepper* s, uint64_t* units_done, uint64_t* units_per_st
   return 0;
 }
 
+int gs_stepper_clock(gs_stepper* s, double* out4) {
+  for (int i = 0; i < 4; ++i) out4[i] = 0.0;
+  if (!s->clk) return 0;  // one-sided schedules: no clock record
+  GS_HIP(hipSetDevice(s->cfg.device));
+  GS_HIP(hipStreamSynchronize(s->s_comp));
+  GS_HIP(hipStreamSynchronize(s->s_rem));
+  unsigned long long h[3] = {0, 0, 0};
+  GS_HIP(hipMemcpy(h, s->clk, sizeof(h), hipMemcpyDeviceToHost));
+  GS_HIP(hipMemsetAsync(s->clk, 0, 4 * sizeof(unsigned long long), s->s_comp));
+  GS_HIP(hipStreamSynchronize(s->s_comp));
+  out4[0] = h[1] ? (double)h[0] / (double)h[1] * s->clk_khz * 1e-6 : 0.0;  // GHz
+  out4[1] = (double)h[0];
+  out4[2] = (double)h[1] / (s->clk_khz * 1e3);  // workgroup-seconds
+  out4[3] = (double)h[2];
+  return 0;
+}
+
 int gs_stepper_audit_reset(gs_stepper* s) {
   if (!s->audit) return 0;
   GS_HIP(hipSetDevice(s->cfg.device));
@@ -1161,7 +1201,8 @@ int64_t gs_stepper_unit_trace(gs_stepper* s, uint64_t* out, int64_t cap) {
 
 int gs_stepper_set_timeout(gs_stepper* s, double step_timeout_s) {
   s->step_timeout_s = step_timeout_s > 0 ? step_timeout_s : 0.0;
-  return 0;
+  // the device-side bound follows (a word the wait kernels read, graphs included: ADVICE r5)
+  return write_sync_limit(s);
 }
 
 int gs_stepper_sync(gs_stepper* s) {
@@ -1170,7 +1211,7 @@ int gs_stepper_sync(gs_stepper* s) {
   GS_HIP(hipStreamSynchronize(s->s_rem2));
   GS_HIP(hipStreamSynchronize(s->s_comp));
   s->prog_done = s->prog_rec;
-  return 0;
+  return sync_failed(s) ? -1 : 0;
 }
 
 // Bounded wait for every stream, polling RCCL async errors. The deadline bounds PROGRESS: it

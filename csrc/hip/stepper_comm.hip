@@ -104,6 +104,9 @@ bool abort_comm(gs_stepper* s) {
   ncclComm_t c = s->comm_live.exchange(nullptr);
   if (!c) return false;
   s->comm_stage.store(-1);
+  // flag-sync waits still spinning on this communicator's collectives fall through (a wait
+  // that gave up first keeps its own code, 1)
+  if (s->sync_fail && s->sync_fail[0] == 0u) s->sync_fail[0] = 2u;
   (void)ncclCommAbort(c);
   return true;
 }
@@ -343,6 +346,27 @@ int gs_stepper_comm_init(gs_stepper* s, const void* id128, int32_t rank, int32_t
   s->comm_stage.store(1);
   GS_NCCL(ncclCommInitRank(&s->comm, nranks, id, rank));
   s->comm_live.store(s->comm);
+  // What RCCL actually formed: the rank count, this rank's place in it and the
+  // device its kernels run on must be the ones the layout and the stepper were built for.
+  {
+    int cnt = 0, ur = -1, dev = -1;
+    GS_NCCL(ncclCommCount(s->comm, &cnt));
+    GS_NCCL(ncclCommUserRank(s->comm, &ur));
+    GS_NCCL(ncclCommCuDevice(s->comm, &dev));
+    s->comm_count = cnt;
+    s->comm_user_rank = ur;
+    s->comm_cu_device = dev;
+    if (cnt != nranks || ur != rank || dev != s->cfg.device) {
+      char b[256];
+      snprintf(b, sizeof(b),
+               "comm_init: RCCL formed %d rank(s), this one rank %d on device %d; expected %d "
+               "rank(s), rank %d on device %d",
+               cnt, ur, dev, nranks, rank, s->cfg.device);
+      abort_comm(s);
+      gs_set_error(b);
+      return -1;
+    }
+  }
   // GRAVSIM_FORCE_COMM keeps a 1-rank communicator live so the full multi-rank schedule
   // (in-place ncclAllGather, local/remote split on two streams, events) runs on one GPU.
   s->have_comm = nranks > 1 || getenv("GRAVSIM_FORCE_COMM") != nullptr;
@@ -350,6 +374,7 @@ int gs_stepper_comm_init(gs_stepper* s, const void* id128, int32_t rank, int32_t
     s->comm_live.store(nullptr);
     (void)ncclCommDestroy(s->comm);
     s->comm = nullptr;
+    s->comm_count = 0;  // (none kept)
   }
   drop_graphs(s);
   if (s->have_comm) {
@@ -390,6 +415,14 @@ int gs_stepper_comm_init(gs_stepper* s, const void* id128, int32_t rank, int32_t
 }
 
 int32_t gs_stepper_comm_stage(gs_stepper* s) { return s ? s->comm_stage.load() : 0; }
+
+int gs_stepper_comm_info(gs_stepper* s, int32_t* count, int32_t* user_rank, int32_t* cu_device) {
+  if (!s) return -1;
+  if (count) *count = s->comm_count;
+  if (user_rank) *user_rank = s->comm_user_rank;
+  if (cu_device) *cu_device = s->comm_cu_device;
+  return 0;
+}
 
 int32_t gs_stepper_abort(gs_stepper* s) { return s && abort_comm(s) ? 1 : 0; }
 

@@ -111,8 +111,32 @@ int comm_do(gs_stepper* s, std::function<int()> fn) {
 
 // ---- cross-stream points: events, or device counters (flag sync) ------------------------
 uint64_t sync_limit_ticks(const gs_stepper* s) {
-  const double t = s->step_timeout_s > 0 ? s->step_timeout_s : 600.0;
+  double t = s->step_timeout_s > 0 ? 2.0 * s->step_timeout_s + 10.0 : 600.0;
+  if (const char* v = getenv("GRAVSIM_SYNC_LIMIT_S")) t = atof(v);
   return (uint64_t)(t * s->clk_khz * 1e3);
+}
+
+int write_sync_limit(gs_stepper* s) {
+  if (!s->sync_stats) return 0;
+  const unsigned long long v = sync_limit_ticks(s);
+  // (a blocking copy from pageable memory: the word is current before any later enqueue; the
+  // streams are non-blocking, so nothing in flight is waited for)
+  GS_HIP(hipMemcpy(s->sync_stats + 9, &v, sizeof(v), hipMemcpyHostToDevice));
+  return 0;
+}
+
+bool sync_failed(gs_stepper* s) {
+  if (!s->sync_fail || s->sync_fail[0] == 0u) return false;
+  if (s->have_comm) {
+    abort_comm(s);
+    s->have_comm = false;
+  }
+  gs_set_error(s->sync_fail[0] == 1u
+                   ? "flag sync: a cross-stream wait gave up (a collective or a peer stalled "
+                     "past the device bound); the step's results are invalid"
+                   : "flag sync: the communicator was aborted while a step waited on it; the "
+                     "step's results are invalid");
+  return true;
 }
 
 int comp_signal(gs_stepper* s, hipEvent_t ev, int id, unsigned* clear) {
@@ -127,7 +151,7 @@ int comm_wait_comp(gs_stepper* s, hipEvent_t ev, int id) {
     return 0;
   }
   GS_HIP(gs::launch_sync_wait(s->sync_buf + 2 * id, s->sync_buf + 2 * id + 1, s->sync_stats + 6,
-                              sync_limit_ticks(s), s->s_comm));
+                              s->sync_stats + 9, s->sync_fail_dev, s->s_comm));
   return 0;
 }
 
@@ -141,10 +165,11 @@ int comp_wait_comm(gs_stepper* s, hipEvent_t ev, int mark, int id, const unsigne
   if (!fsync(s)) return comp_wait(s, ev, mark);
   unsigned long long* st = s->sync_stats + (mark == kMarkExchange ? 3 : 0);
   if (flag) {
-    GS_HIP(gs::launch_sync_wait(flag, nullptr, st, sync_limit_ticks(s), s->s_comp));
+    GS_HIP(gs::launch_sync_wait(flag, nullptr, st, s->sync_stats + 9, s->sync_fail_dev,
+                                s->s_comp));
   } else {
     GS_HIP(gs::launch_sync_wait(s->sync_buf + 2 * id, s->sync_buf + 2 * id + 1, st,
-                                sync_limit_ticks(s), s->s_comp));
+                                s->sync_stats + 9, s->sync_fail_dev, s->s_comp));
   }
   return 0;
 }
@@ -236,6 +261,9 @@ int run_plan_fsync(gs_stepper* s) {
       pe[0]->nsteps = 2;
       pe[1]->nsteps = 0;  // (comm spans of step 1 only)
     } else {
+      // (the 256-set cap: a lone first set would never be recorded, so phase_stats must not
+      // count it)
+      if (pe[0]) --s->pev_used;
       pe[0] = pe[1] = nullptr;
     }
   }
@@ -318,6 +346,7 @@ int wait_until(gs_stepper* s, int64_t target, double timeout_s) {
       ++s->prog_done;
       last = std::chrono::steady_clock::now();
     }
+    if (sync_failed(s)) return -1;
     bool done = s->prog_done >= target;
     if (all) {
       hipError_t a = hipStreamQuery(s->s_comp);
@@ -349,6 +378,9 @@ int wait_until(gs_stepper* s, int64_t target, double timeout_s) {
         abort_comm(s);
         s->have_comm = false;
       }
+      // flag-sync waits still spinning fall through instead of holding the streams until
+      // their own (longer) bound; the stepper stays failed
+      if (s->sync_fail && s->sync_fail[0] == 0u) s->sync_fail[0] = 2u;
       gs_set_error(m);
       return -1;
     }

@@ -220,6 +220,14 @@ int gs_stepper_set_cutoff_mode(gs_stepper* s, int32_t mode);
 // schedules.
 int gs_stepper_audit(gs_stepper* s, uint64_t* units_done, uint64_t* units_per_step);
 int gs_stepper_audit_reset(gs_stepper* s);
+// Engine clock of the sym force launches since the last call (then reset; waits for the
+// compute stream): out4[0] the duration-weighted shader clock (GHz, s_memtime against
+// s_memrealtime per workgroup), [1] workgroup shader-cycles, [2] workgroup-seconds, [3]
+// workgroups. All 0 for the one-sided schedules.
+int gs_stepper_clock(gs_stepper* s, double* out4);
+// Compiled force-tile shape of the sym kernels for fp64 (0) or fp32: *waves per workgroup,
+// *ipl i-bodies and *jpl j-bodies per lane (bench.py builds its kernel label from this).
+int gs_sym_tile_shape(int32_t fp64, int32_t* waves, int32_t* ipl, int32_t* jpl);
 // What the last replayed steps ran from: *mode 0 eager, 1 one hipGraph per two steps, 2 a
 // segmented plan (multi-rank: compute segments as graphs, collectives eager between them);
 // *segments = graph segments per two steps (mode 2).
@@ -251,6 +259,10 @@ int gs_stepper_comm_check(gs_stepper* s);
 // 0 not started, 1 in ncclCommInitRank, 2 warm-up all-gather, 3 warm-up ring send/recv,
 // 4 warm-up peer send/recv, 5 waiting for the warm-up, 6 done, -1 aborted.
 int32_t gs_stepper_comm_stage(gs_stepper* s);
+// What the communicator is (ncclCommCount, ncclCommUserRank, ncclCommCuDevice, read at init
+// and checked there against nranks / rank / the stepper's device): count 0 before comm_init
+// or when none was kept (one rank).
+int gs_stepper_comm_info(gs_stepper* s, int32_t* count, int32_t* user_rank, int32_t* cu_device);
 // Abort the live RCCL communicator once (ncclCommAbort; callable from another thread to
 // unblock collectives that will never complete). Returns 1 if it aborted, 0 if there was none.
 int32_t gs_stepper_abort(gs_stepper* s);

@@ -138,6 +138,14 @@ struct SymArgs {
   // completed and released its writes at the kernel boundary). Saves the one-lane signal
   // kernel between two stages. nullptr: none.
   unsigned* sig;
+  // Engine-clock record of the force launches (nullptr: off): wave 0 of every workgroup reads
+  // s_memtime (shader clock) and s_memrealtime (100 MHz) when it starts and when it leaves,
+  // and adds the two differences and a count to clk[0..2] (one relaxed atomic each). The
+  // duration-weighted clock the launch ran at is clk[0] / clk[1] x 100 MHz, and clk[0] is the
+  // workgroup-cycles it took: a cost in cycles, independent of the box's DVFS state
+  // (bench.py engine_clock_ghz / cycles_per_pair_eval). Diagnostic only: no output value
+  // depends on it.
+  unsigned long long* clk;
 };
 
 hipError_t launch_force_sym(const SymArgs& a, hipStream_t s);
@@ -165,10 +173,12 @@ hipError_t launch_gate_set(unsigned* gate, hipStream_t s);
 // zeroing the level flag `clear`, if given); wait =
 // one wave polling `flag` until it passes seen[0] (a counter; seen nullptr: a level flag),
 // adding its stall to stats[0] (s_memrealtime ticks) and 1 to stats[1]; gives up after
-// limit_ticks (counted in stats[2]).
+// *limit_ticks (a device word) or once the sticky host-mapped word *fail is set, counting it
+// in stats[2], setting *fail and leaving seen[0] as it was.
 hipError_t launch_sync_signal(unsigned* count, unsigned* clear, hipStream_t s);
 hipError_t launch_sync_wait(const unsigned* flag, unsigned* seen, unsigned long long* stats,
-                            uint64_t limit_ticks, hipStream_t s);
+                            const unsigned long long* limit_ticks, unsigned* fail,
+                            hipStream_t s);
 hipError_t launch_sym_block_reduce(const SymArgs& a, hipStream_t s);  // band leaves -> Bbuf
 hipError_t launch_sym_node_reduce(const SymArgs& a, hipStream_t s);   // own nodes -> Sbuf
 hipError_t launch_sym_row_reduce(const SymArgs& a, hipStream_t s);    // the band's rows -> Ti

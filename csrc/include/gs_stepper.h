@@ -76,6 +76,10 @@ struct gs_stepper {
   // another thread): the handle once ncclCommInitRank returned it, and the init stage.
   std::atomic<ncclComm_t> comm_live{nullptr};
   std::atomic<int> comm_stage{0};
+  // What RCCL formed (ncclCommCount / ncclCommUserRank / ncclCommCuDevice after init): checked
+  // against the layout's nranks / rank and the stepper's device there, reported by
+  // gs_stepper_comm_info (bench.py enforces one distinct GPU per rank on top of it).
+  int32_t comm_count = 0, comm_user_rank = -1, comm_cu_device = -1;
   bool virt = false;  // member of a virtual-rank group (gather = device copies, gs_group_step)
   bool emulate = false;  // GRAVSIM_EMULATE_RANK: run one rank's launch shapes, no exchange
   // sym work beside a pending gather (GRAVSIM_SYM_OVERLAP, gs_stepper_set_overlap): 0 none
@@ -171,6 +175,9 @@ struct gs_stepper {
   // units it ran); a step runs rows x (S + D + (Np - 1) Kr) units on this rank (each split
   // segment counts as its Np parts) whatever the launch split or fetch order.
   unsigned long long* audit = nullptr;
+  // Engine-clock record of the sym force launches (SymArgs::clk): {shader cycles, 100 MHz
+  // ticks, workgroups} summed since the last gs_stepper_clock read.
+  unsigned long long* clk = nullptr;
   // Fault injection for the audit's own test (GRAVSIM_FAULT_SKIP_UNITS=k): every dynamic
   // force launch starts its unit counter at k instead of 0, so units 0 .. k-1 never run,
   // exactly the failure class of a stale re-armed counter (a memset node when captured).
@@ -214,8 +221,16 @@ struct gs_stepper {
   // no cut points. sync_buf[2 id] = signals of point id, [2 id + 1] = waits taken (kSync*);
   // sync_stats[3 k] = {stall ticks, waits, timeouts} of the compute stream's gather (k 0) and
   // exchange (k 1) waits, k 2 the comm stream's waits. GRAVSIM_SYNC=events keeps the events.
+  // sync_stats[9]: the wait kernels' give-up bound in s_memrealtime ticks (a device word,
+  // written by gs_stepper_set_timeout: captured graphs read the current value). sync_fail: a
+  // sticky host-mapped word (hipHostMalloc, coherent) a wait that gave up sets, and the host
+  // sets when it aborts the communicator; nonzero fails sync / wait / state reads
+  // (sync_failed) and makes every later wait kernel fall through. [0] host view, device
+  // pointer in sync_fail_dev.
   unsigned* sync_buf = nullptr;
   unsigned long long* sync_stats = nullptr;
+  volatile unsigned* sync_fail = nullptr;
+  unsigned* sync_fail_dev = nullptr;
   bool sync_events = false;  // GRAVSIM_SYNC=events
   bool plan_fsync = false;   // the recorded plan is one graph (flag sync) + comm host ops
 };
@@ -308,8 +323,15 @@ int ring_src(const gs_stepper* s, int sub);
 void rank_chunks(const gs_stepper* s, int src, int* c0, int* c1);
 int ring_xfer_rccl(gs_stepper* s, int cur, int sub);
 int sym_reduce_exchange(gs_stepper* s, const gs::SymArgs& a0, bool* exchanged, bool* row_done);
-// The flag-sync wait bound in s_memrealtime ticks (the native step timeout, 600 s if none).
+// The flag-sync wait bound in s_memrealtime ticks: above the host's own progress bound
+// (2 x the step timeout + 10 s, 600 s if unbounded; GRAVSIM_SYNC_LIMIT_S overrides, a test
+// knob), so the host's abort wins a stall.
 uint64_t sync_limit_ticks(const gs_stepper* s);
+// Write it to the device word the wait kernels read (sync_stats[9]).
+int write_sync_limit(gs_stepper* s);
+// A flag-sync wait gave up (or the host aborted the communicator under one): sets the error,
+// aborts a live communicator, returns true. Every host-side completion point checks it.
+bool sync_failed(gs_stepper* s);
 void maybe_install_crash_trace();
 // ncclCommAbort once (the watchdog thread, a timeout or an async error may all ask for it).
 bool abort_comm(gs_stepper* s);

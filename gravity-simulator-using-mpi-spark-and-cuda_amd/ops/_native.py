@@ -180,6 +180,10 @@ def hip_lib():
         _sig(lib, "gs_stepper_set_persist", c_int32, [S, c_int32], optional=True)
         _sig(lib, "gs_stepper_audit", c_int32, [S, POINTER(c_uint64), POINTER(c_uint64)])
         _sig(lib, "gs_stepper_audit_reset", c_int32, [S])
+        # (optional: A/B runs load round-5 builds, which have neither)
+        _sig(lib, "gs_stepper_clock", c_int32, [S, _PD], optional=True)
+        _sig(lib, "gs_sym_tile_shape", c_int32, [c_int32] + [POINTER(c_int32)] * 3,
+             optional=True)
         _sig(lib, "gs_stepper_graph_info", c_int32, [S, POINTER(c_int32), POINTER(c_int32)])
         _sig(lib, "gs_stepper_mem_entry", c_int32,
              [S, c_int32, POINTER(ctypes.c_char_p), POINTER(c_uint64)])
@@ -193,6 +197,7 @@ def hip_lib():
         _sig(lib, "gs_stepper_comm_check", c_int32, [S])
         _sig(lib, "gs_stepper_comm_stage", c_int32, [S])
         _sig(lib, "gs_stepper_abort", c_int32, [S])
+        _sig(lib, "gs_stepper_comm_info", c_int32, [S] + [POINTER(c_int32)] * 3, optional=True)
         _sig(lib, "gs_hip_device_count", c_int32, [])
         VP = POINTER(c_void_p)
         _sig(lib, "gs_dev_alloc", c_int32, [c_int32, c_uint64, VP])
@@ -208,6 +213,24 @@ def hip_lib():
         _sig(lib, "gs_hip_kernel_info", ctypes.c_char_p, [])
         _hip = lib
         return lib
+
+
+def sym_tile_shape(fp64: bool) -> dict:
+    """Compiled register-tile shape of the sym force kernels (nbody_sym.hip Shape<T>): waves
+    per workgroup and i / j bodies per lane."""
+    lib = hip_lib()
+    w, i, j = c_int32(), c_int32(), c_int32()
+    lib.gs_sym_tile_shape(int(bool(fp64)), ctypes.byref(w), ctypes.byref(i), ctypes.byref(j))
+    return {"waves": w.value, "ipl": i.value, "jpl": j.value}
+
+
+def sym_kernel_label(fp64: bool) -> str:
+    """bench.py's description of the sym force kernel, from the compiled tile shape."""
+    t = sym_tile_shape(fp64)
+    tile = (f"{t['ipl']} i x {t['jpl']} j per lane, "
+            + ("fp64" if fp64 else "j-pair packed fp32" if t["jpl"] == 2 else "fp32"))
+    return (f"sym: register tile (LDS-staged j, DPP carriers), {tile}, {t['waves']} waves, "
+            "cyclic half-shell of 2048-body chunks")
 
 
 def check(lib, rc: int, what: str) -> None:

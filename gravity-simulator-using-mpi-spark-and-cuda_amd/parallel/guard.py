@@ -93,8 +93,9 @@ class RunGuard:
         self.poll_s, self.ack_wait_s = poll_s, ack_wait_s
         self.out = out  # stream of rank 0's JSON line (default: file descriptor 1)
         self.t_start = time.time()
+        self.job = job_id()
         self.rec: dict = {"rank": rank, "pid": os.getpid(), "stage": "start", "status": "running",
-                          "t_stage": self.t_start, "t_start": self.t_start}
+                          "t_stage": self.t_start, "t_start": self.t_start, "job": self.job}
         self._deadline: Optional[float] = None
         self._aborts: list[Callable[[], None]] = []
         self._probes: list[Callable[[], dict]] = []
@@ -214,9 +215,12 @@ class RunGuard:
                                    f"{rec.get('stage')}: {rec.get('error', '')[:500]}")
 
     def _peer_records(self) -> list[dict]:
-        """Peer records of THIS job: a record left in a reused directory by an earlier job (its
-        process gone, or started long before this guard) is ignored until the peer of this job
-        overwrites it, so it cannot fire a false error."""
+        """Peer records of THIS job: a record left in a reused directory by an earlier job (a
+        different job id, or started long before this guard) is ignored until the peer of this
+        job overwrites it, so it cannot fire a false error. Whether the peer's
+        process is still alive does not matter: a peer of this job that recorded "failed" or
+        "timeout" and exited is still reported, and with a GRAVSIM_GUARD_DIR shared across
+        nodes a remote pid says nothing at all."""
         out = []
         for r in range(1, self.world):
             try:
@@ -224,8 +228,8 @@ class RunGuard:
                     rec = json.load(f)
             except (OSError, ValueError):
                 continue
-            if _pid_alive(rec.get("pid")) and float(rec.get("t_start") or 0.0) >= \
-                    self.t_start - STALE_RECORD_S:
+            same_job = not (self.job and rec.get("job")) or rec.get("job") == self.job
+            if same_job and float(rec.get("t_start") or 0.0) >= self.t_start - STALE_RECORD_S:
                 out.append(rec)
         return out
 
@@ -278,14 +282,18 @@ class RunGuard:
 STALE_RECORD_S = 120.0
 
 
-def _pid_alive(pid) -> bool:
-    try:
-        os.kill(int(pid), 0)
-    except (TypeError, ValueError, ProcessLookupError):
-        return False
-    except PermissionError:
-        return True
-    return True
+def job_id() -> str:
+    """Identity of the job every rank of it shares: torchrun's rendezvous run id when it names
+    one, else the rendezvous endpoint (MASTER_ADDR:MASTER_PORT); GRAVSIM_JOB_ID overrides.
+    "" when none is known (a single process): records are then filtered by start time only."""
+    if os.environ.get("GRAVSIM_JOB_ID"):
+        return os.environ["GRAVSIM_JOB_ID"]
+    run_id = os.environ.get("TORCHELASTIC_RUN_ID", "")
+    if run_id not in ("", "none"):
+        return run_id
+    if os.environ.get("MASTER_PORT"):
+        return f"{os.environ.get('MASTER_ADDR', '')}:{os.environ['MASTER_PORT']}"
+    return ""
 
 
 STEP_TIMEOUT_FLOOR_S = 60.0

@@ -96,6 +96,14 @@ class HipEngine:
         _native.check(lib, lib.gs_rccl_unique_id(buf), "rccl unique id")
         return buf.raw
 
+    def comm_info(self) -> dict:
+        """What RCCL formed for this rank (ncclCommCount / UserRank / CuDevice, checked
+        natively at comm_init): rccl_nranks 0 when no communicator is kept (one rank)."""
+        c, r, d = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
+        _native.check(self.lib, self.lib.gs_stepper_comm_info(
+            self._s, ctypes.byref(c), ctypes.byref(r), ctypes.byref(d)), "comm info")
+        return {"rccl_nranks": c.value, "rccl_rank": r.value, "rccl_device": d.value}
+
     def comm_check(self) -> None:
         _native.check(self.lib, self.lib.gs_stepper_comm_check(self._s), "rccl health")
 
@@ -271,6 +279,17 @@ class HipEngine:
             self.lib.gs_stepper_mem_entry(self._s, i, ctypes.byref(tag), ctypes.byref(nb))
             out[tag.value.decode()] = out.get(tag.value.decode(), 0) + int(nb.value)
         return out
+
+    def clock(self) -> dict:
+        """Engine clock of the sym force launches since the last call (then reset): each
+        workgroup's s_memtime span against its s_memrealtime span. ghz: the duration-weighted
+        shader clock; wg_cycles: workgroup shader-cycles (a cost independent of the DVFS
+        state); wg_seconds, workgroups. Zeros for the one-sided schedules. Waits for the GPU."""
+        out = (ctypes.c_double * 4)()
+        if hasattr(self.lib, "gs_stepper_clock"):  # (round-5 builds for A/B runs: zeros)
+            _native.check(self.lib, self.lib.gs_stepper_clock(self._s, out), "clock")
+        return {"ghz": out[0], "wg_cycles": out[1], "wg_seconds": out[2],
+                "workgroups": int(out[3])}
 
     def audit_reset(self) -> None:
         _native.check(self.lib, self.lib.gs_stepper_audit_reset(self._s), "audit reset")

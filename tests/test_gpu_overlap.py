@@ -231,3 +231,45 @@ def test_stalled_step_trips_step_timeout(hip, monkeypatch):
             e.sync(timeout_s=0.3)
     finally:
         e.close()
+
+
+def test_device_wait_give_up_fails_sync(hip, monkeypatch):
+    """A flag-sync wait kernel that gives up (here its device bound forced to 0.2 s against a
+    ~1.8 s modeled gather, the host's own progress bound 30 s) must not let the step finish
+    silently on an unfinished gather: it sets the sticky failure word, later waits fall
+    through, and sync() raises. Without the bound override the device waits
+    outlast the host's timeout (2 x timeout + 10 s), so the host abort wins a stall."""
+    monkeypatch.setenv("GRAVSIM_SYNC_LIMIT_S", "0.2")
+    e = _emu(monkeypatch, 65536, 8, 3, 0.0005, 0)
+    try:
+        e.set_step_timeout(30.0)
+        e.init_ics("solar+random", 2)
+        e.step(2)
+        with pytest.raises(RuntimeError, match="flag sync: a cross-stream wait gave up"):
+            e.sync()
+        with pytest.raises(RuntimeError, match="flag sync"):
+            e.state()  # a state the wait gave up on is never returned
+    finally:
+        e.close()
+
+
+def test_host_step_timeout_beats_device_wait_bound(hip, monkeypatch):
+    """With the default device bound (2 x the step timeout + 10 s) a stalled gather trips the
+    host's 0.3 s progress bound first; the host then releases the spinning wait kernels
+    (failure word), so close() does not sit out the device bound, and the stepper stays
+    failed."""
+    import time
+
+    e = _emu(monkeypatch, 65536, 8, 3, 0.0005, 0)
+    try:
+        e.set_step_timeout(0.3)
+        e.init_ics("solar+random", 2)
+        e.step(2)
+        with pytest.raises(RuntimeError, match="step timeout: no step completed"):
+            e.sync()
+        with pytest.raises(RuntimeError, match="flag sync"):
+            e.sync()
+    finally:
+        t0 = time.perf_counter()
+        e.close()
+        assert time.perf_counter() - t0 < 5.0  # the 1.8 s modeled gather, not a 10.6 s wait

@@ -197,3 +197,27 @@ def test_stale_peer_record_of_an_earlier_job_is_ignored(tmp_path):
         assert [r["error"] for r in g._peer_records()] == ["this job"]
     finally:
         g._closed = True
+
+
+def test_failed_record_of_an_exited_peer_of_this_job_is_reported(tmp_path, monkeypatch):
+    """A peer of THIS job that recorded "failed" and exited (its pid gone) is still reported,
+    and so is one whose pid lives on another node (a shared GRAVSIM_GUARD_DIR); a record with
+    another job id is not (the filter is the job and its start time, not pid
+    liveness)."""
+    import io
+
+    from gravsim.parallel import guard as gd
+
+    monkeypatch.setenv("GRAVSIM_JOB_ID", "job-a")
+    g = gd.RunGuard(0, 3, lambda reason, recs: {"error": reason}, directory=str(tmp_path),
+                    poll_s=60.0, out=io.StringIO())
+    try:
+        now = time.time()
+        dead = {"rank": 1, "pid": 2 ** 22 + 4321, "stage": "timed", "status": "failed",
+                "error": "exited peer", "t_stage": now, "t_start": now, "job": "job-a"}
+        other = dict(dead, rank=2, error="other job", job="job-b")
+        (tmp_path / "rank1.json").write_text(json.dumps(dead))
+        (tmp_path / "rank2.json").write_text(json.dumps(other))
+        assert [r["error"] for r in g._peer_records()] == ["exited peer"]
+    finally:
+        g._closed = True

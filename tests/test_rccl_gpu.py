@@ -1,11 +1,18 @@
 """Real RCCL path (in-place all-gather + overlapped local chunks, ring pass, the sym
 schedule's node-sum send/recv) with 2 to 8 processes (P = 3, 5, 6: uneven slices).
 
-The GPU box exposes one MI355X, so every rank shares device 0. RCCL refuses two ranks of one
-host on one device ("Duplicate GPU detected"), so each rank gets its own NCCL_HOSTID: RCCL
-then treats the ranks as separate hosts and moves data through its socket transport over
-loopback instead of xGMI. The collectives, peer calls, stream/event ordering and buffer
-offsets of the multi-rank schedule are the production ones; only the transport differs.
+Two families:
+* one device for every rank (always run): the GPU box usually exposes one MI355X, and RCCL
+  refuses two ranks of one host on one device ("Duplicate GPU detected"), so each rank gets its
+  own NCCL_HOSTID: RCCL then treats the ranks as separate hosts and moves data through its
+  socket transport over loopback instead of xGMI. The collectives, peer calls, stream/event
+  ordering and buffer offsets of the multi-rank schedule are the production ones; only the
+  transport differs.
+* one distinct device per rank (run when the box shows at least that many GPUs, skipped
+  otherwise): no NCCL_HOSTID, LOCAL_RANK = rank, so RCCL connects the ranks peer-to-peer over
+  xGMI. These check what the one-device family cannot: what RCCL formed (ncclCommCount /
+  UserRank / CuDevice), the P2P transport, the gated launch's system-scope gate with remote
+  writes, the collectives captured into the step graph, and a dead peer on another GPU.
 """
 import json
 import os
@@ -28,10 +35,19 @@ def _port():
 
 
 def _worker(rank, world, port, out_dir, n, steps, strategy="allgather", mode="auto",
-            dtype="fp32", env=None):
-    # one "host" per rank (see the module docstring): gravsim.parallel.comm.rccl_rank_hosts
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
-                      WORLD_SIZE=str(world), LOCAL_RANK="0", GRAVSIM_RCCL_RANK_HOSTS="1")
+            dtype="fp32", env=None, devices=False):
+    if devices:
+        # one GPU per rank, one host: RCCL's intra-node transports (P2P over xGMI); the INFO
+        # log names the transport of every connection
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                          WORLD_SIZE=str(world), LOCAL_RANK=str(rank), NCCL_DEBUG="INFO",
+                          NCCL_DEBUG_SUBSYS="INIT,P2P,NET",
+                          NCCL_DEBUG_FILE=os.path.join(out_dir, f"rccl.{rank}.log"))
+        os.environ.pop("GRAVSIM_RCCL_RANK_HOSTS", None)
+    else:
+        # one "host" per rank (see the module docstring): gravsim.parallel.comm.rccl_rank_hosts
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                          WORLD_SIZE=str(world), LOCAL_RANK="0", GRAVSIM_RCCL_RANK_HOSTS="1")
     os.environ.update(env or {})
     if os.environ.get("GRAVSIM_TEST_NCCL_DEBUG"):  # diagnostics: RCCL INFO log per rank
         os.makedirs(os.environ["GRAVSIM_TEST_NCCL_DEBUG"], exist_ok=True)
@@ -57,7 +73,7 @@ def _worker(rank, world, port, out_dir, n, steps, strategy="allgather", mode="au
         cfg = SimConfig(n=n, dtype=dtype, device="gpu", chunk=1024, step_timeout_s=120,
                         strategy=strategy, mode=mode.removesuffix("-graph").removesuffix("-eager"),
                         graph_comm=graph_comm, graph=not eager)
-        eng = HipEngine(cfg, rank, world, device=0, dist=dist)
+        eng = HipEngine(cfg, rank, world, device=rank if devices else 0, dist=dist)
         uid = HipEngine.unique_id() if rank == 0 else None
         uid = comm.broadcast_bytes(dist, uid)
         t_mark.append(("engine", time.perf_counter()))
@@ -68,6 +84,16 @@ def _worker(rank, world, port, out_dir, n, steps, strategy="allgather", mode="au
         t_mark.append(("rccl_init", time.perf_counter()))
         ok = comm.allreduce_sum(dist, 0.0 if status == "ok" else 1.0)
         if ok == 0:
+            import torch
+
+            from gravsim.parallel.guard import parse_rccl_log
+
+            p = torch.cuda.get_device_properties(eng.device)
+            with open(os.path.join(out_dir, f"topo{rank}.json"), "w") as f:
+                json.dump({"rank": rank, "device": eng.device, "host": "this",
+                           "pci": f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}",
+                           **eng.comm_info(),
+                           **parse_rccl_log(os.environ.get("NCCL_DEBUG_FILE"))}, f)
             eng.init_ics("solar+random", 5)
             eng.audit_reset()
             eng.step(steps)
@@ -155,9 +181,13 @@ _GRAPH_COMM_XFAIL = pytest.mark.xfail(
 def test_rccl_multi_rank_match_single_rank(hip, tmp_path, world, strategy, mode, dtype, n, env):
     """P real RCCL ranks (one process each) give the same bits as one rank without a
     communicator (the canonical decomposition makes the result P-independent)."""
-    steps = 5
+    _run_and_check(tmp_path, world, strategy, mode, dtype, n, env, devices=False)
+
+
+def _run_and_check(tmp_path, world, strategy, mode, dtype, n, env, devices, steps=5):
+    tmp_path.mkdir(parents=True, exist_ok=True)
     mp.start_processes(_worker, args=(world, _port(), str(tmp_path), n, steps, strategy, mode,
-                                      dtype, env),
+                                      dtype, env, devices),
                        nprocs=world, start_method="spawn", join=True)
     status = open(tmp_path / "status.txt").read()
     assert status == "ok", f"RCCL with {world} ranks: {status[:300]}"
@@ -176,6 +206,11 @@ def test_rccl_multi_rank_match_single_rank(hip, tmp_path, world, strategy, mode,
                 # flag sync (all-gather): one compute graph per period; the ring's event
                 # points cut it into segments
                 assert (int(segs) >= 4) if strategy == "ring" else (int(segs) == 1), segs
+    # what RCCL formed: the whole job, this rank, the device the rank bound
+    topo = [json.loads(open(tmp_path / f"topo{r}.json").read()) for r in range(world)]
+    for t in topo:
+        assert (t["rccl_nranks"], t["rccl_rank"], t["rccl_device"]) == \
+            (world, t["rank"], t["device"]), t
     eng = HipEngine(SimConfig(n=n, dtype=dtype, device="gpu", chunk=1024, mode=mode))
     eng.init_ics("solar+random", 5)
     eng.step(steps)
@@ -189,6 +224,61 @@ def test_rccl_multi_rank_match_single_rank(hip, tmp_path, world, strategy, mode,
     assert np.array_equal(vel, ref.vel)
     # every multi-rank schedule times its collectives (all-gather or ring stages + exchange)
     assert float(open(tmp_path / "comm_ms.txt").read()) > 0.0
+    return topo
+
+
+def _need_devices(hip, world):
+    n = int(hip.gs_hip_device_count())
+    if n < world:
+        pytest.skip(f"needs {world} distinct GPUs, the box shows {n}")
+
+
+@pytest.mark.parametrize("world,strategy,mode,dtype,n,env", [
+    (2, "allgather", "sym", "fp32", 20000, OV3),
+    (2, "allgather", "sym", "fp64", 20000, None),
+    (3, "allgather", "sym", "fp32", 40000, None),  # uneven blocks: broadcast group
+    (4, "allgather", "sym", "fp32", 40000, OV3),
+    (4, "ring", "sym", "fp32", 40000, None),
+    (8, "allgather", "sym", "fp32", 40000, OV3),   # the headline shape: gated + node exchange
+    (8, "allgather", "sym", "fp32", 40000, OV0),
+    (8, "allgather", "sym-eager", "fp32", 40000, OV3),
+    (8, "ring", "sym", "fp32", 40000, None),
+    (8, "allgather", "auto", "fp32", 9000, None),   # one-sided split schedule
+])
+def test_rccl_distinct_devices_match_single_rank(hip, tmp_path, world, strategy, mode, dtype, n,
+                                                 env):
+    """One process per distinct GPU (no NCCL_HOSTID): RCCL's peer-to-peer transport over
+    xGMI, the gated launch reading rows that peers wrote through the system-scope gate, and
+    the node-sum exchange between devices; bitwise equal to one rank, and every connection
+    P2P, none through a network transport (VERDICT r5 next #1)."""
+    _need_devices(hip, world)
+    topo = _run_and_check(tmp_path, world, strategy, mode, dtype, n, env, devices=True)
+    assert len({t["pci"] for t in topo}) == world, topo  # one GPU per rank
+    from gravsim.parallel import verify
+
+    for t in topo:
+        assert t["transports"], f"rank {t['rank']}: no transport parsed from the RCCL log"
+    assert verify.topology_problems(world, topo) == [], topo
+    assert verify.transport_summary(topo)["p2p"], topo
+
+
+@pytest.mark.parametrize("world,mode,n,env", [
+    (2, "sym-graph", 20000, None),
+    (2, "auto-graph", 5000, None),      # one-sided split: the all-gather captured
+    (4, "sym-graph", 40000, OV3),       # gated launch + gate kernels + exchange captured
+    (8, "sym-graph", 40000, OV3),
+])
+def test_rccl_graph_comm_distinct_devices(hip, tmp_path, world, mode, n, env):
+    """--graph-comm on real devices: the whole multi-rank step, RCCL collectives included,
+    captured in one hipGraph and replayed, bitwise equal to eager steps and to one rank. Over
+    the one-device socket transport this capture crashes (the xfail above); on distinct GPUs
+    it runs automatically (VERDICT r5 next #6)."""
+    _need_devices(hip, world)
+    _run_and_check(tmp_path / "graph", world, "allgather", mode, "fp32", n, env, devices=True)
+    eager = mode.replace("-graph", "-eager")
+    _run_and_check(tmp_path / "eager", world, "allgather", eager, "fp32", n, env, devices=True)
+    assert np.array_equal(np.load(tmp_path / "graph" / "pos.npy"),
+                          np.load(tmp_path / "eager" / "pos.npy"))
 
 
 @pytest.mark.parametrize("graph,strategy", [(1, "allgather"), (2, "allgather"), (1, "ring"),
@@ -244,13 +334,15 @@ def test_rccl_one_rank_full_schedule_bitwise(hip, monkeypatch, graph, strategy):
     assert np.array_equal(got, ref)
 
 
-def _dead_peer_worker(rank, world, port, out_dir):
+def _dead_peer_worker(rank, world, port, out_dir, devices=False):
     """Rank 1 dies after the communicator is up, before any step's collective; rank 0 steps
     and must get an error from its bounded wait instead of hanging in the exchange."""
     import time
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
-                      WORLD_SIZE=str(world), LOCAL_RANK="0", GRAVSIM_RCCL_RANK_HOSTS="1")
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank) if devices else "0")
+    if not devices:
+        os.environ["GRAVSIM_RCCL_RANK_HOSTS"] = "1"
     import gravsim  # noqa: F401
     from gravsim.config import SimConfig
     from gravsim.parallel import comm
@@ -259,7 +351,7 @@ def _dead_peer_worker(rank, world, port, out_dir):
     dist = comm.init(timeout_s=60)
     cfg = SimConfig(n=20000, dtype="fp32", device="gpu", chunk=1024, mode="sym",
                     step_timeout_s=10)
-    eng = HipEngine(cfg, rank, world, device=0, dist=dist)
+    eng = HipEngine(cfg, rank, world, device=rank if devices else 0, dist=dist)
     uid = HipEngine.unique_id() if rank == 0 else None
     eng.comm_init(comm.broadcast_bytes(dist, uid))
     eng.init_ics("solar+random", 5)
@@ -279,14 +371,18 @@ def _dead_peer_worker(rank, world, port, out_dir):
     os._exit(3 if "communicator aborted" in msg else 4)  # skip teardown with a dead peer
 
 
-def test_rccl_dead_peer_aborts_instead_of_hanging(hip, tmp_path):
+@pytest.mark.parametrize("devices", [False, True], ids=["one-device", "two-devices"])
+def test_rccl_dead_peer_aborts_instead_of_hanging(hip, tmp_path, devices):
     """Failure detection (the reference has none, cuda.cu:145-177): a dead peer
-    turns into an aborted communicator and a non-zero exit within the step timeout."""
+    turns into an aborted communicator and a non-zero exit within the step timeout (over
+    sockets on one device, and over P2P between two GPUs when the box has them)."""
     import multiprocessing
 
+    if devices:
+        _need_devices(hip, 2)
     ctx = multiprocessing.get_context("spawn")
     port = _port()
-    procs = [ctx.Process(target=_dead_peer_worker, args=(r, 2, port, str(tmp_path)))
+    procs = [ctx.Process(target=_dead_peer_worker, args=(r, 2, port, str(tmp_path), devices))
              for r in range(2)]
     for p in procs:
         p.start()
