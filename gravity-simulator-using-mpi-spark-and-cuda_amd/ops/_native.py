@@ -219,6 +219,8 @@ def sym_tile_shape(fp64: bool) -> dict:
     """Compiled register-tile shape of the sym force kernels (nbody_sym.hip Shape<T>): waves
     per workgroup and i / j bodies per lane."""
     lib = hip_lib()
+    if not hasattr(lib, "gs_sym_tile_shape"):  # (a round-5 build loaded for an A/B run)
+        return {}
     w, i, j = c_int32(), c_int32(), c_int32()
     lib.gs_sym_tile_shape(int(bool(fp64)), ctypes.byref(w), ctypes.byref(i), ctypes.byref(j))
     return {"waves": w.value, "ipl": i.value, "jpl": j.value}
@@ -227,6 +229,8 @@ def sym_tile_shape(fp64: bool) -> dict:
 def sym_kernel_label(fp64: bool) -> str:
     """bench.py's description of the sym force kernel, from the compiled tile shape."""
     t = sym_tile_shape(fp64)
+    if not t:
+        return "sym: register tile (this library does not report its tile shape)"
     tile = (f"{t['ipl']} i x {t['jpl']} j per lane, "
             + ("fp64" if fp64 else "j-pair packed fp32" if t["jpl"] == 2 else "fp32"))
     return (f"sym: register tile (LDS-staged j, DPP carriers), {tile}, {t['waves']} waves, "
