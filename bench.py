@@ -577,8 +577,11 @@ def run(a, g) -> int:
     ghz_max = comm.allreduce_max(dist, clk["ghz"])
     ghz_sum = comm.allreduce_sum(dist, clk["ghz"])
     wg_cycles = comm.allreduce_sum(dist, clk["wg_cycles"])
-    cus_total = comm.allreduce_sum(dist, float(torch.cuda.get_device_properties(
-        torch.cuda.current_device()).multi_processor_count))
+    # CUs of the distinct GPUs the job ran on (the one-GPU rehearsal's ranks share one)
+    cus_local = float(torch.cuda.get_device_properties(torch.cuda.current_device())
+                      .multi_processor_count)
+    cus_total = (float(sum({(r.get("host"), r.get("pci")): r.get("cus") or 0
+                            for r in ranks_info}.values())) if ranks_info else cus_local)
 
     # P-independence (untimed, P > 1): the multi-rank bits against one rank on rank 0's GPU.
     p_audit = None
