@@ -966,11 +966,13 @@ __global__ __launch_bounds__(256) void sym_finalize_kernel(SymArgs a) {
 // Ti round trip, two launches fewer: at 65K bodies the three took ~28 us plus launch gaps of
 // a 0.73 ms step). The sums keep the exact order of the three-kernel path, so the bits are
 // the same: Ti = h0 + h1 (ti_mid); S = the tree over the B row blocks (leaves row-ascending
-// from 0); a = Ti + S. Block: 6 waves over 64 bodies; wave w sums half w / 3 of component
-// w % 3 (coalesced partial reads), the second-half waves the j-side tree S too; wave 0 then
+// from 0); a = Ti + S. SPLIT: 6 waves over 64 bodies; wave w sums half w / 3 of component
+// w % 3 (coalesced partial reads), the second-half waves the j-side tree S too (65K: the tail
+// 28.8 -> 24.8 us, the step -0.6 %); else 3 waves, each thread both halves as two chains
+// (256K: the split form measured 1 % slower per step). Same sums either way; wave 0 then
 // integrates the 64 bodies.
-template <typename T>
-__global__ __launch_bounds__(384) void sym_tail_kernel(SymArgs a) {
+template <typename T, bool SPLIT>
+__global__ __launch_bounds__(SPLIT ? 384 : 192) void sym_tail_kernel(SymArgs a) {
   using V4 = sym::Vec4<T>;
   __shared__ T h1_s[3][64], s_s[3][64], acc_s[3][64];
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
@@ -993,9 +995,8 @@ __global__ __launch_bounds__(384) void sym_tail_kernel(SymArgs a) {
     const int segs = (16 * shell_len(X, a.NC) + a.L - 1) / a.L;
     const int ns = min(segs, a.S - a.Kr);
     const int m = ti_mid(a, segs, ns);
-    if (half == 0) {
-      h = ti_half0<T>(a, br, k, c, m);
-    } else {
+    if (half == 0) h = ti_half0<T>(a, br, k, c, m);
+    if (half == 1 || !SPLIT) {
       h1_s[k][l] = ti_half1<T>(a, br, k, c, m, ns, segs);
       // S: the tree over the B row blocks (sym_node_reduce_kernel's single node [0, B))
       TreeAcc<T, 1> t;
@@ -1192,11 +1193,16 @@ hipError_t launch_sym_finalize(const SymArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t launch_sym_tail(const SymArgs& a, hipStream_t s) {
+hipError_t launch_sym_tail(const SymArgs& a, hipStream_t s, bool split) {
   if (a.P != 1 || a.band_rows != a.rows) return hipErrorInvalidValue;  // one rank, one band
   const dim3 grid((unsigned)((a.n_local + 63) / 64));
-  if (a.fp64) hipLaunchKernelGGL(sym_tail_kernel<double>, grid, dim3(384), 0, s, a);
-  else hipLaunchKernelGGL(sym_tail_kernel<float>, grid, dim3(384), 0, s, a);
+  if (split) {
+    if (a.fp64) hipLaunchKernelGGL((sym_tail_kernel<double, true>), grid, dim3(384), 0, s, a);
+    else hipLaunchKernelGGL((sym_tail_kernel<float, true>), grid, dim3(384), 0, s, a);
+  } else {
+    if (a.fp64) hipLaunchKernelGGL((sym_tail_kernel<double, false>), grid, dim3(192), 0, s, a);
+    else hipLaunchKernelGGL((sym_tail_kernel<float, false>), grid, dim3(192), 0, s, a);
+  }
   return hipGetLastError();
 }
 

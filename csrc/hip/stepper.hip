@@ -479,7 +479,7 @@ int enqueue_sym(gs_stepper* s, int cur, bool need_gather, bool gathered_external
   }
   if (part & 2) {
     if (fused_tail(s)) {
-      GS_HIP(gs::launch_sym_tail(a, s->s_comp));
+      GS_HIP(gs::launch_sym_tail(a, s->s_comp, s->tail_split_on()));
     } else {
       GS_HIP(gs::launch_sym_finalize(a, s->s_comp));
     }
@@ -688,7 +688,7 @@ int accel_impl(gs_stepper* s, double* acc4, bool step_path) {
       sa.acc_out = s->acc;
       if (sym_force(s, sa, false, xcomm(s))) return -1;
       if (fused_tail(s)) {
-        GS_HIP(gs::launch_sym_tail(sa, s->s_comp));
+        GS_HIP(gs::launch_sym_tail(sa, s->s_comp, s->tail_split_on()));
       } else {
         GS_HIP(gs::launch_sym_finalize(sa, s->s_comp));
       }
@@ -761,6 +761,7 @@ int gs_stepper_create(const gs_config* cfg, gs_stepper** out) {
   }
   if (s->esz == 8) s->dyn_cap = 4;  // fp64: 512K 101.9-102.0 ms at 4 vs 102.0-102.5 at 2
   if (const char* v = getenv("GRAVSIM_FAULT_SKIP_UNITS")) s->fault_skip = (unsigned)atoi(v);
+  if (const char* v = getenv("GRAVSIM_TAIL_SPLIT")) s->tail_split = atoi(v);
   // GRAVSIM_SYNC=events: the multi-rank step orders its streams by hipEvents (and replays a
   // segmented plan) instead of device counters (flag sync, one graph per period)
   if (const char* v = getenv("GRAVSIM_SYNC")) s->sync_events = strcmp(v, "events") == 0;

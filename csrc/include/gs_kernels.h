@@ -186,7 +186,8 @@ hipError_t launch_sym_row_reduce(const SymArgs& a, hipStream_t s);    // the ban
 hipError_t launch_sym_node_row(const SymArgs& a, hipStream_t s);
 hipError_t launch_sym_finalize(const SymArgs& a, hipStream_t s);
 // One rank, one band: group reduce + row reduce + finalize in one kernel, same bits.
-hipError_t launch_sym_tail(const SymArgs& a, hipStream_t s);
+// split: the two halves of Ti in separate waves (small N), else in one thread (same bits).
+hipError_t launch_sym_tail(const SymArgs& a, hipStream_t s, bool split);
 int sym_occupancy(int fp64);
 
 template <typename T>

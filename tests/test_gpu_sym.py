@@ -235,13 +235,19 @@ def test_sym_bands_bitwise(hip, monkeypatch, P, dtype):
     assert np.array_equal(out[0].vel, out[1].vel)
 
 
-@pytest.mark.parametrize("n,dtype", [(20000, "fp32"), (65536, "fp32"), (40000, "fp64")])
+@pytest.mark.parametrize("n,dtype", [(20000, "fp32"), (65536, "fp32"), (262144, "fp32"),
+                                     (40000, "fp64")])
 def test_sym_fused_tail_bitwise(hip, monkeypatch, n, dtype):
     """One rank, one band: group reduce + row reduce + finalize fused into sym_tail_kernel
     keeps every sum's order, so steps and step-path accelerations are bitwise those of the
-    three-kernel tail (set_tuning(fused_tail=0))."""
+    three-kernel tail (set_tuning(fused_tail=0)), whether the tail sums Ti's two halves in
+    separate waves (GRAVSIM_TAIL_SPLIT=1, the small-N form) or in one thread (=0)."""
     out = []
-    for fused in (0, 1):
+    for fused, split in ((0, None), (1, "1"), (1, "0")):
+        if split is None:
+            monkeypatch.delenv("GRAVSIM_TAIL_SPLIT", raising=False)
+        else:
+            monkeypatch.setenv("GRAVSIM_TAIL_SPLIT", split)
         e = _engine(n, dtype)
         e.set_tuning(fused_tail=fused)
         e.init_ics("solar+random", 13)
@@ -249,9 +255,11 @@ def test_sym_fused_tail_bitwise(hip, monkeypatch, n, dtype):
         e.step(3)
         out.append((a, e.state()))
         e.close()
-    assert np.array_equal(out[0][0], out[1][0])
-    assert np.array_equal(out[0][1].pos, out[1][1].pos)
-    assert np.array_equal(out[0][1].vel, out[1][1].vel)
+    monkeypatch.delenv("GRAVSIM_TAIL_SPLIT", raising=False)
+    for a, st in out[1:]:
+        assert np.array_equal(out[0][0], a)
+        assert np.array_equal(out[0][1].pos, st.pos)
+        assert np.array_equal(out[0][1].vel, st.vel)
 
 
 @pytest.mark.parametrize("n,dtype,P,first_wave", [
