@@ -968,9 +968,9 @@ __global__ __launch_bounds__(256) void sym_finalize_kernel(SymArgs a) {
 // the same: Ti = h0 + h1 (ti_mid); S = the tree over the B row blocks (leaves row-ascending
 // from 0); a = Ti + S. SPLIT: 6 waves over 64 bodies; wave w sums half w / 3 of component
 // w % 3 (coalesced partial reads), the second-half waves the j-side tree S too (65K: the tail
-// 28.8 -> 24.8 us, the step -0.6 %); else 3 waves, each thread both halves as two chains
-// (256K: the split form measured 1 % slower per step). Same sums either way; wave 0 then
-// integrates the 64 bodies.
+// 28.8 -> 24.8 us, the step -0.4 to -0.6 %); else 3 waves, each thread both halves as two
+// chains (128K / 256K: the split form measured 0.6 / 1.3 % slower per step). Same sums either
+// way; wave 0 then integrates the 64 bodies.
 template <typename T, bool SPLIT>
 __global__ __launch_bounds__(SPLIT ? 384 : 192) void sym_tail_kernel(SymArgs a) {
   using V4 = sym::Vec4<T>;

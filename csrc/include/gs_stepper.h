@@ -157,10 +157,11 @@ struct gs_stepper {
   int fuse_tail = -1;         // -1 by size (<= 256K), 0 off, 1 on (gs_stepper_set_tuning)
   // fused tail: Ti's two halves in separate waves (1) or in one thread (0); -1 by size
   // (GRAVSIM_TAIL_SPLIT overrides, an A/B knob: same bits either way)
-  // The split pays where a thread's chain is long against a small grid: 65K (NC 32) -0.6 %
-  // per step; at 256K (NC 128) it measured 1 % slower (profiles/r6_tail_split_ab.jsonl).
+  // The split pays only where the grid is small: 65K (NC 32) 0.6875-0.6879 against
+  // 0.6886-0.6904 ms one-thread; 128K (NC 64) 2.638 against 2.622 ms and 256K 10.44-10.46
+  // against 10.31 ms, slower (profiles/r6_tail_split_ab.jsonl).
   int tail_split = -1;
-  bool tail_split_on() const { return tail_split >= 0 ? tail_split != 0 : sym_NC <= 64; }
+  bool tail_split_on() const { return tail_split >= 0 ? tail_split != 0 : sym_NC <= 32; }
   // Phase timing of eager steps (timed): one event set per step, summed by phase_stats.
   struct PhaseEv {
     hipEvent_t t0, end, g0, g1, w0, w1, x0, x1, j0, j1;
