@@ -39,8 +39,19 @@ the last timed step, the relative drift of total momentum over the run, the drif
 energy (kinetic + exact-cutoff potential) and angular momentum (two O(N^2) passes), a few
 steps with phase events for the comm split (multi-rank: replayed from the same segmented plan
 as the timed loop), and the reference's exact hard-cutoff select timed on its own
-(exact_cutoff_ms_per_step). Multi-rank runs record per rank the device it bound and the RCCL
-transports its connections used (parsed from RCCL's INFO log, sent to a file).
+(exact_cutoff_ms_per_step). Multi-rank runs record per rank the device it bound, what RCCL formed
+(ncclCommCount / UserRank / CuDevice) and the RCCL transports its connections used (parsed from
+RCCL's INFO log, sent to a file), and refuse to report a number (error line, exit 70) when two
+ranks share a GPU, the communicator is not the job, or a single-node connection runs through a
+network transport (parallel/verify.py; recorded but not enforced in the one-GPU rehearsal,
+GRAVSIM_RCCL_RANK_HOSTS=1). After the timed run they also check P-independence: rank 0 recomputes
+2 steps from the same ICs as a 1-rank engine on its own GPU and every rank's rows must be bitwise
+equal (--p-audit).
+
+Clock-normalised cost: every force workgroup of the timed steps records its s_memtime (shader
+clock) and s_memrealtime (100 MHz) spans; the line reports engine_clock_ghz and
+cycles_per_pair_eval (step wall x clock x CUs / pair evaluations), so a slow box and a slow kernel
+no longer look alike (profiles/r6_clock_normalised_boxes.txt).
 
 Bounded and self-reporting (gravsim/parallel/guard.py): every stage (gloo init, device,
 engine, RCCL init + warm-up, first step, overlap check, warmup, timed, audits, ...) has a

@@ -41,6 +41,8 @@ def topology_problems(world: int, ranks: list[dict]) -> list[str]:
         out.append(f"{len(ranks)} rank record(s) for a world of {world}")
     for r in sorted(ranks, key=lambda x: x.get("rank", -1)):
         q = r.get("rank")
+        if r.get("rccl_nranks") is None:  # (a library that cannot report it: nothing to check)
+            continue
         if r.get("rccl_nranks") != world:
             out.append(f"rank {q}: RCCL communicator has {r.get('rccl_nranks')} rank(s), the job "
                        f"{world}")

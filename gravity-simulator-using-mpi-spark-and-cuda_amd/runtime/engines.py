@@ -99,6 +99,8 @@ class HipEngine:
     def comm_info(self) -> dict:
         """What RCCL formed for this rank (ncclCommCount / UserRank / CuDevice, checked
         natively at comm_init): rccl_nranks 0 when no communicator is kept (one rank)."""
+        if not hasattr(self.lib, "gs_stepper_comm_info"):  # (round-5 builds for A/B runs)
+            return {"rccl_nranks": None, "rccl_rank": None, "rccl_device": None}
         c, r, d = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
         _native.check(self.lib, self.lib.gs_stepper_comm_info(
             self._s, ctypes.byref(c), ctypes.byref(r), ctypes.byref(d)), "comm info")

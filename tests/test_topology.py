@@ -93,3 +93,10 @@ def test_unparsed_logs_are_reported_not_guessed(tmp_path):
                    over={0: {"transports": None}, 1: {"transports": None}})
     assert verify.topology_problems(2, ranks) == []
     assert verify.transport_summary(ranks)["parsed_ranks"] == 0
+
+
+def test_unknown_communicator_fields_are_not_guessed(tmp_path):
+    """A library that cannot report what RCCL formed (None) is not a failure by itself."""
+    ranks = _ranks(tmp_path, 2, P2P_LOG, over={0: {"rccl_nranks": None, "rccl_rank": None,
+                                                   "rccl_device": None}})
+    assert verify.topology_problems(2, ranks) == []
