@@ -128,6 +128,10 @@ int main(int argc, char** argv) {
     char id[128];
     share_unique_id(a, id);
     if (gs_stepper_comm_init(s, id, a.cfg.rank, a.cfg.nranks)) die("comm_init");
+    int32_t cnt = 0, ur = -1, dev = -1;  // (comm_init has checked them against the layout)
+    gs_stepper_comm_info(s, &cnt, &ur, &dev);
+    fprintf(stderr, "gravsim_bench: rank %d: RCCL communicator of %d ranks, rank %d on device %d\n",
+            a.cfg.rank, cnt, ur, dev);
   }
   if (gs_stepper_init_ics(s, a.ic, a.seed)) die("init_ics");
   gs_layout L;
@@ -151,6 +155,8 @@ int main(int argc, char** argv) {
               stamp, a.cfg.nranks, (long long)a.cfg.n, a.steps, a.cfg.dt);
   }
 
+  double clk[4];
+  gs_stepper_clock(s, clk);  // (reset: the engine-clock record covers the timed loop only)
   const auto t0 = std::chrono::steady_clock::now();
   for (int done = 0; done < a.steps;) {
     if (root && a.progress_every > 0 && done % a.progress_every == 0)
@@ -163,6 +169,7 @@ int main(int argc, char** argv) {
   if (gs_stepper_sync(s)) die("sync");
   const double wall =
       std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  if (gs_stepper_clock(s, clk)) die("clock");  // {GHz, workgroup cycles, wg-seconds, wgs}
   const int64_t bad = gs_stepper_count_nonfinite(s);
 
   std::vector<double> pos((size_t)a.cfg.n * 3);
@@ -188,11 +195,12 @@ int main(int argc, char** argv) {
     const double n = (double)a.cfg.n;
     printf("{\"n\": %lld, \"steps\": %d, \"nranks\": %d, \"dtype\": \"%s\", \"wall_s\": %.6f, "
            "\"ms_per_step\": %.4f, \"body_updates_per_s\": %.6e, \"interactions_per_s\": %.6e, "
-           "\"kernel\": %d, \"mode\": %d, \"ipl\": %d, \"chunk\": %d, \"nonfinite\": %lld}\n",
+           "\"kernel\": %d, \"mode\": %d, \"ipl\": %d, \"chunk\": %d, \"nonfinite\": %lld, "
+           "\"engine_clock_ghz\": %.4f}\n",
            (long long)a.cfg.n, a.steps, a.cfg.nranks, a.cfg.dtype == GS_FP64 ? "fp64" : "fp32",
            wall, a.steps ? 1e3 * wall / a.steps : 0.0, a.steps ? n * a.steps / wall : 0.0,
            a.steps ? n * n * a.steps / wall : 0.0, L.kernel, L.mode, L.ipl, L.chunk,
-           (long long)bad);
+           (long long)bad, clk[0]);
   }
   gs_stepper_destroy(s);
   return bad ? 3 : 0;

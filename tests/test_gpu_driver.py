@@ -111,3 +111,27 @@ def test_gpu_leapfrog_matches_oracle_kdk(hip, mode):
     x, v, _ = oracle.simulate(b0.pos, b0.vel, b0.mass, cfg.dt, 10, integrator="leapfrog")
     assert np.abs(got.pos - x).max() / np.abs(x).max() < 1e-12
     assert np.abs(got.vel - v).max() / np.abs(v).max() < 1e-10
+
+
+def test_native_driver_matches_python_cli_dump(hip, tmp_path, capsys):
+    """gravsim_bench (the C++ driver, no Python) runs the same Stepper: its final-position
+    dump equals the Python CLI's for the same N / steps / seed, its metrics line reports the
+    engine clock of the sym force launches, and no body goes non-finite."""
+    import subprocess
+
+    from gravsim.ops import _native
+
+    exe = _native.NATIVE_DIR / "gravsim_bench"
+    assert exe.exists(), "gravsim_bench not built (csrc/build.py)"
+    seed = 20250307  # (gravsim_bench's default seed)
+    r = subprocess.run([str(exe), "--n", "20000", "--steps", "4", "--dump",
+                        str(tmp_path / "native.txt"), "--progress-every", "0"],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    m = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert m["nonfinite"] == 0 and m["n"] == 20000 and m["steps"] == 4
+    assert 0.5 < m["engine_clock_ghz"] < 3.5, m
+    assert main(["--n", "20000", "--steps", "4", "--device", "gpu", "--seed", str(seed),
+                 "--dump", str(tmp_path / "py.txt"), "--log-format", "none", "--quiet"]) == 0
+    capsys.readouterr()
+    assert (tmp_path / "native.txt").read_text() == (tmp_path / "py.txt").read_text()
