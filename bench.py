@@ -197,7 +197,13 @@ def p_independence_audit(eng, cfg, dist, comm, dev: int, steps: int = 2) -> str:
     recs = comm.allgather_object(dist, mine)
     verdict = ""
     if dist.rank == 0:
-        one = HipEngine(cfg, 0, 1, device=dev)
+        # (the schedule the P-rank engine resolved, so "auto" cannot pick another one for P = 1)
+        import dataclasses
+
+        from gravsim.ops import _native
+
+        one_cfg = dataclasses.replace(cfg, mode=_native.MODE_NAMES[eng.native_layout["mode"]])
+        one = HipEngine(one_cfg, 0, 1, device=dev)
         try:
             one.init_ics("solar+random", cfg.seed)
             one.step(steps)
@@ -290,6 +296,24 @@ def overlap_self_check(eng, cfg, dist, comm, steps: int = 2):
                                         lambda: eng.init_ics("solar+random", cfg.seed),
                                         steps=steps, race=race)
     return mode, verdict
+
+
+def clock_summary(ghz_sum: float, ghz_min: float, ghz_max: float, wg_cycles: float,
+                  wall: float, cus: float, pair_evals: float, world: int) -> dict:
+    """Clock-normalised cost of the timed steps (a slow box and a slow kernel look
+    alike in ms): the engine clock the force launches ran at (per workgroup s_memtime span /
+    s_memrealtime span, duration-weighted; mean over ranks), the CU-cycles per pair evaluation
+    of the whole step at that clock, and the force kernels' own workgroup-cycles per pair (no
+    clock in it at all). None where the schedule keeps no clock record (one-sided kernels)."""
+    ghz = ghz_sum / world if ghz_sum > 0 else None
+    return {"engine_clock_ghz": ghz,
+            "engine_clock_ghz_ranks": [ghz_min, ghz_max] if world > 1 and ghz else None,
+            "cycles_per_pair_eval": wall * ghz * 1e9 * cus / pair_evals if ghz else None,
+            "force_wg_cycles_per_pair_eval": wg_cycles / pair_evals if wg_cycles else None,
+            "cus": int(cus),
+            "method": "per workgroup: s_memtime span / s_memrealtime span x 100 MHz, "
+                      "duration-weighted over the timed steps' force launches; "
+                      "cycles_per_pair_eval = step wall x clock x CUs / pair evals"}
 
 
 def launch_info() -> dict:
@@ -644,21 +668,8 @@ def run(a, g) -> int:
             pairs = float(cfg.n) * cfg.n  # one-sided: every ordered pair evaluated
         parallelism = (f"body-decomposition x{world} (RCCL {exch})" if world > 1
                        else "single GPU")
-        # Clock-normalised cost (a slow box and a slow kernel look alike in ms):
-        # the engine clock the force launches ran at (s_memtime / s_memrealtime per
-        # workgroup, mean over ranks), CU-cycles per pair evaluation of the whole step at that
-        # clock, and the force kernels' own workgroup-cycles per pair (no clock in it at all).
-        ghz = ghz_sum / world if ghz_sum > 0 else None
-        step_pairs = pairs * a.steps
-        clock = {"engine_clock_ghz": ghz,
-                 "engine_clock_ghz_ranks": [ghz_min, ghz_max] if world > 1 else None,
-                 "cycles_per_pair_eval": (wall * ghz * 1e9 * cus_total / step_pairs)
-                 if ghz else None,
-                 "force_wg_cycles_per_pair_eval": wg_cycles / step_pairs if wg_cycles else None,
-                 "cus": int(cus_total),
-                 "method": "per workgroup: s_memtime span / s_memrealtime span x 100 MHz, "
-                           "duration-weighted over the timed steps' force launches; "
-                           "cycles_per_pair_eval = step wall x clock x CUs / pair evals"}
+        clock = clock_summary(ghz_sum, ghz_min, ghz_max, wg_cycles, wall, cus_total,
+                              pairs * a.steps, world)
         out = {
             "metric": METRIC,
             "value": value,

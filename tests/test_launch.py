@@ -87,3 +87,22 @@ def test_bench_self_launches_two_ranks():
     assert [x["stage"] for x in e["config"]["ranks"]] == ["device", "device"]
     assert "bench.py needs a HIP device" in e["error"]
     assert "--gpus 2 but" not in r.stderr  # the children saw WORLD_SIZE == --gpus
+
+
+def test_bench_clock_summary_normalises_boxes():
+    """bench.py's clock-normalised cost: two boxes 6 % apart in ms/step (round 6, 1M on one
+    GPU: 170.26 ms at 2.0934 GHz, 160.26 ms at 2.2256 GHz) give the same CU-cycles per pair;
+    a schedule without a clock record reports None rather than 0."""
+    import bench
+
+    pairs = 1048576 * 1048575 / 2 * 10
+    a = bench.clock_summary(2.0934, 2.0934, 2.0934, 0.0, 1.7026, 256, pairs, 1)
+    b = bench.clock_summary(2.2256, 2.2256, 2.2256, 0.0, 1.6026, 256, pairs, 1)
+    assert abs(a["cycles_per_pair_eval"] - 0.1660) < 5e-4
+    assert abs(a["cycles_per_pair_eval"] / b["cycles_per_pair_eval"] - 1) < 2e-3
+    assert a["engine_clock_ghz_ranks"] is None and a["force_wg_cycles_per_pair_eval"] is None
+    m = bench.clock_summary(2 * 2.1, 2.0, 2.2, 3.3e11, 1.0, 512, pairs, 2)
+    assert m["engine_clock_ghz"] == 2.1 and m["engine_clock_ghz_ranks"] == [2.0, 2.2]
+    assert m["force_wg_cycles_per_pair_eval"] == 3.3e11 / pairs
+    none = bench.clock_summary(0.0, 0.0, 0.0, 0.0, 1.0, 256, pairs, 1)
+    assert none["engine_clock_ghz"] is None and none["cycles_per_pair_eval"] is None
