@@ -80,10 +80,12 @@ def main() -> int:
         e.init_ics("solar+random", cfg.seed)
         e.step(2)
         e.sync()
+        e.clock()  # (reset: the engine-clock record of the timed steps only)
         t0 = time.perf_counter()
         e.step(a.steps)
         e.sync()
         ms = 1e3 * (time.perf_counter() - t0) / a.steps
+        ghz = e.clock()["ghz"] or None
         phase = None
         if P > 1:
             if e.graph_info()["mode"] == "segmented":
@@ -93,14 +95,19 @@ def main() -> int:
             phase = e.phase_stats()
             e.set_timing(False)
         key = (ipl, kernel, strategy, mode, a.dtype)
+        # the step in engine-clock cycles (ms x GHz): a prediction that does not depend on the
+        # clock the box held during each run (DVFS; r6_clock_normalised_boxes.txt)
+        mcyc = ms * ghz if ghz else None
         if P == 1:
-            base[key] = ms
-        b = base.get(key)
+            base[key] = (ms, mcyc)
+        b, bc = base.get(key, (None, None))
         print(json.dumps(dict(P=P, rank=r, n=a.n, dtype=a.dtype, ipl=ipl, kernel=kernel,
                               strategy=strategy, mode=e.native_layout["mode"], comm_gbps=gbps,
                               comm_us=a.comm_us, overlap=ov, graph=gmode, graph_info=e.graph_info(),
-                              ms_per_step=ms,
+                              ms_per_step=ms, engine_clock_ghz=ghz, step_mcycles=mcyc,
                               predicted_efficiency=(b / (P * ms)) if b else None,
+                              predicted_efficiency_cycles=(bc / (P * mcyc)) if bc and mcyc
+                              else None,
                               predicted_body_updates_per_s=a.n / (ms * 1e-3), phase=phase,
                               layout=e.native_layout)), flush=True)
         e.close()
