@@ -1078,9 +1078,8 @@ int gs_stepper_set_timing(gs_stepper* s, int32_t on) {
   // memset on the compute stream, so a comm-side timeout could be erased or an old stall
   // survive into the timed window. A timeout already counted fails here.)
   if (s->sync_stats) {
-    GS_HIP(hipStreamSynchronize(s->s_comm));
-    GS_HIP(hipStreamSynchronize(s->s_comp));
-    if (sync_failed(s)) return -1;
+    // (a bounded wait for every stream: a hung collective fails here instead of blocking)
+    if (wait_until(s, s->prog_rec, s->step_timeout_s)) return -1;
     GS_HIP(hipMemsetAsync(s->sync_stats, 0, 9 * sizeof(unsigned long long), s->s_comp));
     GS_HIP(hipStreamSynchronize(s->s_comp));
   }

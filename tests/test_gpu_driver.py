@@ -131,7 +131,8 @@ def test_native_driver_matches_python_cli_dump(hip, tmp_path, capsys):
     m = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert m["nonfinite"] == 0 and m["n"] == 20000 and m["steps"] == 4
     assert 0.5 < m["engine_clock_ghz"] < 3.5, m
-    assert main(["--n", "20000", "--steps", "4", "--device", "gpu", "--seed", str(seed),
-                 "--dump", str(tmp_path / "py.txt"), "--log-format", "none", "--quiet"]) == 0
+    assert main(["--n", "20000", "--steps", "4", "--device", "gpu", "--dtype", "fp32",
+                 "--seed", str(seed), "--dump", str(tmp_path / "py.txt"), "--log-format", "none",
+                 "--quiet"]) == 0  # (gravsim_bench's defaults: fp32, dt 3600 s, cutoff 1e-10 m)
     capsys.readouterr()
     assert (tmp_path / "native.txt").read_text() == (tmp_path / "py.txt").read_text()
