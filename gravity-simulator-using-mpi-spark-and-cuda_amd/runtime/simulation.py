@@ -260,6 +260,7 @@ class Simulation:
             self.engine.set_timing(True)
         if gpu:
             self.engine.audit_reset()
+            self.engine.clock()  # (reset: the engine-clock record of this run's steps)
         comm.barrier(self.dist)
         t0 = time.perf_counter()
         s = 0
@@ -302,6 +303,10 @@ class Simulation:
                 raise RuntimeError(f"work audit: {int(short)} rank(s) ran the wrong number of "
                                    f"force units (rank {self.dist.rank}: {done} of {per * steps})")
             gi = self.engine.graph_info()
+            # engine clock of the run's force launches (sym schedule; mean over ranks): the
+            # clock-normalised cost next to the wall time (bench.py clock_summary)
+            ghz = comm.allreduce_sum(self.dist, self.engine.clock()["ghz"]) / self.dist.world
+            extra.update(engine_clock_ghz=ghz or None)
             extra.update(work_audit="ok" if per else "n/a (one-sided schedule)",
                          overlap=self.engine.overlap, graph=gi["mode"],
                          graph_segments=gi["segments"] or None,

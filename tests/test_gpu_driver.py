@@ -133,6 +133,9 @@ def test_native_driver_matches_python_cli_dump(hip, tmp_path, capsys):
     assert 0.5 < m["engine_clock_ghz"] < 3.5, m
     assert main(["--n", "20000", "--steps", "4", "--device", "gpu", "--dtype", "fp32",
                  "--seed", str(seed), "--dump", str(tmp_path / "py.txt"), "--log-format", "none",
-                 "--quiet"]) == 0  # (gravsim_bench's defaults: fp32, dt 3600 s, cutoff 1e-10 m)
+                 "--metrics-json", str(tmp_path / "m.json"), "--quiet"]) == 0
+    # (gravsim_bench's defaults: fp32, dt 3600 s, cutoff 1e-10 m)
     capsys.readouterr()
     assert (tmp_path / "native.txt").read_text() == (tmp_path / "py.txt").read_text()
+    pm = json.loads((tmp_path / "m.json").read_text().splitlines()[-1])
+    assert pm["mode"] == "sym" and 0.5 < pm["extra"]["engine_clock_ghz"] < 3.5, pm
