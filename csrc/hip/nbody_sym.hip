@@ -149,40 +149,30 @@ struct Smem {
 
 // Visit the unit's j-tiles. SYM: pairs both ways, j-side partials to Pj (the diagonal chunk
 // runs with SYM = false: every ordered pair once on the i side).
-// A workgroup barrier. The paired kernel counts them: each of its units must pass exactly
-// SymArgs::pair_k of them (force_sym_pair_entry).
-template <bool PAIR>
-__device__ __forceinline__ void bar(int& nb) {
-  __syncthreads();
-  if constexpr (PAIR) ++nb;
-}
-
-// tid: the thread's index within the unit's 4 waves (threadIdx.x, or threadIdx.x & 255 in the
-// paired kernel); nb: the barrier count (PAIR).
-template <typename T, bool SYM, bool EXACT, bool PAIR = false>
+template <typename T, bool SYM, bool EXACT>
 __device__ __forceinline__ void run_tiles(const SymArgs& a, ISetK<T>& is, TileSeq<T> seq,
-                                          int br, Smem<T>& sm, int tid, int& nb) {
+                                          int br, Smem<T>& sm) {
   using G = Geo<T>;
   using V4 = sym::Vec4<T>;
   constexpr int J = G::J;
-  const int w = tid >> 6, lane = tid & 63;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const V4* X4 = static_cast<const V4*>(a.X);
   const T eps2 = (T)a.eps2, cut2 = (T)a.cut2;
   int buf = 0, cur = 0;
-  const bool stager = tid < StageQ<T>::kThreads;
+  const bool stager = threadIdx.x < StageQ<T>::kThreads;
   if (!seq.done() && stager) {
     StageQ<T> sq;
-    sq.load(X4, seq.row0(), tid);
-    sq.store(sm.jt[0], tid);
+    sq.load(X4, seq.row0(), threadIdx.x);
+    sq.store(sm.jt[0], threadIdx.x);
   }
-  bar<PAIR>(nb);
+  __syncthreads();
   while (!seq.done()) {
     TileSeq<T> nx = seq;
     nx.next();
     const int d = seq.d(), t = seq.t();
     StageQ<T> q_next;
     const bool stage_next = !nx.done() && stager;
-    if (stage_next) q_next.load(X4, nx.row0(), tid);  // lands during the arithmetic
+    if (stage_next) q_next.load(X4, nx.row0(), threadIdx.x);  // lands during the arithmetic
     T cx[J], cy[J], cz[J];
     sym::CSetT<T, J> cs;
 #pragma unroll
@@ -203,12 +193,12 @@ __device__ __forceinline__ void run_tiles(const SymArgs& a, ISetK<T>& is, TileSe
       }
     }
     // jt[cur ^ 1] was last read in the previous tile, before the previous barrier.
-    if (stage_next) q_next.store(sm.jt[cur ^ 1], tid);
-    bar<PAIR>(nb);
+    if (stage_next) q_next.store(sm.jt[cur ^ 1], threadIdx.x);
+    __syncthreads();
     if constexpr (SYM) {
       // Sum the waves' carriers in wave order (fixed) and store the tile's j-side partial.
       T* pj = static_cast<T*>(a.Pj) + ((int64_t)br * a.H + (d - 1)) * 3 * kSymC;
-      for (int v = tid; v < 3 * G::kTileJ; v += G::kThreads) {
+      for (int v = threadIdx.x; v < 3 * G::kTileJ; v += G::kThreads) {
         const int c = v / G::kTileJ, b = v % G::kTileJ;
         T acc = sm.slot[buf][0][c][b];
 #pragma unroll
@@ -285,12 +275,12 @@ __device__ __forceinline__ void audit_unit(const SymArgs& a, unsigned long long 
 
 // One unit b (row a, segment s) per call; s == S is the row's diagonal chunk. b is the
 // workgroup index, or the index the workgroup fetched (SymArgs.work).
-template <typename T, bool EXACT, bool PAIR>
-__device__ __forceinline__ unsigned force_sym_body(const SymArgs& a, int b, Smem<T>& sm, int tid,
-                                                   int& nb) {
+template <typename T, bool EXACT>
+__device__ __forceinline__ unsigned force_sym_body(const SymArgs& a, int b) {
   using G = Geo<T>;
   using V4 = sym::Vec4<T>;
-  const int w = tid >> 6, lane = tid & 63;
+  __shared__ Smem<T> sm;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   // Units per row: S shell segments, then D parts of the diagonal chunk.
   // br: row within the band (index into Pi/Pj/Pd); the rank's row is band0 + br.
   // part: -1 a whole unit, 0 .. Np-1 one part of a split segment (part 0 -> Pi, others -> Px).
@@ -375,7 +365,7 @@ __device__ __forceinline__ unsigned force_sym_body(const SymArgs& a, int b, Smem
   if (diag) {
     // Part of the 2048-body diagonal chunk, one-sided (self term 0 through the core, or
     // through the cutoff select in the exact path).
-    run_tiles<T, false, EXACT, PAIR>(a, is, seq, br, sm, tid, nb);
+    run_tiles<T, false, EXACT>(a, is, seq, br, sm);
     store_i(static_cast<T*>(a.Pd) + ((int64_t)br * a.D + (s - a.S)) * 3 * kSymC);
   } else {
     // One piece (the segment), or for a split segment its Np parts: part p covers the tiles
@@ -401,13 +391,13 @@ __device__ __forceinline__ unsigned force_sym_body(const SymArgs& a, int b, Smem
         for (int i = 0; i < G::I; ++i)
           is.ax[i] = is.ay[i] = is.az[i] = std::remove_reference_t<decltype(is.ax[i])>(0);
       }
-      run_tiles<T, true, EXACT, PAIR>(a, is, sq, br, sm, tid, nb);
+      run_tiles<T, true, EXACT>(a, is, sq, br, sm);
       store_i(pc == 0 ? pi : px + (int64_t)(pc - 1) * 3 * kSymC);
-      if (pc + 1 < pc1) bar<PAIR>(nb);  // the next piece restages the LDS tiles and slots
+      if (pc + 1 < pc1) __syncthreads();  // the next piece restages the LDS tiles and slots
 
     }
   }
-  if (a.utrace && tid == 0) {
+  if (a.utrace && threadIdx.x == 0) {
     // hwreg(HW_ID) whole register, hwreg(XCC_ID) bits 3:0 (ids 4 and 20 on gfx9.4+)
     const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);
     const unsigned xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20);
@@ -419,14 +409,6 @@ __device__ __forceinline__ unsigned force_sym_body(const SymArgs& a, int b, Smem
     e[3] = ((unsigned long long)(unsigned)br << 32) | (unsigned)s;
   }
   return a.audit ? (unsigned)weight : 0u;
-}
-
-// The one-unit-per-workgroup form (every kernel but the paired one): its own LDS tiles.
-template <typename T, bool EXACT>
-__device__ __forceinline__ unsigned force_sym_body(const SymArgs& a, int b) {
-  __shared__ Smem<T> sm;
-  int nb = 0;
-  return force_sym_body<T, EXACT, false>(a, b, sm, (int)threadIdx.x, nb);
 }
 
 // units 7 runs a separate instantiation (DEFER): a small grid that walks the deferred list
@@ -553,67 +535,6 @@ __device__ __forceinline__ void force_sym_entry(SymArgs a) {
     if (done) audit_unit(a, done);
   }
   ClockSpan::end();
-}
-
-// Paired units (SymArgs::pair_k > 0: one rank, units 0, dynamic fetch). Two 4-wave
-// workgroups on a CU are issued oldest-first: at 65K the younger one's units ran up to 3x
-// longer (p90 184 against a median of 57 us), and persistent workgroups left the starved one
-// starved to the end of the launch, so small N kept workgroup turnover, at 5-27 us per exit
-// (docs/DESIGN.md §12). Here ONE 8-wave workgroup per CU runs two units at a time, waves 0-3
-// one and waves 4-7 the other, each with its own LDS tiles and carrier slots. The halves
-// share every s_barrier (one per tile), so neither runs more than a tile ahead of the other,
-// and the workgroup stays resident (no turnover). Every unit is padded to exactly pair_k
-// barriers (1 + its most tiles), so the halves meet at every unit boundary, see each other's
-// next unit there, and leave together once both are dry. Same units into the same slots:
-// same bits as every other form.
-template <typename T, bool EXACT>
-__device__ __forceinline__ void force_sym_pair_entry(SymArgs a) {
-  __shared__ Smem<T> sm2[2];
-  __shared__ unsigned next2[2];
-  const int half = (int)(threadIdx.x >> 8), tid = (int)(threadIdx.x & 255);
-  const unsigned n = (unsigned)a.n_units, base = (unsigned)a.first_wave;
-  ClockSpan::begin(a);
-  // the first wave: slot 2 blockIdx.x + half takes that unit without a fetch (the grid is
-  // first_wave / 2 workgroups); later fetches return first_wave + the counter's next value
-  unsigned u = 2u * blockIdx.x + (unsigned)half;
-  unsigned done = 0;  // audit weight of this half's units
-  for (;;) {
-    if (tid == 0) next2[half] = u;
-    __syncthreads();
-    const bool any = next2[0] < n || next2[1] < n;
-    __syncthreads();  // (both halves have read next2 before it is rewritten)
-    if (!any) break;  // both dry: both halves leave after the same barrier
-    // the next unit's index is taken when this one starts (its latency hides behind the
-    // unit), except among the queue's last first_wave units, where a unit held back behind
-    // a running one would lengthen the launch tail
-    const bool early = u < n && u + base < n;
-    unsigned nx = ~0u;
-    if (tid == 0 && early)
-      nx = base + __hip_atomic_fetch_add(a.work, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    int nb = 0;
-    if (u < n) done += force_sym_body<T, EXACT, true>(a, (int)u, sm2[half], tid, nb);
-    for (; nb < a.pair_k; ++nb) __syncthreads();  // pad: every unit passes pair_k barriers
-    if (tid == 0)
-      next2[half] = early ? nx
-                  : u < n ? base + __hip_atomic_fetch_add(a.work, 1u, __ATOMIC_RELAXED,
-                                                          __HIP_MEMORY_SCOPE_AGENT)
-                          : ~0u;
-    __syncthreads();
-    u = next2[half];
-  }
-  if (done && tid == 0 && a.audit)
-    __hip_atomic_fetch_add(a.audit, (unsigned long long)done, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-  ClockSpan::end();
-}
-
-template <bool EXACT>
-__global__ __launch_bounds__(2 * Geo<float>::kThreads) void force_sym_pair_kernel_f32(SymArgs a) {
-  force_sym_pair_entry<float, EXACT>(a);
-}
-template <bool EXACT>
-__global__ __launch_bounds__(2 * Geo<double>::kThreads) void force_sym_pair_kernel_f64(SymArgs a) {
-  force_sym_pair_entry<double, EXACT>(a);
 }
 
 // (separate instantiations: the static kernels keep their own register allocation)
@@ -1165,23 +1086,6 @@ hipError_t launch_force_sym_t(const SymArgs& a, hipStream_t s) {
     b.work = nullptr;  // static: unit = blockIdx.x
     b.persist = 0;
   }
-  if (a.pair_k != 0 && a.units == 0 && b.work && a.first_wave >= 2 && a.first_wave % 2 == 0) {
-    // paired units: pair_k = 1 + the most tiles a unit visits (a shell segment, a diagonal part)
-    using G = Geo<T>;
-    const int seg = a.L * G::kTilesPerQuantum, dg = G::kTilesPerChunk / a.D;
-    b.pair_k = 1 + (seg > dg ? seg : dg);
-    b.persist = 1;
-    const dim3 pgrid((unsigned)(a.first_wave / 2)), pblock(2 * G::kThreads);
-    if constexpr (sizeof(T) == 8) {
-      if (a.exact) hipLaunchKernelGGL((force_sym_pair_kernel_f64<true>), pgrid, pblock, 0, s, b);
-      else hipLaunchKernelGGL((force_sym_pair_kernel_f64<false>), pgrid, pblock, 0, s, b);
-    } else {
-      if (a.exact) hipLaunchKernelGGL((force_sym_pair_kernel_f32<true>), pgrid, pblock, 0, s, b);
-      else hipLaunchKernelGGL((force_sym_pair_kernel_f32<false>), pgrid, pblock, 0, s, b);
-    }
-    return hipGetLastError();
-  }
-  b.pair_k = 0;
   const dim3 grid(g), block(Geo<T>::kThreads);
   const bool d = a.units == 7, y = b.work != nullptr;
   // the first-wave / early-fetch form of the dynamic loop up to 128 units per resident slot

@@ -186,8 +186,6 @@ gs::SymArgs sym_args(gs_stepper* s, int cur) {
     a.unit_cap = s->dyn_cap;
     a.first_wave = s->sym_first_wave;
     a.persist = s->cfg.nranks == 1 && !xcomm(s) && s->sym_persist ? 1 : 0;
-    const bool pair = s->sym_pair > 0 || (s->sym_pair < 0 && false);
-    a.pair_k = s->cfg.nranks == 1 && !xcomm(s) && !s->virt && pair ? 1 : 0;
   }
   a.trace_defer0 = (int32_t)s->utrace_main;
   a.audit = s->audit;
@@ -764,7 +762,6 @@ int gs_stepper_create(const gs_config* cfg, gs_stepper** out) {
   if (s->esz == 8) s->dyn_cap = 4;  // fp64: 512K 101.9-102.0 ms at 4 vs 102.0-102.5 at 2
   if (const char* v = getenv("GRAVSIM_FAULT_SKIP_UNITS")) s->fault_skip = (unsigned)atoi(v);
   if (const char* v = getenv("GRAVSIM_TAIL_SPLIT")) s->tail_split = atoi(v);
-  if (const char* v = getenv("GRAVSIM_SYM_PAIR")) s->sym_pair = atoi(v);
   // GRAVSIM_SYNC=events: the multi-rank step orders its streams by hipEvents (and replays a
   // segmented plan) instead of device counters (flag sync, one graph per period)
   if (const char* v = getenv("GRAVSIM_SYNC")) s->sync_events = strcmp(v, "events") == 0;

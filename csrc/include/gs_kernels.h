@@ -146,10 +146,6 @@ struct SymArgs {
   // (bench.py engine_clock_ghz / cycles_per_pair_eval). Diagnostic only: no output value
   // depends on it.
   unsigned long long* clk;
-  // Paired units (one rank, units 0, dynamic fetch; != 0 requests it): one 8-wave workgroup
-  // per CU runs two units at once, sharing every barrier (nbody_sym.hip force_sym_pair_entry).
-  // The launcher overwrites it with the barriers every unit is padded to.
-  int32_t pair_k;
 };
 
 hipError_t launch_force_sym(const SymArgs& a, hipStream_t s);

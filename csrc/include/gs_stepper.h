@@ -141,9 +141,6 @@ struct gs_stepper {
   int dyn_cap = 3;
   int sym_first_wave = 0;
   bool sym_persist = true;  // one-rank dynamic launches: persistent workgroups (SymArgs::persist)
-  // one-rank dynamic launches as paired units (SymArgs::pair_k): -1 by size, 0 off, 1 on
-  // (GRAVSIM_SYM_PAIR; same bits either way)
-  int sym_pair = -1;
   int64_t utrace_main = 0;               // entries of the main launch (deferred ones follow)
   size_t emu_cap = 0;
   double clk_khz = 100000.0;  // device wall clock (wall_clock64) rate

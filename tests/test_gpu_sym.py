@@ -317,36 +317,6 @@ def test_sym_persistent_workgroups_bitwise(hip, n, dtype, first_wave):
     assert np.array_equal(out[0][1].vel, out[1][1].vel)
 
 
-@pytest.mark.parametrize("n,dtype,first_wave", [(65536, "fp32", 0), (20000, "fp32", 16),
-                                                (262144, "fp32", 0), (40000, "fp64", 0)])
-def test_sym_paired_units_bitwise(hip, monkeypatch, n, dtype, first_wave):
-    """One rank: paired units (GRAVSIM_SYM_PAIR=1: one 8-wave workgroup per CU runs two units
-    at a time sharing every barrier, each unit padded to the same barrier count) run the same
-    units into the same slots as the default launch: same bits, every unit counted once,
-    eager and replayed."""
-    from gravsim.runtime.engines import HipEngine
-
-    out = []
-    for pair in ("0", "1"):
-        monkeypatch.setenv("GRAVSIM_SYM_PAIR", pair)
-        e = HipEngine(SimConfig(n=n, dtype=dtype, device="gpu", mode="sym"))
-        if first_wave:
-            e.set_tuning(first_wave=first_wave)
-        e.init_ics("solar+random", 31)
-        a = e.accel(step_path=True)
-        e.audit_reset()
-        e.step(5)
-        e.sync()
-        done, per = e.audit()
-        assert done == 5 * per and per > 0, (pair, done, per)
-        out.append((a, e.state()))
-        e.close()
-    monkeypatch.delenv("GRAVSIM_SYM_PAIR")
-    assert np.array_equal(out[0][0], out[1][0])
-    assert np.array_equal(out[0][1].pos, out[1][1].pos)
-    assert np.array_equal(out[0][1].vel, out[1][1].vel)
-
-
 @pytest.mark.parametrize("fused", ["0", "1"])
 def test_sym_graph_replays_rezero_unit_counter(hip, monkeypatch, fused):
     """A fresh engine whose first steps are hipGraph replays (no eager step or accel query
