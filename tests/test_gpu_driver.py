@@ -139,3 +139,30 @@ def test_native_driver_matches_python_cli_dump(hip, tmp_path, capsys):
     assert (tmp_path / "native.txt").read_text() == (tmp_path / "py.txt").read_text()
     pm = json.loads((tmp_path / "m.json").read_text().splitlines()[-1])
     assert pm["mode"] == "sym" and 0.5 < pm["extra"]["engine_clock_ghz"] < 3.5, pm
+
+
+def test_bench_json_contract(hip, tmp_path):
+    """bench.py's one JSON line (the driver's contract) on a short run: metric / config of
+    BASELINE.json, the audits, the kernel label from the compiled tile and the clock-normalised
+    cost (engine clock within MI355X's range, CU-cycles per pair in the 0.1-0.4 band of the
+    sym tile)."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "bench.py", "--n", "65536", "--steps", "20", "--warmup",
+                        "4", "--exact-steps", "2", "--phase-steps", "2"], cwd=root,
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    d = json.loads(lines[0])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+              "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config"):
+        assert k in d, k
+    assert d["n_gpus"] == 1 and d["steps"] == 20 and d["warmup"] == 4 and d["dtype"] == "fp32"
+    assert d["status"] == "ok" and d["work_audit"] == "ok", d.get("work_audit")
+    assert d["audit"]["replay"] == "bitwise"
+    assert "8 i x 2 j per lane" in d["config"]["kernel"]
+    assert 0.5 < d["engine_clock_ghz"] < 3.5 and 0.1 < d["cycles_per_pair_eval"] < 0.4, d
+    assert abs(d["value"] - 65536 * 1e3 / d["ms_per_step"]) < 1e-6 * d["value"]
