@@ -233,6 +233,18 @@ class RunGuard:
                 out.append(rec)
         return out
 
+    def _await_peers(self) -> None:
+        """Before rank 0 reports: give peers that have not ended in failed / timeout up to
+        PEER_GRACE_S to get there, so a failure every rank meets (no GPU, a bad device) shows
+        every rank's own error rather than whichever stage the slower ranks were entering."""
+        t_end = time.monotonic() + PEER_GRACE_S
+        while time.monotonic() < t_end:
+            done = {r["rank"] for r in self._peer_records()
+                    if r.get("status") in ("failed", "timeout") and "rank" in r}
+            if len(done) >= self.world - 1:
+                return
+            time.sleep(0.1)
+
     def _fire(self, reason: str) -> None:
         with self._lock:
             if self._fired or self._closed:
@@ -246,6 +258,7 @@ class RunGuard:
                 self.rec["probe_error"] = repr(e)
         self._write()
         if self.rank == 0:
+            self._await_peers()
             try:
                 line = json.dumps(self.report(reason, self.records()), default=str)
             except Exception as e:  # noqa: BLE001
@@ -280,6 +293,9 @@ class RunGuard:
 # A peer record whose guard started this long before rank 0's belongs to an earlier job (the
 # ranks of one job start their guards within seconds of each other).
 STALE_RECORD_S = 120.0
+# How long rank 0 waits, once the run is being stopped, for the other ranks' records to show
+# how they ended (a stalled peer never does: the report then goes out after this).
+PEER_GRACE_S = 2.0
 
 
 def job_id() -> str:

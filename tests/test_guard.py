@@ -55,6 +55,11 @@ SCRIPT = textwrap.dedent("""
                 g.fail(str(e))
         g.stage("wait_for_peer", 60)
         time.sleep(30)
+    elif mode == "both_fail":
+        # every rank meets the same failure, rank 1 a little later (it started slower)
+        g.stage("device", 30)
+        time.sleep(0.8 * rank)
+        g.fail(f"no device on rank {rank}")
     elif mode == "stall_hook":
         g.stage("setup", 0.8)  # GRAVSIM_TEST_STALL sleeps past this budget
         g.close()
@@ -100,6 +105,19 @@ def test_failure_on_another_rank_is_reported_by_rank0(tmp_path):
     assert line["stages"] == ["wait_for_peer", "compute"]
     assert "boom on rank 1" in line["errors"][1]
     assert took < 20, took  # rank 0 did not sit out its 60 s stage
+
+
+def test_report_waits_briefly_for_peers_to_end(tmp_path):
+    """Rank 0 fails first; rank 1 meets the same failure 0.8 s later. The report shows both
+    ranks' own errors (PEER_GRACE_S), not rank 1 still entering its stage."""
+    from gravsim.parallel.guard import EXIT_CODE
+
+    rcs, outs, took = _run("both_fail", world=2, guard_dir=tmp_path)
+    assert rcs == [EXIT_CODE, EXIT_CODE], outs
+    line = json.loads(outs[0][0].strip().splitlines()[-1])
+    assert line["stages"] == ["device", "device"], line
+    assert line["errors"] == ["no device on rank 0", "no device on rank 1"], line
+    assert took < 20, took
 
 
 def test_stall_hook(tmp_path):
