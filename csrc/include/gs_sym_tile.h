@@ -47,7 +47,10 @@
 // splats by op_sel from the (x, y) / (z, mu) pairs as loaded (inline asm: 231 -> 189 VGPRs,
 // the compiler otherwise duplicates each coordinate into a register pair) +0.6 % at 2 waves
 // per SIMD and +1.2 % at 3 (168 VGPRs), same bits (r4s2_opsel_occupancy3_ab.jsonl): more
-// waves per SIMD do not raise this tile's issue rate.
+// waves per SIMD do not raise this tile's issue rate; the carriers rotated by ds_bpermute at
+// the top of each step with the j-side FMA chain starting from them (no v_sub_f32_dpp) keep
+// the same cycles per pair but lower the power-limited engine clock, 2.22 -> 2.17 GHz:
+// +2.2 % at 1M, +1.4 % fp64 (r6_carry_bpermute_rejected_ab.jsonl).
 #pragma once
 #include <hip/hip_runtime.h>
 
