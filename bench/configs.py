@@ -38,11 +38,13 @@ def gpu_run(n, dtype, steps, warmup, P=1, rank=0, overlap=None, **kw):
     e.init_ics("solar+random", cfg.seed)
     e.step(warmup)
     e.sync()
+    e.clock()  # (reset: the engine clock of the timed steps only)
     t0 = time.perf_counter()
     e.step(steps)
     e.sync()
     ms = 1e3 * (time.perf_counter() - t0) / steps
-    lay = e.native_layout
+    ghz = e.clock()["ghz"] or None  # (None: a schedule without clock stamps)
+    lay = dict(e.native_layout, engine_clock_ghz=ghz)
     phase = None
     if P > 1:  # comm split of two more event-timed steps, replayed from the segmented plan
         e.align_period()
@@ -126,15 +128,18 @@ def main() -> int:
         with open(a.md, "w") as f:
             from gravsim.ops._native import MODE_NAMES
 
-            f.write("| config | GPUs | how | schedule | ms/step | body-updates/s | comm ms | "
-                    "exposed comm ms |\n|---|---|---|---|---|---|---|---|\n")
+            f.write("| config | GPUs | how | schedule | ms/step | engine GHz | body-updates/s | "
+                    "comm ms | exposed comm ms |\n|---|---|---|---|---|---|---|---|---|\n")
             for r in rows:
                 mode = MODE_NAMES.get(r.get("layout", {}).get("mode"), "cpu")
                 ph = r.get("phase") or {}
                 c = f"{ph['comm_ms']:.3f}" if ph else "-"
                 x = f"{ph['exposed_comm_ms']:.3f}" if ph else "-"
+                g = (r.get("layout") or {}).get("engine_clock_ghz")
+                g = f"{g:.3f}" if g else "-"
                 f.write(f"| {r['config']} | {r['gpus']} | {r['how']} | {mode} | "
-                        f"{r['ms_per_step']:.3f} | {r['body_updates_per_s']:.4g} | {c} | {x} |\n")
+                        f"{r['ms_per_step']:.3f} | {g} | {r['body_updates_per_s']:.4g} | {c} | "
+                        f"{x} |\n")
     return 0
 
 
