@@ -762,6 +762,11 @@ int gs_stepper_create(const gs_config* cfg, gs_stepper** out) {
   if (s->esz == 8) s->dyn_cap = 4;  // fp64: 512K 101.9-102.0 ms at 4 vs 102.0-102.5 at 2
   if (const char* v = getenv("GRAVSIM_FAULT_SKIP_UNITS")) s->fault_skip = (unsigned)atoi(v);
   if (const char* v = getenv("GRAVSIM_TAIL_SPLIT")) s->tail_split = atoi(v);
+  // Long one-rank graphs only where a launch of graph_steps steps stays far inside the host's
+  // progress bound (one progress event per launch; >= 60 s): up to 2M bodies (fp64 2M on one
+  // GPU: ~1.5 s per step). At 1M and above the launch gap is noise anyway.
+  s->graph_steps = s->L.n_pad <= (int64_t{1} << 21) ? 8 : 2;
+  if (const char* v = getenv("GRAVSIM_GRAPH_STEPS")) s->graph_steps = atoi(v) & ~1;
   // GRAVSIM_SYNC=events: the multi-rank step orders its streams by hipEvents (and replays a
   // segmented plan) instead of device counters (flag sync, one graph per period)
   if (const char* v = getenv("GRAVSIM_SYNC")) s->sync_events = strcmp(v, "events") == 0;
@@ -1037,28 +1042,39 @@ int gs_stepper_step(gs_stepper* s, int32_t nsteps) {
           continue;
         }
         if (run_plan(s)) return -1;
-      } else {
-        if (!s->graph && build_graph(s)) {
-          if (!xcomm(s)) return -1;
-          s->graph_failed = true;  // eager from here on (the error text is kept for inspection)
-          continue;
+      }
+      // one-rank graphs: graph_steps steps per launch while that many are left
+      const int gsteps = !seg && !xcomm(s) && s->graph_steps > 2 && left >= s->graph_steps
+                             ? s->graph_steps : 2;
+      if (!seg) {
+        hipGraphExec_t& gx = gsteps > 2 ? s->graph_long : s->graph;
+        if (!gx) {
+          // both one-rank graphs at the first replay (the warm-up), so a timed loop never
+          // pays a capture
+          const bool both = !xcomm(s) && s->graph_steps > 2;
+          if ((!s->graph && build_graph(s, 2)) ||
+              (both && !s->graph_long && build_graph(s, s->graph_steps))) {
+            if (!xcomm(s)) return -1;
+            s->graph_failed = true;  // eager from here on (the error text is kept)
+            continue;
+          }
         }
         gs_stepper::PhaseEv* pe = s->timed ? phase_begin(s) : nullptr;
         if (pe) {
-          pe->nsteps = 2;
+          pe->nsteps = gsteps;
           GS_HIP(hipEventRecord(pe->t0, s->s_comp));
         }
-        GS_HIP(hipGraphLaunch(s->graph, s->s_comp));
+        GS_HIP(hipGraphLaunch(gx, s->s_comp));
         if (pe) {
           GS_HIP(hipEventRecord(pe->end, s->s_comp));
-          s->pev_plan += 2;
+          s->pev_plan += gsteps;
         }
       }
-      s->k += 2;
+      s->k += gsteps;
       // After one period: X[1] was gathered in the second step, X[0] holds only the own slice.
       s->full[0] = !xcomm(s);
       s->full[1] = true;
-      left -= 2;
+      left -= gsteps;
       if (note_progress(s)) return -1;
       continue;
     }

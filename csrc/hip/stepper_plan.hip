@@ -175,9 +175,11 @@ int comp_wait_comm(gs_stepper* s, hipEvent_t ev, int mark, int id, const unsigne
 }
 
 void drop_graphs(gs_stepper* s) {
-  if (s->graph) {
-    (void)hipGraphExecDestroy(s->graph);
-    s->graph = nullptr;
+  for (hipGraphExec_t* g : {&s->graph, &s->graph_long}) {
+    if (*g) {
+      (void)hipGraphExecDestroy(*g);
+      *g = nullptr;
+    }
   }
   for (auto& op : s->plan)
     if (op.g) (void)hipGraphExecDestroy(op.g);
@@ -186,8 +188,9 @@ void drop_graphs(gs_stepper* s) {
   s->plan_fsync = false;
 }
 
-int build_graph(gs_stepper* s) {
-  // One ping-pong period (two steps) starting from an even step with a gathered buffer.
+int build_graph(gs_stepper* s, int steps) {
+  // `steps` / 2 ping-pong periods (s->graph: one, two steps; s->graph_long: graph_steps)
+  // starting from an even step with a gathered buffer.
   const int64_t k0 = s->k;
   const bool f0 = s->full[0], f1 = s->full[1];
   hipGraph_t g = nullptr;
@@ -199,15 +202,15 @@ int build_graph(gs_stepper* s) {
   // of every bench and CLI run guard it.)
   s->work_zero = true;
   GS_HIP(hipStreamBeginCapture(s->s_comp, hipStreamCaptureModeThreadLocal));
-  int rc = enqueue_step_any(s, true);
-  if (rc == 0) rc = enqueue_step_any(s, true);
+  int rc = 0;
+  for (int i = 0; i < steps && rc == 0; ++i) rc = enqueue_step_any(s, true);
   hipError_t e = hipStreamEndCapture(s->s_comp, &g);
   s->k = k0;
   s->full[0] = f0;
   s->full[1] = f1;
   if (rc) return rc;
   GS_HIP(e);
-  GS_HIP(hipGraphInstantiate(&s->graph, g, nullptr, nullptr, 0));
+  GS_HIP(hipGraphInstantiate(steps > 2 ? &s->graph_long : &s->graph, g, nullptr, nullptr, 0));
   GS_HIP(hipGraphDestroy(g));
   return 0;
 }

@@ -87,6 +87,13 @@ struct gs_stepper {
   // gated on the gather in-kernel (the multi-rank default).
   int sym_overlap = 0;
   hipGraphExec_t graph = nullptr;
+  // One-rank runs also replay a graph of graph_steps steps (graph_steps / 2 ping-pong periods)
+  // whenever that many are left: each graph launch costs an idle gap on the GPU (~14 us at
+  // 65K under the profiler, against 0 between the kernels inside a graph), paid once per
+  // launch instead of once per period. 8 up to 2M bodies, else 2 (stepper.hip create);
+  // GRAVSIM_GRAPH_STEPS overrides (even; <= 2: periods only).
+  hipGraphExec_t graph_long = nullptr;
+  int graph_steps = 2;
   bool timed = false;  // eager steps record phase events
   int own_c0 = 0, own_c1 = 0;  // this rank's chunks clipped to [0, n_chunks)
   bool exact = true;           // hard-cutoff select vs fast core-softened path
@@ -315,7 +322,7 @@ int comm_wait_comp(gs_stepper* s, hipEvent_t ev, int id);
 int comm_signal_comp(gs_stepper* s, hipEvent_t ev, int id);
 int comp_wait_comm(gs_stepper* s, hipEvent_t ev, int mark, int id, const unsigned* flag = nullptr);
 void drop_graphs(gs_stepper* s);
-int build_graph(gs_stepper* s);
+int build_graph(gs_stepper* s, int steps = 2);
 bool plan_ok(const gs_stepper* s);
 int build_plan(gs_stepper* s);
 int run_plan(gs_stepper* s);
