@@ -45,12 +45,18 @@ def main() -> int:
                     help="comma list of multi-rank step modes: eager | segmented (the default: "
                          "compute segments as graphs, collectives eager between them) | full "
                          "(collectives captured too)")
+    ap.add_argument("--links", action="store_true",
+                    help="price the node-sum exchange per xGMI link (GRAVSIM_EMU_LINKS=1: each "
+                         "source peer's bytes at --comm-gbps, peers in parallel) instead of all "
+                         "of a rank's bytes through one --comm-gbps pipe")
     ap.add_argument("--rank", default="-1",
                     help="emulated rank: an index, -1 the last, 'all' every rank")
     ap.add_argument("--repeat", type=int, default=1, help="run the whole grid this many times "
                     "(alternating configurations, for A/B on a noisy clock)")
     a = ap.parse_args()
     os.environ["GRAVSIM_EMULATE_RANK"] = "1"
+    if a.links:
+        os.environ["GRAVSIM_EMU_LINKS"] = "1"
     import torch  # noqa: F401
 
     import gravsim  # noqa: F401
@@ -103,6 +109,7 @@ def main() -> int:
         b, bc = base.get(key, (None, None))
         print(json.dumps(dict(P=P, rank=r, n=a.n, dtype=a.dtype, ipl=ipl, kernel=kernel,
                               strategy=strategy, mode=e.native_layout["mode"], comm_gbps=gbps,
+                              exchange_model="per-link" if a.links else "one pipe",
                               comm_us=a.comm_us, overlap=ov, graph=gmode, graph_info=e.graph_info(),
                               ms_per_step=ms, engine_clock_ghz=ghz, step_mcycles=mcyc,
                               predicted_efficiency=(b / (P * ms)) if b else None,

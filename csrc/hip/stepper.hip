@@ -752,6 +752,7 @@ int gs_stepper_create(const gs_config* cfg, gs_stepper** out) {
   // soon as the gather lands, nothing waits on it (see sym_force).
   s->sym_overlap = cfg->nranks > 1 ? 3 : 0;
   if (const char* ov = getenv("GRAVSIM_SYM_OVERLAP")) s->sym_overlap = atoi(ov);
+  s->emu_links = getenv("GRAVSIM_EMU_LINKS") != nullptr && atoi(getenv("GRAVSIM_EMU_LINKS")) != 0;
   if (const char* v = getenv("GRAVSIM_EMU_COMM")) {
     double us = s->emu_lat_us;
     int wgs = s->emu_wgs;

@@ -16,9 +16,12 @@ namespace gs::rt {
 // by emu_wgs workgroups that stay resident for latency + bytes / rate (comm_model.hip). The
 // kernel copies min(bytes, src_cap, emu_cap) bytes (src_cap: what the source buffer holds);
 // the modeled time always uses the full byte count.
-int comm_model(gs_stepper* s, const void* src, size_t bytes, size_t src_cap) {
+// time_bytes: the bytes that set the modeled duration (default: all of them); the kernel
+// still moves `bytes` (clamped to the buffers).
+int comm_model(gs_stepper* s, const void* src, size_t bytes, size_t src_cap, size_t time_bytes) {
   if (s->emu_gbps <= 0.0 || bytes == 0) return 0;
-  const double us = s->emu_lat_us + (double)bytes / (s->emu_gbps * 1e3);
+  if (time_bytes > bytes) time_bytes = bytes;
+  const double us = s->emu_lat_us + (double)time_bytes / (s->emu_gbps * 1e3);
   if (bytes > s->emu_cap) bytes = s->emu_cap;  // (sized at create for the larger collective)
   if (bytes > src_cap) bytes = src_cap;
   const uint64_t ticks = (uint64_t)(us * s->clk_khz / 1e3);
@@ -219,12 +222,17 @@ int sym_reduce_exchange(gs_stepper* s, const gs::SymArgs& a0, bool* exchanged, b
           // evaluate the same table, so every send still meets its receive).
           if (s->emulate) {
             // the bytes this rank receives in this stage, read from its receive buffer
-            size_t bytes = 0;
+            size_t bytes = 0, peak = 0;
             for (int k = kb; k < ke; ++k) {
               const int src = (r - k + P) % P;
-              if (s->pair_live(src, r)) bytes += (size_t)s->nn[src] * 3 * nl * e;
+              if (!s->pair_live(src, r)) continue;
+              const size_t b = (size_t)s->nn[src] * 3 * nl * e;
+              bytes += b;
+              peak = b > peak ? b : peak;
             }
-            if (comm_model(s, s->sym_R, bytes, (size_t)s->sym_NN * 3 * nl * e)) return -1;
+            if (comm_model(s, s->sym_R, bytes, (size_t)s->sym_NN * 3 * nl * e,
+                           s->emu_links ? peak : bytes))
+              return -1;
           } else {
             const ncclDataType_t dt = s->esz == 8 ? ncclFloat64 : ncclFloat32;
             GS_NCCL(ncclGroupStart());

@@ -135,6 +135,11 @@ struct gs_stepper {
   // and node-sum exchange becomes a comm_model_kernel of the same byte count on s_comm.
   double emu_gbps = 0.0, emu_lat_us = 15.0;
   int emu_wgs = 16;
+  // GRAVSIM_EMU_LINKS=1: price the node-sum exchange per xGMI link (each source peer's bytes
+  // at emu_gbps, the peers of a stage in parallel: the time of the largest) instead of all of
+  // a rank's bytes through one emu_gbps pipe. The all-gather keeps the one-pipe price (a ring
+  // is per-link bound).
+  bool emu_links = false;
   void* emu_buf = nullptr;
   unsigned long long* utrace = nullptr;  // GRAVSIM_UNIT_TRACE: per force workgroup timeline
   // Dynamic unit fetch of the sym force launch (gs_stepper_set_schedule; <= 1: static units):
@@ -330,7 +335,8 @@ int wait_until(gs_stepper* s, int64_t target, double timeout_s);
 int note_progress(gs_stepper* s);
 
 // stepper_comm.hip: the collectives (RCCL, the per-rank emulation's modeled ones).
-int comm_model(gs_stepper* s, const void* src, size_t bytes, size_t src_cap);
+int comm_model(gs_stepper* s, const void* src, size_t bytes, size_t src_cap,
+               size_t time_bytes = SIZE_MAX);
 void rank_slice(const gs_stepper* s, int q, int64_t* b0, int64_t* cnt);
 int gather(gs_stepper* s, int cur, bool gate = false);
 int ring_src(const gs_stepper* s, int sub);

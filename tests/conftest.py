@@ -33,7 +33,7 @@ def hip():
 _PROCESS_KNOBS = ("GRAVSIM_EMULATE_RANK", "GRAVSIM_UNIT_TRACE", "GRAVSIM_EMU_COMM",
                   "GRAVSIM_SYM_BAND_MB", "GRAVSIM_FAULT_SKIP_UNITS", "GRAVSIM_SYM_OVERLAP",
                   "GRAVSIM_FORCE_COMM", "GRAVSIM_TEST_STALL", "GRAVSIM_SYNC",
-                  "GRAVSIM_SYNC_LIMIT_S", "GRAVSIM_TAIL_SPLIT", "GRAVSIM_GRAPH_STEPS",
+                  "GRAVSIM_SYNC_LIMIT_S", "GRAVSIM_TAIL_SPLIT", "GRAVSIM_GRAPH_STEPS", "GRAVSIM_EMU_LINKS",
                   "ROCPROF_COUNTER_COLLECTION")
 
 
