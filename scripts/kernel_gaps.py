@@ -27,12 +27,17 @@ def load(path: str, match: list[str]) -> list[tuple[int, int, str]]:
     return out
 
 
-def main() -> int:
+def main(argv: list[str] | None = None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("csv")
     ap.add_argument("--match", default="force_sym,sym_tail")
-    a = ap.parse_args()
-    ks = load(a.csv, a.match.split(","))
+    a = ap.parse_args(argv)
+    print(summarise(load(a.csv, a.match.split(","))))
+    return 0
+
+
+def summarise(ks: list[tuple[int, int, str]]) -> dict:
+    """Durations and gaps (us) of a force / tail kernel sequence sorted by start time."""
     kinds = ["tail" if "tail" in n else "force" for _, _, n in ks]
     gaps: dict[str, list[float]] = {"force->tail": [], "tail->force": []}
     for i in range(1, len(ks)):
@@ -50,14 +55,13 @@ def main() -> int:
     # gaps inside the step loop (longer ones are host pauses between bench phases)
     allgaps = [g for g in gaps["force->tail"] + tf if g < 100.0]
     steps = max(1, len(ks) // 2)
-    print({"kernels": len(ks), "force_us": med(dur["force"]), "tail_us": med(dur["tail"]),
+    return ({"kernels": len(ks), "force_us": med(dur["force"]), "tail_us": med(dur["tail"]),
            "idle_between_kernels_us_per_step": round(sum(g for g in allgaps if g > 0) / steps, 2),
            "gaps_over_5us": sum(1 for g in allgaps if g > 5.0),
            "gap_force_tail_us": med(gaps["force->tail"]),
            "gap_tail_force_even_us": med(even), "gap_tail_force_odd_us": med(odd),
            "step_us_median": med([(ks[i + 2][0] - ks[i][0]) / 1e3
                                   for i in range(0, len(ks) - 2, 2)])})
-    return 0
 
 
 if __name__ == "__main__":

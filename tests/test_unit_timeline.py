@@ -43,3 +43,26 @@ def test_timeline_diag_units_and_empty_slots():
     assert r["units"] == 2 and r["n_shell"] == 1 and r["n_diag"] == 1
     assert r["diag_ms"] == 0.0005 and r["shell_ms"] == 0.001
     assert analyse(np.zeros((3, 4), dtype=np.uint64), S) == {"units": 0}
+
+
+def test_kernel_gaps_period_and_graph_boundaries(tmp_path):
+    """scripts/kernel_gaps.py on a synthetic kernel trace: force 100 us, tail 10 us, no gap
+    inside a graph, 14 us at every graph launch of two-step periods (r6_kernel_gaps_65k.txt)."""
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "scripts"))
+    import kernel_gaps
+
+    rows, t = [], 0
+    for step in range(8):
+        rows.append((t, t + 100_000, "force_sym_kernel_f32"))
+        rows.append((t + 100_000, t + 110_000, "sym_tail_kernel"))
+        t += 110_000 + (14_000 if step % 2 == 1 else 0)  # (ns) graph launch after odd steps
+    p = tmp_path / "kt_kernel_trace.csv"
+    p.write_text("Kernel_Name,Start_Timestamp,End_Timestamp\n"
+                 + "".join(f"{n},{s},{e}\n" for s, e, n in rows))
+    r = kernel_gaps.summarise(kernel_gaps.load(str(p), ["force_sym", "sym_tail"]))
+    assert r["kernels"] == 16 and r["force_us"] == 100.0 and r["tail_us"] == 10.0
+    assert r["gap_force_tail_us"] == 0.0
+    assert sorted([r["gap_tail_force_even_us"], r["gap_tail_force_odd_us"]]) == [0.0, 14.0]
+    assert r["gaps_over_5us"] == 3  # (7 tail -> force gaps, 3 of them at a graph launch)
+    assert r["idle_between_kernels_us_per_step"] == round(3 * 14.0 / 8, 2)
