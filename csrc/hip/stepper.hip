@@ -764,9 +764,10 @@ int gs_stepper_create(const gs_config* cfg, gs_stepper** out) {
   if (const char* v = getenv("GRAVSIM_FAULT_SKIP_UNITS")) s->fault_skip = (unsigned)atoi(v);
   if (const char* v = getenv("GRAVSIM_TAIL_SPLIT")) s->tail_split = atoi(v);
   // Long one-rank graphs only where a launch of graph_steps steps stays far inside the host's
-  // progress bound (one progress event per launch; >= 60 s): up to 2M bodies (fp64 2M on one
-  // GPU: ~1.5 s per step). At 1M and above the launch gap is noise anyway.
-  s->graph_steps = s->L.n_pad <= (int64_t{1} << 21) ? 8 : 2;
+  // progress bound (one progress event per launch; >= 60 s): 32 steps up to 256K bodies, 8 up
+  // to 2M (fp64 2M on one GPU: ~1.5 s per step). At 1M and above the launch gap is noise.
+  // 32 against 8 steps: 16K -0.8 %, 65K -0.15 %, 256K even (profiles/r6_graph_steps_32_ab.jsonl).
+  s->graph_steps = s->L.n_pad <= (int64_t{1} << 18) ? 32 : s->L.n_pad <= (int64_t{1} << 21) ? 8 : 2;
   if (const char* v = getenv("GRAVSIM_GRAPH_STEPS")) s->graph_steps = atoi(v) & ~1;
   // GRAVSIM_SYNC=events: the multi-rank step orders its streams by hipEvents (and replays a
   // segmented plan) instead of device counters (flag sync, one graph per period)

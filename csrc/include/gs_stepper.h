@@ -90,7 +90,7 @@ struct gs_stepper {
   // One-rank runs also replay a graph of graph_steps steps (graph_steps / 2 ping-pong periods)
   // whenever that many are left: each graph launch costs an idle gap on the GPU (~14 us at
   // 65K under the profiler, against 0 between the kernels inside a graph), paid once per
-  // launch instead of once per period. 8 up to 2M bodies, else 2 (stepper.hip create);
+  // launch instead of once per period. 32 up to 256K bodies, 8 up to 2M, else 2 (create);
   // GRAVSIM_GRAPH_STEPS overrides (even; <= 2: periods only).
   hipGraphExec_t graph_long = nullptr;
   int graph_steps = 2;

@@ -339,13 +339,14 @@ def test_sym_graph_replays_rezero_unit_counter(hip, monkeypatch, fused):
 
 @pytest.mark.parametrize("mode", ["sym", "fused"])
 def test_long_graphs_match_periods_and_eager(hip, monkeypatch, mode):
-    """One-rank replays of graph_steps steps per launch (GRAVSIM_GRAPH_STEPS, default 8) give
-    the bits of two-step periods and of eager steps, including runs that mix them (an odd
-    eager step first, then 8 + 2 steps, then a remainder shorter than a long graph)."""
+    """One-rank replays of graph_steps steps per launch (GRAVSIM_GRAPH_STEPS; default 32 at
+    this size) give the bits of two-step periods and of eager steps, including runs that mix
+    them (an odd eager step first, then long graphs and periods, then a remainder shorter than
+    a long graph)."""
     from gravsim.runtime.engines import HipEngine
 
     out = []
-    for graph, steps in ((False, None), (True, "2"), (True, "8"), (True, "4")):
+    for graph, steps in ((False, None), (True, "2"), (True, "8"), (True, "4"), (True, None)):
         if steps is None:
             monkeypatch.delenv("GRAVSIM_GRAPH_STEPS", raising=False)
         else:
@@ -353,7 +354,7 @@ def test_long_graphs_match_periods_and_eager(hip, monkeypatch, mode):
         e = HipEngine(SimConfig(n=32768, dtype="fp32", device="gpu", mode=mode, graph=graph))
         e.init_ics("solar+random", 5)
         e.step(1)
-        e.step(10)
+        e.step(36)
         e.step(5)
         e.sync()
         out.append(e.state())
