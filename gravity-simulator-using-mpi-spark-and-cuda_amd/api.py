@@ -6,6 +6,7 @@ same names, so code written against it ports by changing the import:
   Particle (pyspark.py:10-29)             -> Particle (dataclass, to_dict / from_dict)
   create_solar_system() (pyspark.py:124-141)
   generate_random_particles(n) (:144-149) -> seeded counter RNG (``seed=``), same ranges
+  calculate_force_between(p1, p2, G) (:32-42) -> the pair force on p1 from p2 (dicts, a list)
   SparkGravitySimulator(particles, dt, cores, memory) (:45-57)
       .calculate_forces() (:59-86)        -> per-body force vectors F_i = m_i a_i (list)
       .update() (:88-102)                 -> one kick-drift step
@@ -46,6 +47,18 @@ class Particle:
     def from_dict(d: dict) -> "Particle":
         return Particle(position=np.array(d["position"], float),
                         velocity=np.array(d["velocity"], float), mass=float(d["mass"]))
+
+
+def calculate_force_between(p1_data: dict, p2_data: dict, G: float = G_SI,
+                            cutoff: float = 1e-10) -> List[float]:
+    """Force on body 1 from body 2 (the dict form of Particle.to_dict), as a 3-list:
+    G m1 m2 (x2 - x1) / r^3, or zeros closer than `cutoff` (pyspark.py:32-42, mpi.c:59-73).
+    A scalar helper for code written against the reference; the engines never call it."""
+    d = np.asarray(p2_data["position"], float) - np.asarray(p1_data["position"], float)
+    r = float(np.sqrt(d @ d))
+    if r < cutoff:
+        return [0.0, 0.0, 0.0]
+    return (G * float(p1_data["mass"]) * float(p2_data["mass"]) / (r * r * r) * d).tolist()
 
 
 def create_solar_system() -> List[Particle]:

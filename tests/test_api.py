@@ -38,3 +38,22 @@ def test_spark_style_run_simulation(capsys):
     assert len(sim.particles_data) == 40
     sim.close()
     assert GravitySimulator is SparkGravitySimulator
+
+
+def test_calculate_force_between_pair_law():
+    """The reference's scalar pair force (pyspark.py:32-42): G m1 m2 / r^2 along r, equal and
+    opposite, zero inside the 1e-10 m cutoff; m1 times the oracle's acceleration of body 1."""
+    from gravsim.api import calculate_force_between
+    from gravsim.config import G_SI
+
+    s = [p.to_dict() for p in create_solar_system()]
+    f = np.array(calculate_force_between(s[1], s[0]))  # Earth pulled toward the Sun
+    r = 1.496e11
+    assert f[1] == 0.0 and f[2] == 0.0 and f[0] < 0
+    assert np.isclose(-f[0], G_SI * 1.989e30 * 5.972e24 / r**2, rtol=1e-15)
+    assert np.allclose(calculate_force_between(s[0], s[1]), -f, rtol=1e-15)
+    pos = np.array([p["position"] for p in s[:2]])
+    acc = oracle.accelerations(pos, np.array([p["mass"] for p in s[:2]]))
+    assert np.allclose(f, s[1]["mass"] * acc[1], rtol=1e-12)
+    near = dict(s[1], position=[1.496e11 + 5e-11, 0.0, 0.0])
+    assert calculate_force_between(s[1], near) == [0.0, 0.0, 0.0]
