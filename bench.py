@@ -700,10 +700,13 @@ def run(a, g) -> int:
                 "select: bit-identical to the 1e-10 m select for separations above ~1 cm; a "
                 "pair closer than the cutoff gets a finite softened force mu r / (r^2 + c^2)^1.5 "
                 "instead of 0; exact_cutoff_ms_per_step times the select)",
-                # eager | graph (one hipGraph per two steps) | segmented (multi-rank: compute
+                # eager | graph (one-rank hipGraphs of graph_steps_per_launch steps, and of two
+                # for a remainder) | segmented (multi-rank: compute
                 # segments as graphs, RCCL collectives eager between them)
                 "graph": ginfo["mode"],
                 "graph_segments": ginfo["segments"] or None,
+                # one-rank replays: steps per graph launch (every step's kernels are in it)
+                "graph_steps_per_launch": ginfo.get("steps_per_launch"),
                 "overlap": overlap,
                 "overlap_check": overlap_check,
                 "overlap_fallback": fallback,

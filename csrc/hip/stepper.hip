@@ -1156,6 +1156,10 @@ int32_t gs_stepper_mem_entry(gs_stepper* s, int32_t i, const char** tag, uint64_
   return (int32_t)s->mem.size();
 }
 
+int gs_stepper_graph_steps(gs_stepper* s) {
+  return s->graph_steps > 2 && s->cfg.nranks == 1 ? s->graph_steps : 2;
+}
+
 int gs_stepper_graph_info(gs_stepper* s, int32_t* mode, int32_t* segments) {
   if (mode) *mode = !s->plan.empty() ? 2 : (s->graph ? 1 : 0);
   if (segments) *segments = s->plan_graphs;

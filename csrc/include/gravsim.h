@@ -232,6 +232,8 @@ int gs_sym_tile_shape(int32_t fp64, int32_t* waves, int32_t* ipl, int32_t* jpl);
 // segmented plan (multi-rank: compute segments as graphs, collectives eager between them);
 // *segments = graph segments per two steps (mode 2).
 int gs_stepper_graph_info(gs_stepper* s, int32_t* mode, int32_t* segments);
+// Steps per replayed one-rank graph launch (GRAVSIM_GRAPH_STEPS; 2 = one ping-pong period).
+int gs_stepper_graph_steps(gs_stepper* s);
 // Device memory ledger: entry i (name, bytes) of the HBM buffers this stepper owns; returns
 // the entry count (i out of range: only the count).
 int32_t gs_stepper_mem_entry(gs_stepper* s, int32_t i, const char** tag, uint64_t* bytes);

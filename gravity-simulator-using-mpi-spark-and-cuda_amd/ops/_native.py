@@ -185,6 +185,7 @@ def hip_lib():
         _sig(lib, "gs_sym_tile_shape", c_int32, [c_int32] + [POINTER(c_int32)] * 3,
              optional=True)
         _sig(lib, "gs_stepper_graph_info", c_int32, [S, POINTER(c_int32), POINTER(c_int32)])
+        _sig(lib, "gs_stepper_graph_steps", c_int32, [S], optional=True)
         _sig(lib, "gs_stepper_mem_entry", c_int32,
              [S, c_int32, POINTER(ctypes.c_char_p), POINTER(c_uint64)])
         _sig(lib, "gs_stepper_set_timeout", c_int32, [S, c_double])

@@ -269,7 +269,10 @@ class HipEngine:
         (multi-rank: compute segments as graphs, collectives eagerly between them)."""
         m, n = ctypes.c_int32(), ctypes.c_int32()
         self.lib.gs_stepper_graph_info(self._s, ctypes.byref(m), ctypes.byref(n))
-        return {"mode": ("eager", "graph", "segmented")[m.value], "segments": n.value}
+        out = {"mode": ("eager", "graph", "segmented")[m.value], "segments": n.value}
+        if hasattr(self.lib, "gs_stepper_graph_steps"):  # (older builds for A/B runs: absent)
+            out["steps_per_launch"] = int(self.lib.gs_stepper_graph_steps(self._s))
+        return out
 
     def mem_info(self) -> dict:
         """HBM this rank's stepper holds, by buffer (bytes), from its allocation ledger (RCCL's

@@ -164,5 +164,7 @@ def test_bench_json_contract(hip, tmp_path):
     assert d["status"] == "ok" and d["work_audit"] == "ok", d.get("work_audit")
     assert d["audit"]["replay"] == "bitwise"
     assert "8 i x 2 j per lane" in d["config"]["kernel"]
+    # one-rank graph replays: 32 steps per launch at this size (and 2 for the remainder)
+    assert d["config"]["graph"] == "graph" and d["config"]["graph_steps_per_launch"] == 32
     assert 0.5 < d["engine_clock_ghz"] < 3.5 and 0.1 < d["cycles_per_pair_eval"] < 0.4, d
     assert abs(d["value"] - 65536 * 1e3 / d["ms_per_step"]) < 1e-6 * d["value"]
