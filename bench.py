@@ -342,6 +342,24 @@ def error_line(a, world: int, reason: str, records: list) -> dict:
                        "dt": a.dt, "ranks": records, "launch": launch_info()}}
 
 
+
+def check_topology(world: int, ranks_info: list, env, note=None) -> dict:
+    """What RCCL formed and what it runs over (parallel/verify.py): one GPU per rank, the whole
+    job in one communicator, no network transport inside one node. Returns the record for the
+    JSON line; raises SystemExit (the guard turns it into the error line, exit 70) when a
+    problem is found, except in the one-GPU rehearsal, which shares device 0 over sockets by
+    design (recorded, not enforced)."""
+    from gravsim.parallel import verify
+
+    problems = verify.topology_problems(world, ranks_info)
+    topology = {"enforced": not verify.rehearsal(env), "problems": problems,
+                **verify.transport_summary(ranks_info)}
+    if note:
+        note(topology)
+    if problems and topology["enforced"]:
+        raise SystemExit("multi-GPU topology check failed: " + "; ".join(problems))
+    return topology
+
 def main(argv=None) -> int:
     raw = list(sys.argv[1:] if argv is None else argv)
     a = parse(raw)
@@ -423,15 +441,7 @@ def run(a, g) -> int:
         rec = {"rank": rank, **device_record(dev), **eng.comm_info(),
                **rccl_transports(rccl_log)}
         ranks_info = comm.allgather_object(dist, rec)
-        # What RCCL formed and what it runs over (parallel/verify.py): one GPU per rank,
-        # the whole job in one communicator, no network transport inside one node. The
-        # one-GPU rehearsal shares device 0 over sockets by design: recorded, not enforced.
-        problems = verify.topology_problems(world, ranks_info)
-        topology = {"enforced": not verify.rehearsal(os.environ), "problems": problems,
-                    **verify.transport_summary(ranks_info)}
-        g.note(topology=topology)
-        if problems and topology["enforced"]:
-            raise SystemExit("multi-GPU topology check failed: " + "; ".join(problems))
+        topology = check_topology(world, ranks_info, os.environ, note=lambda t: g.note(topology=t))
 
     # One eager step from the ICs: its time bounds every later stage, and the native step
     # timeout becomes max(60 s, 20 x step), at most 240 s (a 16M / 8-rank step is ~5 s).

@@ -100,3 +100,21 @@ def test_unknown_communicator_fields_are_not_guessed(tmp_path):
     ranks = _ranks(tmp_path, 2, P2P_LOG, over={0: {"rccl_nranks": None, "rccl_rank": None,
                                                    "rccl_device": None}})
     assert verify.topology_problems(2, ranks) == []
+
+
+def test_bench_enforces_the_topology(tmp_path):
+    """bench.py's check_topology: a clean node passes and is recorded; a socket connection on
+    one node stops the run (SystemExit, which the guard reports as the error line); the
+    one-GPU rehearsal records the same problems without stopping."""
+    import pytest
+
+    import bench
+
+    seen = []
+    ok = bench.check_topology(2, _ranks(tmp_path, 2, P2P_LOG), {}, note=seen.append)
+    assert ok["enforced"] and ok["problems"] == [] and ok["p2p"] and seen == [ok]
+    bad = _ranks(tmp_path, 2, [P2P_LOG, SOCKET_LOG])
+    with pytest.raises(SystemExit, match="multi-GPU topology check failed: rank 1"):
+        bench.check_topology(2, bad, {})
+    rehearsal = bench.check_topology(2, bad, {"GRAVSIM_RCCL_RANK_HOSTS": "1"})
+    assert not rehearsal["enforced"] and len(rehearsal["problems"]) == 1
