@@ -400,7 +400,6 @@ def run(a, g) -> int:
     from gravsim.ops import _native
     from gravsim.parallel import comm
     from gravsim.parallel import guard as gd
-    from gravsim.parallel import verify
     from gravsim.runtime.engines import HipEngine
     from gravsim.runtime.simulation import conservation_summary, engine_conserved
 
