@@ -273,3 +273,25 @@ def test_host_step_timeout_beats_device_wait_bound(hip, monkeypatch):
         t0 = time.perf_counter()
         e.close()
         assert time.perf_counter() - t0 < 5.0  # the 1.8 s modeled gather, not a 10.6 s wait
+
+
+def test_per_link_exchange_price(hip, monkeypatch):
+    """GRAVSIM_EMU_LINKS=1 prices each exchange stage at its largest single peer's bytes (the
+    peers' xGMI links in parallel) instead of all of them through one pipe: at P = 7 (several
+    peers per stage) the modeled exchange is shorter; the all-gather's price does not change."""
+    out = {}
+    for links in ("0", "1"):
+        monkeypatch.setenv("GRAVSIM_EMU_LINKS", links)
+        e = _emu(monkeypatch, 262144, 7, 3, 8, 3)
+        e.init_ics("solar+random", 2)
+        e.step(2)
+        e.sync()
+        e.set_timing(True)
+        e.step(4)
+        out[links] = e.phase_stats()
+        e.set_timing(False)
+        e.close()
+    monkeypatch.delenv("GRAVSIM_EMU_LINKS", raising=False)
+    one, per = out["0"], out["1"]
+    assert per["exchange_ms"] < 0.8 * one["exchange_ms"], (one, per)
+    assert abs(per["gather_ms"] - one["gather_ms"]) < 0.1 * one["gather_ms"], (one, per)
